@@ -1,0 +1,211 @@
+"""bench.py -- log-likelihood evals/s of the HB light-curve path on MI355X.
+
+Workload (BASELINE.json configs[1]): a synthetic
+1024-cadence heartbeat-binary light curve, 4096 walkers per GPU.  One "step"
+= one batched log-likelihood over the rank's walkers (two launches: per-walker
+constants + the one-workgroup-per-walker model/median/chi^2 kernel), followed,
+when N > 1, by the RCCL all-gather of every walker's logL (what the tempering
+swap of mcmc_wrapper2.c:554-563 needs).  Inputs are resident in HBM before the
+timed region; the walker batches rotate over 4 pre-generated sets.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...
+
+Rank 0 prints ONE JSON line.  `value` = evals over all ranks / max-over-ranks
+wall time of the K timed steps.  `roofline` prices the dominant kernel
+(hb_eval_kernel) with algorithmic bytes B(N) = 24 N + 176 per eval (SURVEY.md
+8(d)) over its HIP-event-timed duration; `cpu_baseline` times the reference
+likelihood3.c (oracle/_ref, else the oracle port) on the host cores on a
+bounded sample of the same workload.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402  (import torch before libhbmi: one HIP runtime)
+import torch.distributed as dist  # noqa: E402
+
+from hb_mcmc_amd import synth  # noqa: E402
+from hb_mcmc_amd.likelihood import HBLikelihood  # noqa: E402
+
+METRIC = "log-likelihood evals/sec (walkers×steps/s), 1k-cadence HB light curve"
+HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md chip table (spec)
+FP64_PEAK_TFLOPS = 78.6    # MI355X fp64 vector (spec), SURVEY.md 8(d)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--walkers", type=int, default=4096, help="walkers per GPU")
+    ap.add_argument("--ncad", type=int, default=1024)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline sample length")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
+                    help="per-launch HBM bytes measured by rocprofv3 --pmc (see profiles/README.md)")
+    return ap.parse_args()
+
+
+def cpu_threads() -> int:
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    env = os.environ.get("OMP_NUM_THREADS")
+    if env and env.isdigit():
+        n = min(n, int(env))
+    return max(1, min(n, 64))
+
+
+def cpu_baseline(t, f, s, target_s):
+    """Reference likelihood3.c (oracle/_ref) or the oracle port, OpenMP over walkers."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as orc  # measurement infrastructure only (the checker)
+
+    kind = "reference" if (orc.reference_available()
+                           and os.path.exists(os.path.join(orc.REF_DIR, "libref_batch.so"))) else "port"
+    impl = orc.Reference() if kind == "reference" else orc.Oracle()
+    nth = cpu_threads()
+    mag, err = synth.MAG_DEFAULT, synth.MAGERR_DEFAULT
+    pilot = synth.walkers(8 * nth, seed=4242)
+    t0 = time.perf_counter()
+    impl.loglike_batch(t, f, s, pilot, mag, err, nth)
+    rate = len(pilot) / (time.perf_counter() - t0)
+    w = int(max(16 * nth, rate * target_s))
+    sample = synth.walkers(w, seed=4243)
+    t0 = time.perf_counter()
+    impl.loglike_batch(t, f, s, sample, mag, err, nth)
+    dt = time.perf_counter() - t0
+    one = sample[: max(8, int(rate / nth * 1.0))]  # ~1 s single-thread sample
+    t1 = time.perf_counter()
+    impl.loglike_batch(t, f, s, one, mag, err, 1)
+    dt1 = time.perf_counter() - t1
+    return {"value": w / dt, "unit": "evals/s", "cores": nth, "kind": kind,
+            "sample": f"{w} walkers x 1 eval, N={len(t)} cadences, {dt:.1f} s wall on {nth} threads "
+                      f"(OpenMP over walkers, mcmc_wrapper2.c:383 style)",
+            "value_1core": len(one) / dt1}
+
+
+def main():
+    a = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    # ---- synthetic workload (resident in HBM before timing) ----
+    n, w = a.ncad, a.walkers
+    t = synth.cadences(n)
+    with HBLikelihood(t, np.ones(n), np.ones(n), device=local) as tmp:
+        truth = tmp.light_curve(synth.THETA_STAR[None, :])[0]
+    s = np.full(n, 1e-3)
+    f = truth + s * synth.noise(n)
+    L = HBLikelihood(t, f, s, device=local)
+    L.reserve(w)
+    nb = 4
+    P_host = [synth.walkers(w, seed=1000 + 97 * rank + k) for k in range(nb)]
+    P = [torch.from_numpy(x).to(dev) for x in P_host]
+    out = torch.empty(w, dtype=torch.float64, device=dev)
+    gathered = torch.empty(world * w, dtype=torch.float64, device=dev)
+    stream = torch.cuda.current_stream()
+
+    def step(k, ev=None):
+        if ev is not None:
+            ev[0].record(stream)
+        L.prepare_dev(P[k % nb], stream)
+        if ev is not None:
+            ev[1].record(stream)
+        L.evaluate_dev(w, out, 0, stream)
+        if ev is not None:
+            ev[2].record(stream)
+        if world > 1:
+            dist.all_gather_into_tensor(gathered, out)
+
+    for k in range(a.warmup):
+        step(k)
+    torch.cuda.synchronize()
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(a.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(a.steps):
+        step(k, evs[k])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    wall = time.perf_counter() - t0
+    prep_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
+    eval_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in evs]))
+    if world > 1:
+        tt = torch.tensor([wall, eval_ms, prep_ms], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        wall, eval_ms, prep_ms = (float(x) for x in tt.tolist())
+    # sanity: finite walkers all produce finite logL, Roche ones the sentinel
+    lv = out.cpu().numpy()
+    assert np.isfinite(lv).all(), "non-finite logL in the bench workload"
+
+    if rank == 0:
+        evals = world * w * a.steps
+        value = evals / wall
+        bytes_per_eval = 24 * n + 176
+        achieved = bytes_per_eval * w / (eval_ms * 1e-3) / 1e9
+        traffic = None
+        if os.path.exists(a.traffic_json):
+            try:
+                tj = json.load(open(a.traffic_json))
+                key = f"N{n}_W{w}"
+                traffic = tj.get(key, {}).get("hbm_bytes_per_launch")
+            except Exception:
+                traffic = None
+        flops_conv = 600.0 * n  # SURVEY.md 8(d) counting convention
+        line = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "evals/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": wall / a.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (SURVEY.md 8(d): truth = test_likelihoods.c:33-36, t_i = 2P i/N, sigma 1e-3)",
+            "config": {"workload": f"C2: synthetic {n}-cadence HB light curve, {w} walkers per GPU",
+                       "ncad": n, "walkers_per_gpu": w, "global_walkers": world * w,
+                       "parallelism": f"walker-sharded x{world}, logL all-gather over RCCL" if world > 1
+                       else "single GPU",
+                       "evals_per_walker_step": 1,
+                       "note": "reference sampler spends 2 evals per walker-step (mcmc_wrapper2.c:488-489)"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "kernel": "hb_eval_kernel", "kernel_ms": eval_ms, "prep_kernel_ms": prep_ms,
+                         "bytes_per_eval": bytes_per_eval},
+            "fp64": {"achieved_tflops": flops_conv * w / (eval_ms * 1e-3) / 1e12, "peak_tflops": FP64_PEAK_TFLOPS,
+                     "frac": flops_conv * w / (eval_ms * 1e-3) / 1e12 / FP64_PEAK_TFLOPS,
+                     "convention": "600*N flop per eval (SURVEY.md 8(d)); fp64 VALU is the binding roof"},
+            "kernel_only_evals_per_s": w / ((eval_ms + prep_ms) * 1e-3),
+        }
+        if world == 1 and not a.no_cpu_baseline:
+            line["cpu_baseline"] = cpu_baseline(t, f, s, a.cpu_seconds)
+        print(json.dumps(line), flush=True)
+    L.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

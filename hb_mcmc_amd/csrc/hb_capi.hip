@@ -1,0 +1,532 @@
+// hb_capi.hip -- extern "C" entry points of libhbmi.so (include/hbmi.h).
+//
+// Part 1: drop-in replacements for the likelihood3.h symbols.  Every compute
+// entry point runs on the GPU; there is no CPU fallback.  With no usable HIP
+// device the drop-in entry points print a message and abort (they have no
+// error channel); the batched API returns a negative code instead.
+// Part 2: the batched context API (hb_create / hb_loglik_batch...).
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include <math.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "hb_device.hpp"
+#include "hb_internal.hpp"
+
+
+#include "../../include/hbmi.h"
+
+using hbdev::WalkerConst;
+using hbk::EvalPlan;
+using hbk::MagArgs;
+
+// ---------------------------------------------------------------------------
+// errors
+// ---------------------------------------------------------------------------
+static thread_local std::string g_err;
+
+static int set_err(const char* where, hipError_t e) {
+  g_err = std::string(where) + ": " + hipGetErrorString(e);
+  return -(int)(e == hipSuccess ? 1 : (int)e);
+}
+static int set_err_msg(const std::string& m, int code = -1) {
+  g_err = m;
+  return code;
+}
+
+#define HB_TRY(expr, where)                     \
+  do {                                          \
+    hipError_t _e = (expr);                     \
+    if (_e != hipSuccess) return set_err(where, _e); \
+  } while (0)
+
+[[noreturn]] static void hb_fatal(const char* what) {
+  fprintf(stderr, "libhbmi: fatal: %s (%s)\n", what, g_err.c_str());
+  fflush(stderr);
+  abort();
+}
+
+extern "C" const char* hb_last_error(void) { return g_err.c_str(); }
+
+extern "C" int hb_device_available(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n > 0 ? 1 : 0;
+}
+
+// ---------------------------------------------------------------------------
+// context
+// ---------------------------------------------------------------------------
+struct hb_ctx {
+  int device = 0;
+  EvalPlan plan;
+  MagArgs mags{};
+  double* d_t = nullptr;
+  double* d_f = nullptr;
+  double* d_s = nullptr;
+  // per-walker workspace
+  int cap = 0;
+  WalkerConst* d_wc = nullptr;
+  double* d_scratch = nullptr;   // cap x n (only when the template does not fit LDS)
+  // host-API staging
+  int hcap = 0;
+  size_t hout = 0;               // elements in d_out
+  double* d_params = nullptr;    // hcap x 21
+  double* d_out = nullptr;       // hcap x n (templates) or hcap (logL)
+  std::mutex mu;
+};
+
+static int ctx_release_ws(hb_ctx* c) {
+  if (c->d_wc) (void)hipFree(c->d_wc);
+  if (c->d_scratch) (void)hipFree(c->d_scratch);
+  c->d_wc = nullptr;
+  c->d_scratch = nullptr;
+  c->cap = 0;
+  return 0;
+}
+
+extern "C" int hb_reserve(hb_ctx* c, int max_walkers) {
+  if (!c) return set_err_msg("hb_reserve: null context");
+  if (max_walkers <= c->cap) return 0;
+  HB_TRY(hipSetDevice(c->device), "hipSetDevice");
+  ctx_release_ws(c);
+  HB_TRY(hipMalloc(&c->d_wc, sizeof(WalkerConst) * (size_t)max_walkers), "hipMalloc(walker consts)");
+  if (!c->plan.lds)
+    HB_TRY(hipMalloc(&c->d_scratch, sizeof(double) * (size_t)max_walkers * (size_t)c->plan.n),
+           "hipMalloc(template scratch)");
+  c->cap = max_walkers;
+  return 0;
+}
+
+static int ctx_host_staging(hb_ctx* c, int w, bool templates) {
+  const size_t out_elems = templates ? (size_t)w * (size_t)c->plan.n : (size_t)w;
+  if (w <= c->hcap && out_elems <= c->hout) return 0;
+  if (c->d_params) (void)hipFree(c->d_params);
+  if (c->d_out) (void)hipFree(c->d_out);
+  c->d_params = c->d_out = nullptr;
+  c->hcap = 0;
+  c->hout = 0;
+  HB_TRY(hipMalloc(&c->d_params, sizeof(double) * 21 * (size_t)w), "hipMalloc(params)");
+  HB_TRY(hipMalloc(&c->d_out, sizeof(double) * out_elems), "hipMalloc(out)");
+  c->hcap = w;
+  c->hout = out_elems;
+  return 0;
+}
+
+extern "C" hb_ctx* hb_create(const double* t, const double* f, const double* sigma, long n,
+                             const double* mag5, const double* magerr4, int device) {
+  if (n < 2) {
+    set_err_msg("hb_create: need N >= 2 cadences (the reference median reads out of bounds for N=1)");
+    return nullptr;
+  }
+  if (!t || !f || !sigma) {
+    set_err_msg("hb_create: null array");
+    return nullptr;
+  }
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
+    set_err_msg("hb_create: no HIP device available (libhbmi has no CPU fallback)");
+    return nullptr;
+  }
+  if (device < 0 || device >= ndev) {
+    set_err_msg("hb_create: device index out of range");
+    return nullptr;
+  }
+  std::unique_ptr<hb_ctx> c(new hb_ctx);
+  c->device = device;
+  c->plan = hbk::make_plan(n);
+  const double defmag[5] = {1000., 1., 1., 1., 1.};  // mcmc_wrapper2.c:321-327 fallback
+  const double deferr[4] = {1e15, 1e15, 1e15, 1e15};
+  for (int k = 0; k < 5; ++k) c->mags.mag[k] = mag5 ? mag5[k] : defmag[k];
+  for (int k = 0; k < 4; ++k) c->mags.magerr[k] = magerr4 ? magerr4[k] : deferr[k];
+
+  if (hipSetDevice(device) != hipSuccess) { set_err_msg("hb_create: hipSetDevice failed"); return nullptr; }
+  std::vector<double> s(sigma, sigma + n);
+  for (long i = 0; i < n; ++i)
+    if (s[i] < 1.e-5) s[i] = 1.e-5;  // likelihood3.c:824-827, applied once
+  const size_t bytes = sizeof(double) * (size_t)n;
+  if (hipMalloc(&c->d_t, bytes) != hipSuccess || hipMalloc(&c->d_f, bytes) != hipSuccess ||
+      hipMalloc(&c->d_s, bytes) != hipSuccess) {
+    set_err_msg("hb_create: hipMalloc failed");
+    hb_destroy(c.release());
+    return nullptr;
+  }
+  if (hipMemcpy(c->d_t, t, bytes, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(c->d_f, f, bytes, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(c->d_s, s.data(), bytes, hipMemcpyHostToDevice) != hipSuccess) {
+    set_err_msg("hb_create: upload failed");
+    hb_destroy(c.release());
+    return nullptr;
+  }
+  return c.release();
+}
+
+extern "C" void hb_destroy(hb_ctx* c) {
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  ctx_release_ws(c);
+  if (c->d_params) (void)hipFree(c->d_params);
+  if (c->d_out) (void)hipFree(c->d_out);
+  if (c->d_t) (void)hipFree(c->d_t);
+  if (c->d_f) (void)hipFree(c->d_f);
+  if (c->d_s) (void)hipFree(c->d_s);
+  delete c;
+}
+
+extern "C" long hb_ctx_ncad(const hb_ctx* c) { return c ? c->plan.n : -1; }
+extern "C" int hb_ctx_waves_per_walker(const hb_ctx* c) { return c ? c->plan.nw : -1; }
+extern "C" int hb_ctx_template_in_lds(const hb_ctx* c) { return c ? (c->plan.lds ? 1 : 0) : -1; }
+
+static int run_batch(hb_ctx* c, const double* d_params, int w, double* d_logl, double* d_tmpl,
+                     hipStream_t s) {
+  if (!c) return set_err_msg("null context");
+  if (w < 0) return set_err_msg("negative walker count");
+  if (w == 0) return 0;
+  if (!d_params || (!d_logl && !d_tmpl)) return set_err_msg("null pointer");
+  HB_TRY(hipSetDevice(c->device), "hipSetDevice");
+  if (w > c->cap) {
+    int rc = hb_reserve(c, w);
+    if (rc) return rc;
+  }
+  HB_TRY(hbk::launch_prep(d_params, w, c->mags, c->d_wc, s), "hb_prep_kernel");
+  HB_TRY(hbk::launch_eval(c->plan, c->d_t, c->d_f, c->d_s, c->d_wc, w, d_logl, d_tmpl, c->d_scratch,
+                          d_tmpl ? 1 : 0, s),
+         "hb_eval_kernel");
+  return 0;
+}
+
+extern "C" int hb_prepare_dev(hb_ctx* c, const double* d_params, int w, void* stream) {
+  if (!c) return set_err_msg("null context");
+  if (w <= 0) return w == 0 ? 0 : set_err_msg("negative walker count");
+  HB_TRY(hipSetDevice(c->device), "hipSetDevice");
+  if (w > c->cap) {
+    int rc = hb_reserve(c, w);
+    if (rc) return rc;
+  }
+  HB_TRY(hbk::launch_prep(d_params, w, c->mags, c->d_wc, (hipStream_t)stream), "hb_prep_kernel");
+  return 0;
+}
+
+extern "C" int hb_evaluate_dev(hb_ctx* c, int w, double* d_out, int mode, void* stream) {
+  if (!c) return set_err_msg("null context");
+  if (w <= 0) return w == 0 ? 0 : set_err_msg("negative walker count");
+  if (w > c->cap) return set_err_msg("hb_evaluate_dev: W exceeds the prepared workspace");
+  if (mode != 0 && mode != 1) return set_err_msg("hb_evaluate_dev: mode must be 0 or 1");
+  HB_TRY(hipSetDevice(c->device), "hipSetDevice");
+  HB_TRY(hbk::launch_eval(c->plan, c->d_t, c->d_f, c->d_s, c->d_wc, w, mode == 0 ? d_out : nullptr,
+                          mode == 1 ? d_out : nullptr, c->d_scratch, mode, (hipStream_t)stream),
+         "hb_eval_kernel");
+  return 0;
+}
+
+extern "C" int hb_loglik_batch_dev(hb_ctx* c, const double* d_params, int w, double* d_logl,
+                                   void* stream) {
+  return run_batch(c, d_params, w, d_logl, nullptr, (hipStream_t)stream);
+}
+
+extern "C" int hb_light_curve_batch_dev(hb_ctx* c, const double* d_params, int w, double* d_out,
+                                        void* stream) {
+  return run_batch(c, d_params, w, nullptr, d_out, (hipStream_t)stream);
+}
+
+static int host_batch(hb_ctx* c, const double* params, int w, double* out, void* stream, bool tmpl) {
+  if (!c) return set_err_msg("null context");
+  if (w <= 0) return w == 0 ? 0 : set_err_msg("negative walker count");
+  std::lock_guard<std::mutex> lk(c->mu);
+  HB_TRY(hipSetDevice(c->device), "hipSetDevice");
+  int rc = ctx_host_staging(c, w, tmpl);
+  if (rc) return rc;
+  hipStream_t s = (hipStream_t)stream;
+  const size_t nout = tmpl ? (size_t)w * (size_t)c->plan.n : (size_t)w;
+  HB_TRY(hipMemcpyAsync(c->d_params, params, sizeof(double) * 21 * (size_t)w, hipMemcpyHostToDevice, s),
+         "upload params");
+  rc = run_batch(c, c->d_params, w, tmpl ? nullptr : c->d_out, tmpl ? c->d_out : nullptr, s);
+  if (rc) return rc;
+  HB_TRY(hipMemcpyAsync(out, c->d_out, sizeof(double) * nout, hipMemcpyDeviceToHost, s), "download");
+  HB_TRY(hipStreamSynchronize(s), "hipStreamSynchronize");
+  return 0;
+}
+
+extern "C" int hb_loglik_batch(hb_ctx* c, const double* params, int w, double* logl, void* stream) {
+  return host_batch(c, params, w, logl, stream, false);
+}
+extern "C" int hb_light_curve_batch(hb_ctx* c, const double* params, int w, double* out, void* stream) {
+  return host_batch(c, params, w, out, stream, true);
+}
+
+// ===========================================================================
+// Part 1: likelihood3.h drop-in
+// ===========================================================================
+namespace {
+
+void require_device() {
+  if (!hb_device_available()) {
+    g_err = "no HIP device";
+    hb_fatal("likelihood3 entry point called without a usable GPU");
+  }
+}
+
+uint64_t mix64(uint64_t h, uint64_t v) {
+  h ^= v + 0x9e3779b97f4a7c15ull + (h << 6) + (h >> 2);
+  h *= 0xbf58476d1ce4e5b9ull;
+  return h ^ (h >> 31);
+}
+uint64_t hash_doubles(uint64_t h, const double* a, long n) {
+  for (long i = 0; i < n; ++i) {
+    uint64_t v;
+    memcpy(&v, a + i, 8);
+    h = mix64(h, v);
+  }
+  return mix64(h, (uint64_t)n);
+}
+
+// Per-thread cache of resident light curves: the reference sampler calls
+// loglikelihood() with the same arrays every step from each OpenMP thread.
+struct CacheEnt {
+  uint64_t key;
+  hb_ctx* ctx;
+};
+struct ThreadCache {
+  std::vector<CacheEnt> ents;
+  ~ThreadCache() {
+    for (auto& e : ents) hb_destroy(e.ctx);
+  }
+  hb_ctx* get(uint64_t key) {
+    for (size_t i = 0; i < ents.size(); ++i)
+      if (ents[i].key == key) {
+        CacheEnt e = ents[i];
+        ents.erase(ents.begin() + i);
+        ents.push_back(e);
+        return e.ctx;
+      }
+    return nullptr;
+  }
+  void put(uint64_t key, hb_ctx* c) {
+    if (ents.size() >= 4) {
+      hb_destroy(ents.front().ctx);
+      ents.erase(ents.begin());
+    }
+    ents.push_back({key, c});
+  }
+};
+thread_local ThreadCache t_cache;
+
+struct DevBuf {
+  double* p = nullptr;
+  size_t cap = 0;
+  ~DevBuf() {
+    if (p) (void)hipFree(p);
+  }
+  double* get(size_t n) {
+    if (n > cap) {
+      if (p) (void)hipFree(p);
+      p = nullptr;
+      cap = 0;
+      if (hipMalloc(&p, n * sizeof(double)) != hipSuccess) hb_fatal("hipMalloc failed");
+      cap = n;
+    }
+    return p;
+  }
+};
+thread_local DevBuf t_buf_a, t_buf_b;
+
+double probe(int op, const double* in, int nin, double* out, int nout) {
+  require_device();
+  double* d_in = t_buf_a.get(32);
+  double* d_out = t_buf_b.get(8);
+  if (hipMemcpy(d_in, in, sizeof(double) * nin, hipMemcpyHostToDevice) != hipSuccess) hb_fatal("upload");
+  if (hbk::launch_probe(op, d_in, d_out, nullptr) != hipSuccess) hb_fatal("probe launch");
+  double tmp[8];
+  if (hipMemcpy(tmp, d_out, sizeof(double) * nout, hipMemcpyDeviceToHost) != hipSuccess) hb_fatal("download");
+  if (out) memcpy(out, tmp, sizeof(double) * nout);
+  return tmp[0];
+}
+
+hb_ctx* cached_ctx(const double* t, const double* f, const double* s, long n, const double* mag,
+                   const double* err) {
+  uint64_t key = hash_doubles(0x5eed, t, n);
+  key = hash_doubles(key, f, n);
+  key = hash_doubles(key, s, n);
+  key = hash_doubles(key, mag, 5);
+  key = hash_doubles(key, err, 4);
+  hb_ctx* c = t_cache.get(key);
+  if (!c) {
+    c = hb_create(t, f, s, n, mag, err, 0);
+    if (!c) hb_fatal("hb_create failed");
+    t_cache.put(key, c);
+  }
+  return c;
+}
+
+}  // namespace
+
+extern "C" double loglikelihood(double time[], double lightcurve[], double noise[], long N,
+                                double params[], double mag_data[], double magerr[]) {
+  require_device();
+  // caller-visible side effect of the reference (likelihood3.c:824-827)
+  for (long i = 0; i < N; ++i)
+    if (noise[i] < 1.e-5) noise[i] = 1.e-5;
+  hb_ctx* c = cached_ctx(time, lightcurve, noise, N, mag_data, magerr);
+  double out = 0.0;
+  if (hb_loglik_batch(c, params, 1, &out, nullptr) != 0) hb_fatal("hb_loglik_batch failed");
+  return out;
+}
+
+extern "C" void calc_light_curve(double* times, long Nt, double* pars, double* tmpl) {
+  require_device();
+  std::vector<double> zeros((size_t)Nt, 0.0), ones((size_t)Nt, 1.0);
+  const double mag[5] = {1000., 1., 1., 1., 1.}, err[4] = {1e15, 1e15, 1e15, 1e15};
+  hb_ctx* c = cached_ctx(times, zeros.data(), ones.data(), Nt, mag, err);
+  if (hb_light_curve_batch(c, pars, 1, tmpl, nullptr) != 0) hb_fatal("hb_light_curve_batch failed");
+}
+
+extern "C" void traj(double* times, double* tp, double* d_arr, double* Z1_arr, double* Z2_arr,
+                     double* rr_arr, double* ff_arr, int Nt) {
+  require_device();
+  if (Nt <= 0) return;
+  // host-side packing of the 7 orbit scalars (likelihood3.c:128-142)
+  double mA = tp[0], mB = tp[1];
+  if (mB > mA) { const double k = mA; mA = mB; mB = k; }
+  const double msum = mA + mB;
+  hbk::TrajArgs ta;
+  memset(&ta, 0, sizeof(ta));
+  const double e = tp[3];
+  ta.w.Pc = tp[2];
+  ta.w.T0c = tp[6];
+  ta.w.e = e;
+  ta.w.e085 = 0.85 * e;
+  ta.w.sq1me2 = sqrt(1.0 - e * e);
+  ta.w.inv1me2 = 1.0 / (1.0 - e * e);
+  ta.w.cw = cos(tp[5]);
+  ta.w.sw = sin(tp[5]);
+  ta.w.ci = cos(tp[4]);
+  ta.w.si = sin(tp[4]);
+  ta.w.aR = pow(hbdev::kG * msum * (tp[2] * tp[2]) / (hbdev::kTwoPi * hbdev::kTwoPi), 1. / 3.);
+  ta.fz1 = mB / msum;
+  ta.fz2 = mA / msum;
+  const size_t n = (size_t)Nt;
+  double* d_t = t_buf_a.get(n);
+  double* d_o = t_buf_b.get(5 * n);
+  if (hipMemcpy(d_t, times, n * 8, hipMemcpyHostToDevice) != hipSuccess) hb_fatal("traj upload");
+  if (hbk::launch_traj(d_t, Nt, ta, d_o, d_o + n, d_o + 2 * n, d_o + 3 * n, d_o + 4 * n, nullptr) !=
+      hipSuccess)
+    hb_fatal("traj launch");
+  std::vector<double> h(5 * n);
+  if (hipMemcpy(h.data(), d_o, 5 * n * 8, hipMemcpyDeviceToHost) != hipSuccess) hb_fatal("traj download");
+  memcpy(d_arr, h.data(), n * 8);
+  memcpy(Z1_arr, h.data() + n, n * 8);
+  memcpy(Z2_arr, h.data() + 2 * n, n * 8);
+  memcpy(rr_arr, h.data() + 3 * n, n * 8);
+  memcpy(ff_arr, h.data() + 4 * n, n * 8);
+}
+
+extern "C" double get_alpha_beam(double logT) { return probe(hbk::kOpAlphaBeam, &logT, 1, nullptr, 1); }
+
+extern "C" double beaming(double P, double M1, double M2, double e, double inc, double omega0, double nu,
+                          double alpha_beam) {
+  const double in[8] = {P, M1, M2, e, inc, omega0, nu, alpha_beam};
+  return probe(hbk::kOpBeaming, in, 8, nullptr, 1);
+}
+
+extern "C" double ellipsoidal(double P, double M1, double M2, double e, double inc, double omega0,
+                              double nu, double R1, double a, double mu, double tau) {
+  const double in[11] = {P, M1, M2, e, inc, omega0, nu, R1, a, mu, tau};
+  return probe(hbk::kOpEllipsoidal, in, 11, nullptr, 1);
+}
+
+extern "C" double reflection(double P, double M1, double M2, double e, double inc, double omega0,
+                             double nu, double R2, double alpha_ref1) {
+  const double in[9] = {P, M1, M2, e, inc, omega0, nu, R2, alpha_ref1};
+  return probe(hbk::kOpReflection, in, 9, nullptr, 1);
+}
+
+extern "C" double eclipse_area(double R1, double R2, double d) {
+  const double in[3] = {R1, R2, d};
+  return probe(hbk::kOpEclipse, in, 3, nullptr, 1);
+}
+
+extern "C" double _getT(double logM) { return probe(hbk::kOpGetT, &logM, 1, nullptr, 1); }
+extern "C" double _getR(double logM) { return probe(hbk::kOpGetR, &logM, 1, nullptr, 1); }
+extern "C" double envelope_Temp(double logM) { return probe(hbk::kOpEnvT, &logM, 1, nullptr, 1); }
+extern "C" double envelope_Radius(double logM) { return probe(hbk::kOpEnvR, &logM, 1, nullptr, 1); }
+extern "C" double Eggleton_RL(double q) { return probe(hbk::kOpEggleton, &q, 1, nullptr, 1); }
+
+extern "C" void calc_radii_and_Teffs(double params[], double* R1, double* R2, double* Teff1,
+                                     double* Teff2) {
+  double o[4];
+  probe(hbk::kOpRadiiTeffs, params, 21, o, 4);
+  *R1 = o[0];
+  *R2 = o[1];
+  *Teff1 = o[2];
+  *Teff2 = o[3];
+}
+
+extern "C" void calc_mags(double params[], double D, double* Gmg, double* BminusV, double* VminusG,
+                          double* GminusT) {
+  double in[22];
+  memcpy(in, params, 21 * sizeof(double));
+  in[21] = D;
+  double o[4];
+  probe(hbk::kOpMags, in, 22, o, 4);
+  *Gmg = o[0];
+  *BminusV = o[1];
+  *VminusG = o[2];
+  *GminusT = o[3];
+}
+
+extern "C" int RocheOverflow(double* pars) {
+  return probe(hbk::kOpRoche, pars, 21, nullptr, 1) != 0.0 ? 1 : 0;
+}
+
+extern "C" void remove_median(double* arr, long begin, long end) {
+  require_device();
+  const long n = end - begin;
+  if (n < 2) {
+    g_err = "remove_median: n < 2 (the reference reads out of bounds)";
+    return;
+  }
+  double* d = t_buf_a.get((size_t)n);
+  if (hipMemcpy(d, arr + begin, n * 8, hipMemcpyHostToDevice) != hipSuccess) hb_fatal("upload");
+  const long kth = (n % 2 == 0) ? n / 2 : n / 2 + 1;
+  if (hbk::launch_median(d, n, kth, nullptr) != hipSuccess) hb_fatal("median launch");
+  if (hipMemcpy(arr + begin, d, n * 8, hipMemcpyDeviceToHost) != hipSuccess) hb_fatal("download");
+}
+
+extern "C" void quickSort(double arr[], int low, int high) {
+  require_device();
+  if (low >= high) return;
+  const int n = high - low + 1;
+  double* d_in = t_buf_a.get((size_t)n);
+  double* d_out = t_buf_b.get((size_t)n);
+  if (hipMemcpy(d_in, arr + low, (size_t)n * 8, hipMemcpyHostToDevice) != hipSuccess) hb_fatal("upload");
+  size_t tmp_bytes = 0;
+  (void)hipcub::DeviceRadixSort::SortKeys(nullptr, tmp_bytes, d_in, d_out, n);
+  void* d_tmp = nullptr;
+  if (hipMalloc(&d_tmp, tmp_bytes > 0 ? tmp_bytes : 16) != hipSuccess) hb_fatal("hipMalloc(sort tmp)");
+  if (hipcub::DeviceRadixSort::SortKeys(d_tmp, tmp_bytes, d_in, d_out, n) != hipSuccess) hb_fatal("sort");
+  if (hipMemcpy(arr + low, d_out, (size_t)n * 8, hipMemcpyDeviceToHost) != hipSuccess) hb_fatal("download");
+  (void)hipFree(d_tmp);
+}
+
+extern "C" double partition(double arr[], int low, int high) {
+  require_device();
+  if (high < low) return (double)low;
+  const int n = high - low + 1;
+  double* d = t_buf_a.get((size_t)n + 1);
+  int* d_res = reinterpret_cast<int*>(t_buf_b.get(1));
+  if (hipMemcpy(d, arr + low, (size_t)n * 8, hipMemcpyHostToDevice) != hipSuccess) hb_fatal("upload");
+  if (hbk::launch_partition(d, 0, n - 1, d_res, nullptr) != hipSuccess) hb_fatal("partition launch");
+  int res = 0;
+  if (hipMemcpy(arr + low, d, (size_t)n * 8, hipMemcpyDeviceToHost) != hipSuccess) hb_fatal("download");
+  if (hipMemcpy(&res, d_res, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess) hb_fatal("download");
+  return (double)(res + low);
+}

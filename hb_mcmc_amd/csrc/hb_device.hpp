@@ -1,0 +1,421 @@
+// hb_device.hpp -- device-side heartbeat-binary model for gfx950 (CDNA4).
+//
+// The reference evaluates, per walker and per cadence, ~120 libm calls
+// (likelihood3.c:125-185 traj, :224-389 beaming/ellipsoidal/reflection/
+// eclipse).  Almost all of them depend only on the walker's 21 parameters, so
+// this file splits the model in two:
+//
+//   hb_prepare_walker()  -- once per walker: every mass/period/radius power,
+//                           stellar tables, flux normalisation, beaming
+//                           coefficients, the Gaia-G chi^2 term and the Roche
+//                           flag, folded into one WalkerConst record.
+//   hb_cadence_flux()    -- once per (walker, cadence): Kepler solve (5 Newton
+//                           steps, exactly like likelihood3.c:160), true
+//                           anomaly by the cos/sin form (no tan/atan), the
+//                           2x3 photometric terms as a polynomial in
+//                           beta = (1+e cos nu)/(1-e^2) and in the angle
+//                           multiples of u = omega0+nu, and the eclipse.
+//
+// Arithmetic is fp64 throughout.  Results agree with the reference to a few
+// ulp per cadence; the parity tolerance (1e-10 relative on logL) is stated in
+// tests/test_gpu_parity.py.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace hbdev {
+
+// physical constants, likelihood3.h:4-10
+constexpr double kPi = 3.14159265358979323846;
+constexpr double kTwoPi = 2.0 * 3.14159265358979323846;  // == 2*PI as a double
+constexpr double kG = 6.6743e-8;
+constexpr double kC = 2.998e10;
+constexpr double kMsun = 1.9885e33;
+constexpr double kRsun = 6.955e10;
+constexpr double kDay = 86400.0;
+constexpr double kBig = 1.e15;
+constexpr int kNpars = 21;
+
+// Per-walker record.  40 doubles = 320 B; read by the cadence kernel with
+// wave-uniform (scalar) loads.
+struct alignas(16) WalkerConst {
+  // orbit (traj, likelihood3.c:125-185)
+  double T0c;      // T0 [s]
+  double Pc;       // P [s]
+  double e;
+  double e085;     // 0.85*e (initial Kepler guess, :157)
+  double sq1me2;   // sqrt(1-e^2)
+  double inv1me2;  // 1/(1-e^2)
+  double cw, sw;   // cos/sin omega0
+  double ci, si;   // cos/sin inc
+  double aR;       // semi-major axis (traj's a) in Rsun
+  // light-curve polynomial coefficients (both stars, Norm-weighted)
+  double kconst;   // Norm1 + Norm2 + constant ellipsoidal term
+  double kb;       // x cos u               (beaming)
+  double kr0, kr2, krs;          // x beta^2 (1, cos2u, sin u)   (reflection)
+  double kam2, kc21;             // x beta^3 (1, cos2u)
+  double ks1, ks3;               // x beta^4 (sin u, sin3u)
+  double kam3, kc22, kc4;        // x beta^5 (1, cos2u, cos4u)
+  // eclipse (eclipse_area, :353-389); radii in Rsun, ordered big/small
+  double ecl1, ecl2;             // Norm_k / (pi R_k^2)
+  double rbig, rsml;             // unswapped R1, R2 are kept below
+  double dcrit;                  // sqrt(Rbig^2 - Rsml^2)
+  double r1, r2;
+  // normalisation and scalar chi^2 pieces
+  double blend, tune;
+  double chi2_extra;             // ((Gmag - G_obs)/sigma_G)^2 (USE_GMAG=1)
+  double roche;                  // 1.0 if RocheOverflow(), else 0.0
+  double pad[6];
+};
+static_assert(sizeof(WalkerConst) == 40 * 8, "WalkerConst layout");
+
+// ------------------------------------------------------------------------
+// small helpers
+// ------------------------------------------------------------------------
+__device__ __forceinline__ double sq(double x) { return x * x; }
+
+// exact fmod(x, 2*PI) (fmod's result is always representable; fma with the
+// right integer quotient reproduces it exactly).  Falls back to the libm
+// routine for |x/2pi| >= 2^50, which folded light curves never reach.
+__device__ __forceinline__ double fmod_twopi(double x) {
+  const double y = kTwoPi;
+  double q = trunc(x / y);
+  if (!(fabs(q) < 1125899906842624.0)) return fmod(x, y);  // 2^50 (also NaN/inf)
+  double r = fma(-q, y, x);
+  if (x >= 0.0) {
+    if (r < 0.0) { q -= 1.0; r = fma(-q, y, x); }
+    else if (r >= y) { q += 1.0; r = fma(-q, y, x); }
+  } else {
+    if (r > 0.0) { q += 1.0; r = fma(-q, y, x); }
+    else if (r <= -y) { q -= 1.0; r = fma(-q, y, x); }
+  }
+  if (r == 0.0) r = copysign(0.0, x);
+  return r;
+}
+
+// sign(sin(M)) for M = fmod(., 2*PI) in (-2PI_d, 2PI_d), without a sine.
+// PI_d < pi < nextafter(PI_d), so sin(M) > 0 exactly on (0, PI_d] and on
+// (-2PI_d, -PI_d) (likelihood3.c:155-157 only uses the sign).
+__device__ __forceinline__ double sign_sin_reduced(double m) {
+  if (m == 0.0) return 0.0;
+  if (m > 0.0) return (m <= kPi) ? 1.0 : -1.0;
+  return (m < -kPi) ? 1.0 : -1.0;
+}
+
+// order-preserving uint64 key of a double (non-NaN)
+__device__ __forceinline__ uint64_t dkey(double v) {
+  uint64_t b = (uint64_t)__double_as_longlong(v);
+  return (b & 0x8000000000000000ull) ? ~b : (b | 0x8000000000000000ull);
+}
+__device__ __forceinline__ double dval(uint64_t k) {
+  uint64_t b = (k & 0x8000000000000000ull) ? (k & 0x7fffffffffffffffull) : ~k;
+  return __longlong_as_double((long long)b);
+}
+
+// ------------------------------------------------------------------------
+// stellar tables (likelihood3.c:396-507); m is the linear mass in Msun
+// ------------------------------------------------------------------------
+__device__ __forceinline__ double logteff_of_mass(double m) {
+  const double mn[16] = {0.1, 0.26, 0.47, 0.59, 0.69, 0.87, 0.98, 1.085,
+                         1.4, 1.65, 2.0,  2.5,  3.0,  4.4,  15., 40.};
+  const double tn[16] = {3.491, 3.531, 3.547, 3.584, 3.644, 3.712, 3.745, 3.774,
+                         3.823, 3.863, 3.913, 3.991, 4.057, 4.182, 4.477, 4.623};
+  if (m <= mn[0]) return tn[0];
+  if (m >= mn[15]) return tn[15];
+  double out = 0.0;
+#pragma unroll
+  for (int k = 15; k >= 1; --k)  // first node with m < mn[k], scanning up
+    if (m < mn[k]) out = tn[k - 1] + (m - mn[k - 1]) * (tn[k] - tn[k - 1]) / (mn[k] - mn[k - 1]);
+  return out;
+}
+
+__device__ __forceinline__ double logradius_of_mass(double m) {
+  const double mn[10] = {0.07, 0.2, 0.356, 0.655, 0.784, 0.787, 1.377, 4.4, 15., 40.};
+  const double rn[10] = {-0.953, -0.627, -0.423, -0.154, -0.082, -0.087, 0.295, 0.477, 0.792, 1.041};
+  if (m <= mn[0]) return rn[0];
+  if (m >= mn[9]) return rn[9];
+  double out = __builtin_nan("");
+#pragma unroll
+  for (int k = 9; k >= 1; --k)
+    if (m < mn[k]) out = rn[k - 1] + (m - mn[k - 1]) * (rn[k] - rn[k - 1]) / (mn[k] - mn[k - 1]);
+  return out;
+}
+
+__device__ __forceinline__ double teff_spread() { return 0.0224; }  // envelope_Temp
+
+__device__ __forceinline__ double radius_spread_of_mass(double m) {  // envelope_Radius
+  const double ex = 4.22, sl = 15.68, lo = 0.01, knee = 1.055, hi = 0.17;
+  return 1.0 / (1.0 / hi + 1.0 / (sl * pow(pow(m, ex) + pow(knee, ex), 1.0 / ex) - (sl * knee - lo)));
+}
+
+// get_alpha_beam (likelihood3.c:194-209)
+__device__ __forceinline__ double beam_coeff(double lt) {
+  if (lt >= 4.5) return 1.2 / 4;
+  if (lt < 3.5) return 6.5 / 4;
+  double a0, a1, l0, l1;
+  if (lt >= 3.9) { a0 = 2.5; a1 = 1.2; l0 = 3.9; l1 = 4.5; }
+  else if (lt >= 3.7) { a0 = 4.0; a1 = 2.5; l0 = 3.7; l1 = 3.9; }
+  else { a0 = 6.5; a1 = 4.0; l0 = 3.5; l1 = 3.7; }
+  return (a1 + (a1 - a0) / (l1 - l0) * (lt - l1)) / 4;
+}
+
+// Stellar parameters from the 21-slot vector (calc_radii_and_Teffs).
+struct Stellar {
+  double m1, m2;          // Msun
+  double r1, r2;          // Rsun
+  double lt1, lt2;        // log10 Teff
+  double t1, t2;          // K
+};
+__device__ __forceinline__ Stellar stellar_of(const double* p) {
+  Stellar s;
+  s.m1 = exp10(p[0]);
+  s.m2 = exp10(p[1]);
+  s.r1 = exp10(logradius_of_mass(s.m1) + p[7] * radius_spread_of_mass(s.m1));
+  s.r2 = exp10(logradius_of_mass(s.m2) + p[8] * radius_spread_of_mass(s.m2));
+  s.lt1 = logteff_of_mass(s.m1) + p[17] * teff_spread();
+  s.lt2 = logteff_of_mass(s.m2) + p[18] * teff_spread();
+  s.t1 = exp10(s.lt1);
+  s.t2 = exp10(s.lt2);
+  return s;
+}
+
+// Gaia-band (673 nm) magnitude of both stars (calc_mags, :725-795) and the
+// full 4-band version for the C-ABI.  R in Rsun, T in K, dist in pc.
+__device__ __forceinline__ double band_flux(double lam_nm, double r1cm, double r2cm, double t1,
+                                            double t2, double dist, double blend) {
+  const double hp = 6.626e-27, kb = 1.38e-16, pc = 3.086e18;
+  double fr = kC / (lam_nm * 1e-7);
+  double pre = 2.0 * hp * (fr * fr * fr) / (kC * kC);
+  double f = kPi * (r1cm * r1cm * (pre / (exp(hp * fr / (kb * t1)) - 1.0)) +
+                    r2cm * r2cm * (pre / (exp(hp * fr / (kb * t2)) - 1.0))) /
+             ((dist * dist) * (pc * pc));
+  return f / (1.0 - blend);
+}
+__device__ __forceinline__ double ab_mag(double f) { return -2.5 * log10(f) - 48.6; }
+
+// Eggleton 1983 Roche-lobe radius over separation (likelihood3.c:945-948)
+__device__ __forceinline__ double lobe_fraction(double q) {
+  double c = cbrt(q);
+  double c2 = c * c;
+  return 0.49 * c2 / (0.6 * c2 + log(1.0 + c));
+}
+
+// ------------------------------------------------------------------------
+// per-star photometric coefficients (beaming :224-236, ellipsoidal :255-307,
+// reflection :322-337) with every cadence-independent factor hoisted:
+//   beaming     = kb * cos u
+//   ellipsoidal = am1 + b^3 (am2 + c21 cos2u) + b^4 (s1 sin u + s3 sin3u)
+//                     + b^5 (am3 + c22 cos2u + c4 cos4u)
+//   reflection  = kref * b^2 * (0.64 - sin i sin u + 0.18 sin^2 i (1 - cos2u))
+// with b = (1 + e cos nu)/(1 - e^2) and u = omega + nu.
+// ------------------------------------------------------------------------
+struct StarCoef {
+  double kb, am1, am2, c21, am3, c22, c4, s1, s3, kref;
+};
+
+__device__ __forceinline__ StarCoef star_coef(double pd, double ma, double mb, double e, double si,
+                                              double rk, double rc, double mu, double tau,
+                                              double aref, double ab) {
+  const double ppm = 1.e-6;
+  const double s2 = si * si, s3 = s2 * si, s4 = s3 * si;
+  const double cP = cbrt(pd);
+  const double inv_pd = 1.0 / pd;
+  const double omE = 1.0 - e;
+  const double prot = pd * (omE * sqrt(omE));  // P (1-e)^{3/2}
+  const double q = mb / ma;
+  const double opq = 1.0 + q;
+  const double cM = cbrt(ma);
+  const double cq = cbrt(opq);
+  const double inv_ma = 1.0 / ma;
+  StarCoef c;
+  // beaming: pow(1+q, 2/3) is integer 2/3 == 0 in the reference -> factor 1
+  c.kb = -2830. * ab * q * cM / cP * si / sqrt(1.0 - e * e) * ppm;
+  const double a11 = 15 * mu * (2 + tau) / (32 * (3 - mu));
+  const double a21 = 3 * (15 + mu) * (1 + tau) / (20 * (3 - mu));
+  const double a2b = 15 * (1 - mu) * (3 + tau) / (64 * (3 - mu));
+  const double a01 = a21 / 9, a0b = 3 * a2b / 20, a31 = 5 * a11 / 3, a41 = 7 * a2b / 4;
+  const double qq = q / opq;
+  const double rk3 = rk * rk * rk;
+  c.am1 = 26870 * a01 * (2 - 3 * s2) * inv_ma / (prot * prot) * rk3 * ppm;
+  c.am2 = 40305 * a01 * (2 - 3 * s2) * inv_ma * qq * (inv_pd * inv_pd) * rk3 * ppm;
+  c.c21 = 13435 * a21 * s2 * inv_ma * qq * (inv_pd * inv_pd) * rk3 * ppm;
+  // M^-5/3 q/(1+q)^5/3 P^-10/3 R^5
+  const double c5 = qq / (cq * cq) * inv_ma / (cM * cM) * (inv_pd * inv_pd * inv_pd) / cP *
+                    (rk3 * rk * rk) * ppm;
+  c.am3 = 759 * a0b * (8 - 40 * s2 + 35 * s4) * c5;
+  c.c22 = 759 * a2b * (6 * s2 - 7 * s4) * c5;
+  c.c4 = 759 * a41 * s4 * c5;
+  // M^-4/3 q/(1+q)^4/3 P^-8/3 R^4
+  const double c4c = qq / cq * inv_ma / cM * (inv_pd * inv_pd) / (cP * cP) * (rk3 * rk) * ppm;
+  c.s1 = 3194 * a11 * (4 * si - 5 * s3) * c4c;
+  c.s3 = 3194 * a31 * s3 * c4c;
+  // reflection: (1+q)^-2/3 M^-2/3 P^-4/3 Rc^2
+  c.kref = 56514 * aref / (cq * cq) / (cM * cM) * inv_pd / cP * (rc * rc) * ppm;
+  return c;
+}
+
+// ------------------------------------------------------------------------
+// per-walker preparation
+// ------------------------------------------------------------------------
+__device__ inline void hb_prepare_walker(const double* __restrict__ p, const double* __restrict__ mag,
+                                         const double* __restrict__ magerr, WalkerConst& w) {
+  const double pd = exp10(p[2]);          // period [d]
+  const double e = p[3], inc = p[4], om = p[5];
+  const Stellar st = stellar_of(p);
+  const double m1 = st.m1, m2 = st.m2;
+
+  // orbit
+  w.Pc = pd * kDay;
+  w.T0c = p[6] * kDay;
+  w.e = e;
+  w.e085 = 0.85 * e;
+  w.sq1me2 = sqrt(1.0 - e * e);
+  w.inv1me2 = 1.0 / (1.0 - e * e);
+  sincos(om, &w.sw, &w.cw);
+  double si, ci;
+  sincos(inc, &si, &ci);
+  w.si = si;
+  w.ci = ci;
+  const double mtot_cgs = m1 * kMsun + m2 * kMsun;
+  const double a_cgs = cbrt(kG * mtot_cgs * (w.Pc * w.Pc) / (kTwoPi * kTwoPi));
+  w.aR = a_cgs / kRsun;
+
+  // flux normalisation (calc_light_curve :613-614)
+  const double l1 = sq(st.r1) * sq(sq(st.t1));
+  const double l2 = sq(st.r2) * sq(sq(st.t2));
+  const double n1 = l1 / (l1 + l2);
+  const double n2 = l2 / (l1 + l2);
+
+  // beaming coefficients (:619-624); log10(Teff) is the table value itself
+  const double ab1 = beam_coeff(st.lt1) * exp(p[15]);
+  const double ab2 = beam_coeff(st.lt2) * exp(p[16]);
+
+  const StarCoef c1 = star_coef(pd, m1, m2, e, si, st.r1, st.r2, p[9], p[10], p[13], ab1);
+  const StarCoef c2 = star_coef(pd, m2, m1, e, si, st.r2, st.r1, p[11], p[12], p[14], ab2);
+
+  // star 2 sees u+pi: odd harmonics of u flip sign
+  const double s2 = si * si;
+  w.kconst = n1 + n2 + (n1 * c1.am1 + n2 * c2.am1);
+  w.kb = n1 * c1.kb - n2 * c2.kb;
+  const double rp = n1 * c1.kref + n2 * c2.kref;
+  const double rm = n1 * c1.kref - n2 * c2.kref;
+  w.kr0 = rp * (0.64 + 0.18 * s2);
+  w.kr2 = -rp * (0.18 * s2);
+  w.krs = -rm * si;
+  w.kam2 = n1 * c1.am2 + n2 * c2.am2;
+  w.kc21 = n1 * c1.c21 + n2 * c2.c21;
+  w.ks1 = n1 * c1.s1 - n2 * c2.s1;
+  w.ks3 = n1 * c1.s3 - n2 * c2.s3;
+  w.kam3 = n1 * c1.am3 + n2 * c2.am3;
+  w.kc22 = n1 * c1.c22 + n2 * c2.c22;
+  w.kc4 = n1 * c1.c4 + n2 * c2.c4;
+
+  // eclipse
+  w.r1 = st.r1;
+  w.r2 = st.r2;
+  w.ecl1 = n1 / (kPi * (st.r1 * st.r1));
+  w.ecl2 = n2 / (kPi * (st.r2 * st.r2));
+  w.rbig = st.r2 > st.r1 ? st.r2 : st.r1;
+  w.rsml = st.r2 > st.r1 ? st.r1 : st.r2;
+  w.dcrit = sqrt(w.rbig * w.rbig - w.rsml * w.rsml);
+
+  w.blend = p[19];
+  w.tune = p[20];
+
+  // Gaia G term (loglikelihood :834-848), only the 673 nm band is used
+  const double g = ab_mag(band_flux(673.0, st.r1 * kRsun, st.r2 * kRsun, st.t1, st.t2, mag[0], p[19]));
+  const double gr = (g - mag[1]) / magerr[0];
+  w.chi2_extra = gr * gr;
+
+  // Roche overflow (:953-974), separation from the same Kepler a
+  const double q12 = m1 / m2;
+  const double peri = a_cgs * (1.0 - e);
+  const double f1 = (st.r1 * kRsun) / peri;
+  const double f2 = (st.r2 * kRsun) / peri;
+  w.roche = ((lobe_fraction(q12) < f1) || (lobe_fraction(1.0 / q12) < f2)) ? 1.0 : 0.0;
+  for (int k = 0; k < 6; ++k) w.pad[k] = 0.0;
+}
+
+// ------------------------------------------------------------------------
+// eclipse_area (likelihood3.c:353-389) with pre-ordered radii (Rsun), d>=0
+// ------------------------------------------------------------------------
+__device__ __forceinline__ double overlap_partial(double ra, double rb, double d, bool inner) {
+  const double cq = d * d - rb * rb + ra * ra;
+  const double hh = sqrt((4. * d * d * ra * ra - cq * cq) / (4. * d * d));
+  const double la = ra * ra * asin(hh / ra) - hh * sqrt(ra * ra - hh * hh);
+  const double lb = rb * rb * asin(hh / rb) - hh * sqrt(rb * rb - hh * hh);
+  return inner ? (kPi * rb * rb - (-la + lb)) : (la + lb);
+}
+
+__device__ __forceinline__ double overlap_area(double ra, double rb, double dc, double d) {
+  double area = 0.0;
+  if (d < ra - rb) area = kPi * rb * rb;
+  const bool outer = (d > dc) & (d < ra + rb);
+  const bool inner = (d <= dc) & (d >= ra - rb);
+  if (outer | inner) area = overlap_partial(ra, rb, d, inner);
+  return area;
+}
+
+// ------------------------------------------------------------------------
+// one cadence: returns Amag1 + Amag2 before median removal
+// ------------------------------------------------------------------------
+struct Orbit {
+  double cu, su;   // cos/sin(omega0 + nu)
+  double beta;     // (1 + e cos nu)/(1 - e^2)
+  double dR;       // projected separation [Rsun]
+  double zz;       // sign carrier of Z1 - Z2 (>0: star 1 in front)
+  double rR;       // radial separation [Rsun]
+  double cnu, snu; // cos/sin nu
+};
+
+__device__ __forceinline__ Orbit hb_orbit(double t, const WalkerConst& w) {
+  const double e = w.e;
+  double m = kTwoPi * (t * kDay - w.T0c) / w.Pc;
+  m = fmod_twopi(m);
+  const double sg = sign_sin_reduced(m);
+  double E = (sg == 0.0) ? m : m + w.e085 * sg;
+  double s, c;
+#pragma unroll
+  for (int it = 0; it < 5; ++it) {
+    sincos(E, &s, &c);
+    E = E - ((E - e * s) - m) / (1.0 - e * c);
+  }
+  sincos(E, &s, &c);
+  const double den = 1.0 - e * c;
+  const double inv = 1.0 / den;
+  Orbit o;
+  o.cnu = (c - e) * inv;
+  o.snu = w.sq1me2 * s * inv;
+  o.cu = w.cw * o.cnu - w.sw * o.snu;
+  o.su = w.sw * o.cnu + w.cw * o.snu;
+  o.beta = (1.0 + e * o.cnu) * w.inv1me2;
+  o.rR = w.aR * den;
+  const double sci = o.su * w.ci;
+  o.dR = o.rR * sqrt(o.cu * o.cu + sci * sci);
+  o.zz = o.su * w.si;
+  return o;
+}
+
+__device__ __forceinline__ double hb_cadence_flux(double t, const WalkerConst& w) {
+  const Orbit o = hb_orbit(t, w);
+  const double cu = o.cu, su = o.su;
+  const double c2 = (cu - su) * (cu + su);   // cos 2u
+  const double s3 = su * (3.0 - 4.0 * su * su);  // sin 3u
+  const double c4 = 2.0 * c2 * c2 - 1.0;     // cos 4u
+  const double b = o.beta;
+  const double b2 = b * b;
+  const double b3 = b2 * b;
+  double v = w.kconst + w.kb * cu;
+  v += b2 * (w.kr0 + w.kr2 * c2 + w.krs * su);
+  v += b3 * (w.kam2 + w.kc21 * c2);
+  v += (b2 * b2) * (w.ks1 * su + w.ks3 * s3);
+  v += (b3 * b2) * (w.kam3 + w.kc22 * c2 + w.kc4 * c4);
+  // eclipse: only lanes with overlap take the branch
+  if (o.dR < w.rbig + w.rsml && o.zz != 0.0) {
+    const double area = overlap_area(w.rbig, w.rsml, w.dcrit, o.dR);
+    v -= area * (o.zz < 0.0 ? w.ecl2 : w.ecl1);
+  }
+  return v;
+}
+
+}  // namespace hbdev

@@ -1,0 +1,71 @@
+// hb_internal.hpp -- types shared between the kernels and the host C-ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#include "hb_device.hpp"
+
+namespace hbk {
+
+struct MagArgs {
+  double mag[5];     // {D [pc], G, B-V, V-G, G-T}
+  double magerr[4];
+};
+
+// LDS scratch of the eval kernel (precedes the template slab); 16-B multiple.
+struct alignas(16) SelShared {
+  uint32_t hist[256];
+  unsigned long long red_min[16];
+  unsigned long long red_max[16];
+  double red_sum[16];
+  unsigned long long ans;
+  int bin;
+  uint32_t before;
+  uint32_t cnt;
+  uint32_t pad[3];
+};
+static_assert(sizeof(SelShared) % 16 == 0, "LDS carve must stay 16-B aligned");
+
+struct EvalPlan {
+  long n = 0;
+  long kth = 0;        // 0-based rank of the subtracted "median"
+  int nw = 1;          // waves per walker
+  bool lds = true;     // template in LDS (else HBM scratch slab)
+  size_t lds_bytes = 0;
+};
+
+struct TrajArgs {
+  hbdev::WalkerConst w;  // orbit fields only; aR carries a in cm
+  double fz1, fz2;       // M2/Mtot, M1/Mtot after the traj() mass swap
+};
+
+enum ProbeOp {
+  kOpAlphaBeam = 0,
+  kOpBeaming,
+  kOpEllipsoidal,
+  kOpReflection,
+  kOpEclipse,
+  kOpGetT,
+  kOpGetR,
+  kOpEnvT,
+  kOpEnvR,
+  kOpRadiiTeffs,
+  kOpMags,
+  kOpRoche,
+  kOpEggleton,
+};
+
+EvalPlan make_plan(long n);
+hipError_t launch_prep(const double* d_params, int nwalk, const MagArgs& ma, hbdev::WalkerConst* d_wc,
+                       hipStream_t s);
+hipError_t launch_eval(const EvalPlan& pl, const double* t, const double* f, const double* sg,
+                       const hbdev::WalkerConst* wc, int nwalk, double* logl, double* tmpl,
+                       double* scratch, int mode, hipStream_t s);
+hipError_t launch_traj(const double* d_times, int nt, const TrajArgs& ta, double* d, double* z1,
+                       double* z2, double* rr, double* ff, hipStream_t s);
+hipError_t launch_probe(int op, const double* d_in, double* d_out, hipStream_t s);
+hipError_t launch_partition(double* d_a, int lo, int hi, int* d_res, hipStream_t s);
+hipError_t launch_median(double* d_a, long n, long kth, hipStream_t s);
+
+}  // namespace hbk

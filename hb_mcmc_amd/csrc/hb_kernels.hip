@@ -1,0 +1,446 @@
+// hb_kernels.hip -- gfx950 kernels for the HB light-curve log-likelihood.
+//
+//   hb_prep_kernel      one lane per walker: WalkerConst (hb_device.hpp)
+//   hb_eval_kernel<NW>  one workgroup of NW waves per walker:
+//                         1. model flux for every cadence (t streamed from
+//                            HBM/L2, coalesced), kept in LDS (or an HBM slab
+//                            when N*8 B exceeds the LDS budget);
+//                         2. exact median by radix-select on order-preserving
+//                            64-bit keys, 8-bit digits starting below the
+//                            common prefix of min/max, LDS histogram
+//                            (replaces quickSort, likelihood3.c:86-105);
+//                         3. normalise + blend (:679-685) and chi^2 with a
+//                            wave-shuffle + LDS reduction (:822-832), then the
+//                            Gaia term and Roche override (:834-869).
+//
+// All launches are asynchronous on the caller's stream and allocation-free
+// once hb_reserve() sized the workspace.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+
+#include "hb_device.hpp"
+#include "hb_internal.hpp"
+
+using namespace hbdev;
+
+namespace hbk {
+
+// ---------------------------------------------------------------------------
+// kernel 1: per-walker constants
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(64) void hb_prep_kernel(const double* __restrict__ params, int nwalk,
+                                                     MagArgs ma, WalkerConst* __restrict__ out) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= nwalk) return;
+  double p[kNpars];
+#pragma unroll
+  for (int k = 0; k < kNpars; ++k) p[k] = params[(size_t)j * kNpars + k];
+  WalkerConst w;
+  hb_prepare_walker(p, ma.mag, ma.magerr, w);
+  out[j] = w;
+}
+
+// ---------------------------------------------------------------------------
+// block-level helpers
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    uint64_t o = __shfl_xor(v, off, 64);
+    v = o < v ? o : v;
+  }
+  return v;
+}
+__device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    uint64_t o = __shfl_xor(v, off, 64);
+    v = o > v ? o : v;
+  }
+  return v;
+}
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+// k-th smallest (0-based) of vals[0..n) by radix select; every thread of the
+// block gets the same answer.  kmin/kmax: block-wide min/max keys.
+template <int NW>
+__device__ double block_select(const double* vals, long n, long kth, uint64_t kmin, uint64_t kmax,
+                               SelShared* sh) {
+  constexpr int NT = 64 * NW;
+  const int tid = threadIdx.x;
+  if (kmin == kmax) return dval(kmin);
+  int hi = 63 - __builtin_clzll(kmin ^ kmax);  // highest undetermined bit
+  uint64_t mask = (hi == 63) ? 0ull : ~((2ull << hi) - 1ull);
+  uint64_t prefix = kmin & mask;
+  uint32_t kk = (uint32_t)kth;
+  uint32_t cnt = 0;
+  while (true) {
+    const int width = hi + 1 < 8 ? hi + 1 : 8;
+    const int shift = hi + 1 - width;
+    const uint32_t dmask = (1u << width) - 1u;
+    for (int b = tid; b < 256; b += NT) sh->hist[b] = 0u;
+    __syncthreads();
+    for (long i = tid; i < n; i += NT) {
+      const uint64_t key = dkey(vals[i]);
+      if ((key & mask) == prefix) atomicAdd(&sh->hist[(uint32_t)(key >> shift) & dmask], 1u);
+    }
+    __syncthreads();
+    if (tid < 64) {
+      const uint32_t c0 = sh->hist[4 * tid + 0], c1 = sh->hist[4 * tid + 1];
+      const uint32_t c2 = sh->hist[4 * tid + 2], c3 = sh->hist[4 * tid + 3];
+      const uint32_t s = c0 + c1 + c2 + c3;
+      uint32_t incl = s;
+#pragma unroll
+      for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t o = __shfl_up(incl, off, 64);
+        if (tid >= off) incl += o;
+      }
+      const uint32_t excl = incl - s;
+      if (excl <= kk && kk < incl) {
+        uint32_t before = excl;
+        int bin = 4 * tid;
+        uint32_t c = c0;
+        if (kk >= before + c0) { before += c0; bin += 1; c = c1;
+          if (kk >= before + c1) { before += c1; bin += 1; c = c2;
+            if (kk >= before + c2) { before += c2; bin += 1; c = c3; } } }
+        sh->bin = bin;
+        sh->before = before;
+        sh->cnt = c;
+      }
+    }
+    __syncthreads();
+    const uint32_t bin = (uint32_t)sh->bin;
+    kk -= sh->before;
+    cnt = sh->cnt;
+    prefix |= (uint64_t)bin << shift;
+    mask |= (uint64_t)dmask << shift;
+    hi = shift - 1;
+    if (cnt == 1 || hi < 0) break;
+  }
+  if (hi < 0) return dval(prefix);
+  // unique survivor: fetch its full key
+  for (long i = tid; i < n; i += NT) {
+    const uint64_t key = dkey(vals[i]);
+    if ((key & mask) == prefix) sh->ans = key;
+  }
+  __syncthreads();
+  return dval(sh->ans);
+}
+
+template <int NW>
+__device__ __forceinline__ void block_minmax(uint64_t& kmn, uint64_t& kmx, SelShared* sh) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  kmn = wave_min_u64(kmn);
+  kmx = wave_max_u64(kmx);
+  if (NW > 1) {
+    if (lane == 0) { sh->red_min[wave] = kmn; sh->red_max[wave] = kmx; }
+    __syncthreads();
+    kmn = sh->red_min[0];
+    kmx = sh->red_max[0];
+#pragma unroll
+    for (int k = 1; k < NW; ++k) {
+      kmn = sh->red_min[k] < kmn ? sh->red_min[k] : kmn;
+      kmx = sh->red_max[k] > kmx ? sh->red_max[k] : kmx;
+    }
+  }
+}
+
+template <int NW>
+__device__ __forceinline__ double block_sum(double v, SelShared* sh) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  v = wave_sum(v);
+  if (NW > 1) {
+    __syncthreads();
+    if (lane == 0) sh->red_sum[wave] = v;
+    __syncthreads();
+    v = sh->red_sum[0];
+#pragma unroll
+    for (int k = 1; k < NW; ++k) v += sh->red_sum[k];
+  }
+  return v;
+}
+
+// ---------------------------------------------------------------------------
+// kernel 2: one workgroup per walker
+// mode 0: logL[w];  mode 1: template[w][0..n)
+// ---------------------------------------------------------------------------
+template <int NW, bool LDS>
+__global__ __launch_bounds__(64 * NW) void hb_eval_kernel(
+    const double* __restrict__ t, const double* __restrict__ f, const double* __restrict__ sg,
+    long n, long kth, const WalkerConst* __restrict__ wcs, double* __restrict__ logl,
+    double* __restrict__ tmpl_out, double* __restrict__ scratch, int mode) {
+  constexpr int NT = 64 * NW;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  SelShared* sh = reinterpret_cast<SelShared*>(smem);
+  const int tid = threadIdx.x;
+  const int wv = blockIdx.x;
+  double* vals = LDS ? reinterpret_cast<double*>(smem + sizeof(SelShared))
+                     : scratch + (size_t)wv * (size_t)n;
+  const WalkerConst& w = wcs[wv];
+
+  // 1. model flux, two independent cadences per iteration for ILP
+  uint64_t kmn = ~0ull, kmx = 0ull;
+  for (long i0 = tid; i0 < n; i0 += 2 * NT) {
+    const long i1 = i0 + NT;
+    const bool ok1 = i1 < n;
+    const double ta = t[i0];
+    const double tb = t[ok1 ? i1 : i0];
+    const double va = hb_cadence_flux(ta, w);
+    const double vb = hb_cadence_flux(tb, w);
+    vals[i0] = va;
+    uint64_t ka = dkey(va);
+    kmn = ka < kmn ? ka : kmn;
+    kmx = ka > kmx ? ka : kmx;
+    if (ok1) {
+      vals[i1] = vb;
+      uint64_t kb = dkey(vb);
+      kmn = kb < kmn ? kb : kmn;
+      kmx = kb > kmx ? kb : kmx;
+    }
+  }
+  __syncthreads();
+  block_minmax<NW>(kmn, kmx, sh);
+
+  // 2. median (element of rank kth in ascending order)
+  const double med = block_select<NW>(vals, n, kth, kmn, kmx, sh);
+
+  // 3. normalise, blend, chi^2
+  const double blend = w.blend, one_m_blend = 1.0 - w.blend, tune = w.tune;
+  if (mode == 1) {
+    double* o = tmpl_out + (size_t)wv * (size_t)n;
+    for (long i = tid; i < n; i += NT) {
+      double m = (vals[i] - med) + 1.0;
+      o[i] = (blend + m * one_m_blend) * tune;
+    }
+    return;
+  }
+  double acc = 0.0;
+  for (long i = tid; i < n; i += NT) {
+    double m = (vals[i] - med) + 1.0;
+    m = (blend + m * one_m_blend) * tune;
+    const double r = (m - f[i]) / sg[i];
+    acc += r * r;
+  }
+  const double chi2 = block_sum<NW>(acc, sh);
+  if (tid == 0) {
+    double c = chi2 + w.chi2_extra;
+    if (w.roche != 0.0) c = kBig;
+    logl[wv] = -c / 2.0;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// auxiliary kernels for the likelihood3.h drop-in entry points
+// ---------------------------------------------------------------------------
+// traj(): one lane per time
+__global__ void hb_traj_kernel(const double* __restrict__ times, int nt, TrajArgs ta,
+                               double* __restrict__ d, double* __restrict__ z1,
+                               double* __restrict__ z2, double* __restrict__ rr,
+                               double* __restrict__ ff) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nt) return;
+  const Orbit o = hb_orbit(times[i], ta.w);
+  d[i] = o.dR;  // aR holds a in cm for this path
+  rr[i] = o.rR;
+  ff[i] = atan2(o.snu, o.cnu);
+  const double zz = o.rR * o.su * ta.w.si;
+  z1[i] = zz * ta.fz1;
+  z2[i] = -zz * ta.fz2;
+}
+
+// scalar entry points, evaluated by one device lane
+__global__ void hb_probe_kernel(int op, const double* __restrict__ in, double* __restrict__ out) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  switch (op) {
+    case kOpAlphaBeam: out[0] = beam_coeff(in[0]); break;
+    case kOpBeaming: {
+      // (P, M1, M2, e, inc, omega0, nu, alpha_beam)
+      const StarCoef c = star_coef(in[0], in[1], in[2], in[3], sin(in[4]), 1.0, 1.0, 0.16, 0.34, 1.0, in[7]);
+      out[0] = c.kb * cos(in[5] + in[6]);
+      break;
+    }
+    case kOpEllipsoidal: {
+      // (P, M1, M2, e, inc, omega0, nu, R1, a, mu, tau)
+      const double e = in[3], nu = in[6], u = in[5] + in[6];
+      const StarCoef c = star_coef(in[0], in[1], in[2], e, sin(in[4]), in[7], 1.0, in[9], in[10], 1.0, 1.0);
+      const double b = (1.0 + e * cos(nu)) / (1.0 - e * e);
+      const double b3 = b * b * b, b4 = b3 * b, b5 = b4 * b;
+      out[0] = c.am1 + b3 * (c.am2 + c.c21 * cos(2 * u)) + b4 * (c.s1 * sin(u) + c.s3 * sin(3 * u)) +
+               b5 * (c.am3 + c.c22 * cos(2 * u) + c.c4 * cos(4 * u));
+      break;
+    }
+    case kOpReflection: {
+      // (P, M1, M2, e, inc, omega0, nu, R2, alpha_ref1)
+      const double e = in[3], nu = in[6], u = in[5] + in[6], si = sin(in[4]);
+      const StarCoef c = star_coef(in[0], in[1], in[2], e, si, 1.0, in[7], 0.16, 0.34, in[8], 1.0);
+      const double b = (1.0 + e * cos(nu)) / (1.0 - e * e);
+      out[0] = c.kref * (b * b) * (0.64 - si * sin(u) + 0.18 * (si * si) * (1.0 - cos(2 * u)));
+      break;
+    }
+    case kOpEclipse: {
+      double ra = in[0], rb = in[1];
+      if (rb > ra) { const double k = ra; ra = rb; rb = k; }
+      const double d = fabs(in[2]) / kRsun;
+      out[0] = overlap_area(ra, rb, sqrt(ra * ra - rb * rb), d);
+      break;
+    }
+    case kOpGetT: out[0] = logteff_of_mass(exp10(in[0])); break;
+    case kOpGetR: out[0] = logradius_of_mass(exp10(in[0])); break;
+    case kOpEnvT: out[0] = teff_spread(); break;
+    case kOpEnvR: out[0] = radius_spread_of_mass(exp10(in[0])); break;
+    case kOpRadiiTeffs: {
+      const Stellar s = stellar_of(in);
+      out[0] = s.r1; out[1] = s.r2; out[2] = s.t1; out[3] = s.t2;
+      break;
+    }
+    case kOpMags: {
+      // in[0..20] params, in[21] distance
+      const Stellar s = stellar_of(in);
+      const double r1 = s.r1 * kRsun, r2 = s.r2 * kRsun;
+      const double mb = ab_mag(band_flux(442.0, r1, r2, s.t1, s.t2, in[21], in[19]));
+      const double mv = ab_mag(band_flux(540.0, r1, r2, s.t1, s.t2, in[21], in[19]));
+      const double mg = ab_mag(band_flux(673.0, r1, r2, s.t1, s.t2, in[21], in[19]));
+      const double mt = ab_mag(band_flux(750.0, r1, r2, s.t1, s.t2, in[21], in[19]));
+      out[0] = mg; out[1] = mb - mv; out[2] = mv - mg; out[3] = mg - mt;
+      break;
+    }
+    case kOpRoche: {
+      const double mag[5] = {1000., 1., 1., 1., 1.};
+      const double err[4] = {1e15, 1e15, 1e15, 1e15};
+      WalkerConst w;
+      hb_prepare_walker(in, mag, err, w);
+      out[0] = w.roche;
+      break;
+    }
+    case kOpEggleton: out[0] = lobe_fraction(in[0]); break;
+    default: out[0] = __builtin_nan(""); break;
+  }
+}
+
+// Lomuto partition, exact reference order (likelihood3.c:48-64), one lane.
+__global__ void hb_partition_kernel(double* __restrict__ a, int lo, int hi, int* __restrict__ res) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  const double piv = a[hi];
+  int slot = lo - 1;
+  for (int k = lo; k < hi; ++k) {
+    if (a[k] < piv) {
+      ++slot;
+      const double x = a[slot]; a[slot] = a[k]; a[k] = x;
+    }
+  }
+  const double x = a[slot + 1]; a[slot + 1] = a[hi]; a[hi] = x;
+  res[0] = slot + 1;
+}
+
+// remove_median on an array already in HBM: one 16-wave workgroup
+__global__ __launch_bounds__(1024) void hb_median_kernel(double* __restrict__ a, long n, long kth) {
+  __shared__ SelShared sh;
+  uint64_t kmn = ~0ull, kmx = 0ull;
+  for (long i = threadIdx.x; i < n; i += 1024) {
+    const uint64_t k = dkey(a[i]);
+    kmn = k < kmn ? k : kmn;
+    kmx = k > kmx ? k : kmx;
+  }
+  block_minmax<16>(kmn, kmx, &sh);
+  const double med = block_select<16>(a, n, kth, kmn, kmx, &sh);
+  __syncthreads();
+  for (long i = threadIdx.x; i < n; i += 1024) a[i] -= med;
+}
+
+// ---------------------------------------------------------------------------
+// host launchers
+// ---------------------------------------------------------------------------
+hipError_t launch_prep(const double* d_params, int nwalk, const MagArgs& ma, WalkerConst* d_wc,
+                       hipStream_t s) {
+  if (nwalk <= 0) return hipSuccess;
+  hipLaunchKernelGGL(hb_prep_kernel, dim3((nwalk + 63) / 64), dim3(64), 0, s, d_params, nwalk, ma, d_wc);
+  return hipGetLastError();
+}
+
+template <int NW, bool LDS>
+static hipError_t launch_eval_t(const EvalPlan& pl, const double* t, const double* f, const double* sg,
+                                const WalkerConst* wc, int nwalk, double* logl, double* tmpl,
+                                double* scratch, int mode, hipStream_t s) {
+  auto kern = hb_eval_kernel<NW, LDS>;
+  static bool attr_set = false;  // per instantiation; benign race (idempotent)
+  if (!attr_set && pl.lds_bytes > 65536) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)pl.lds_bytes);
+    if (e != hipSuccess) return e;
+    attr_set = true;
+  }
+  hipLaunchKernelGGL(kern, dim3(nwalk), dim3(64 * NW), pl.lds_bytes, s, t, f, sg, pl.n, pl.kth, wc,
+                     logl, tmpl, scratch, mode);
+  return hipGetLastError();
+}
+
+hipError_t launch_eval(const EvalPlan& pl, const double* t, const double* f, const double* sg,
+                       const WalkerConst* wc, int nwalk, double* logl, double* tmpl, double* scratch,
+                       int mode, hipStream_t s) {
+  if (nwalk <= 0) return hipSuccess;
+#define HB_CASE(NWV)                                                                              \
+  case NWV:                                                                                       \
+    return pl.lds ? launch_eval_t<NWV, true>(pl, t, f, sg, wc, nwalk, logl, tmpl, scratch, mode, s) \
+                  : launch_eval_t<NWV, false>(pl, t, f, sg, wc, nwalk, logl, tmpl, scratch, mode, s);
+  switch (pl.nw) {
+    HB_CASE(1)
+    HB_CASE(2)
+    HB_CASE(4)
+    HB_CASE(8)
+    HB_CASE(16)
+    default: return hipErrorInvalidValue;
+  }
+#undef HB_CASE
+}
+
+hipError_t launch_traj(const double* d_times, int nt, const TrajArgs& ta, double* d, double* z1,
+                       double* z2, double* rr, double* ff, hipStream_t s) {
+  if (nt <= 0) return hipSuccess;
+  hipLaunchKernelGGL(hb_traj_kernel, dim3((nt + 255) / 256), dim3(256), 0, s, d_times, nt, ta, d, z1, z2,
+                     rr, ff);
+  return hipGetLastError();
+}
+
+hipError_t launch_probe(int op, const double* d_in, double* d_out, hipStream_t s) {
+  hipLaunchKernelGGL(hb_probe_kernel, dim3(1), dim3(64), 0, s, op, d_in, d_out);
+  return hipGetLastError();
+}
+
+hipError_t launch_partition(double* d_a, int lo, int hi, int* d_res, hipStream_t s) {
+  hipLaunchKernelGGL(hb_partition_kernel, dim3(1), dim3(64), 0, s, d_a, lo, hi, d_res);
+  return hipGetLastError();
+}
+
+hipError_t launch_median(double* d_a, long n, long kth, hipStream_t s) {
+  hipLaunchKernelGGL(hb_median_kernel, dim3(1), dim3(1024), 0, s, d_a, n, kth);
+  return hipGetLastError();
+}
+
+// Choose waves-per-walker and template storage for N cadences.
+EvalPlan make_plan(long n) {
+  EvalPlan pl;
+  pl.n = n;
+  pl.kth = (n % 2 == 0) ? n / 2 : n / 2 + 1;  // likelihood3.c:97-99
+  const size_t lds_cap = 163840;
+  const size_t need = sizeof(SelShared) + (size_t)n * sizeof(double);
+  if (need <= lds_cap) {
+    pl.lds = true;
+    pl.lds_bytes = need;
+    const size_t blocks_per_cu = lds_cap / need;  // LDS-limited residency
+    int nw = 1;
+    while (nw < 16 && (size_t)nw * blocks_per_cu < 16) nw <<= 1;
+    pl.nw = nw;
+  } else {
+    pl.lds = false;
+    pl.lds_bytes = sizeof(SelShared);
+    pl.nw = 4;
+  }
+  return pl;
+}
+
+}  // namespace hbk

@@ -1,0 +1,94 @@
+"""Pin the oracle (oracle/hb_oracle.c) against vectors the REFERENCE produced
+(tests/golden/make_golden.py): bit-exact, same box / same glibc libm."""
+import numpy as np
+import pytest
+
+from conftest import golden
+
+
+def same(a, b):
+    a, b = np.asarray(a), np.asarray(b)
+    return a.shape == b.shape and np.array_equal(a, b, equal_nan=True)
+
+
+def test_scalar_functions(oracle):
+    g = golden("scalars.npz")
+    assert same([oracle.get_alpha_beam(x) for x in g["ab_in"]], g["ab_out"])
+    assert same([oracle.getT(x) for x in g["lm_in"]], g["getT_out"])
+    assert same([oracle.getR(x) for x in g["lm_in"]], g["getR_out"])
+    assert same([oracle.envelope_Temp(x) for x in g["lm_in"]], g["envT_out"])
+    assert same([oracle.envelope_Radius(x) for x in g["lm_in"]], g["envR_out"])
+    assert same([oracle.eggleton(x) for x in g["egg_in"]], g["egg_out"])
+    assert same([oracle.beaming(*r) for r in g["beam_in"]], g["beam_out"])
+    assert same([oracle.ellipsoidal(*r) for r in g["ell_in"]], g["ell_out"])
+    assert same([oracle.reflection(*r) for r in g["refl_in"]], g["refl_out"])
+    assert same([oracle.eclipse_area(*r) for r in g["ecl_in"]], g["ecl_out"])
+    assert same([oracle.radii_teffs(p) for p in g["pv"]], g["radii_out"])
+    assert same([oracle.mags(p, d) for p, d in zip(g["pv"], g["dist"])], g["mags_out"])
+    assert same([oracle.roche(p) for p in g["pv"]], g["roche_out"])
+
+
+def test_eclipse_covers_all_regimes():
+    g = golden("scalars.npz")
+    rs = 6.955e10
+    regimes = set()
+    for (r1, r2, d), a in zip(g["ecl_in"], g["ecl_out"]):
+        big, sm = max(r1, r2), min(r1, r2)
+        dd = abs(d) / rs
+        dc = np.sqrt(big * big - sm * sm)
+        regimes.add(0 if dd >= big + sm else 1 if dd < big - sm else 2 if dd > dc else 3)
+    assert regimes == {0, 1, 2, 3}
+
+
+def test_traj(oracle):
+    g = golden("traj.npz")
+    out = oracle.traj(g["times"], g["tp"])
+    for k, name in enumerate(("d", "z1", "z2", "rr", "ff")):
+        assert same(out[k], g[name]), name
+    for tp, ex in zip(g["ex_tp"], g["ex_out"]):
+        assert same(np.stack(oracle.traj(g["ex_times"], tp)), ex)
+
+
+def test_median_sort_partition(oracle):
+    g = golden("median.npz")
+    for i in range(int(g["ncases"][0])):
+        a = g[f"in{i}"]
+        assert same(oracle.remove_median(a), g[f"rm{i}"])
+        assert same(oracle.quicksort(a), g[f"qs{i}"])
+        k, pa = oracle.partition(a)
+        assert k == int(g[f"pk{i}"][0]) and same(pa, g[f"pa{i}"])
+
+
+@pytest.mark.parametrize("name", ["lc_synth1024.npz", "lc_synth7.npz", "lc_real231937440.npz"])
+def test_light_curves_and_loglike(oracle, name):
+    g = golden(name)
+    for p, tm in zip(g["params"], g["templates"]):
+        assert same(oracle.light_curve(g["t"], p), tm)
+    ll = [oracle.loglike(g["t"], g["f"], g["s"], p, g["mag"], g["magerr"])[0] for p in g["params"]]
+    assert same(ll, g["logl"])
+    # batched OpenMP path is the same function
+    assert same(oracle.loglike_batch(g["t"], g["f"], g["s"], g["params"], g["mag"], g["magerr"], 4), g["logl"])
+
+
+def test_sigma_clamp_side_effect(oracle):
+    g = golden("lc_synth1024.npz")
+    assert (g["s"] < 1e-5).any()
+    _, s_after = oracle.loglike(g["t"], g["f"], g["s"], g["params"][0], g["mag"], g["magerr"])
+    assert same(s_after, np.maximum(g["s"], 1e-5))
+
+
+def test_roche_sentinel_present():
+    g = golden("lc_synth1024.npz")
+    assert (g["logl"] == -5e14).sum() >= 1
+    assert np.isfinite(g["logl"]).sum() >= 20
+
+
+@pytest.mark.slow
+def test_20k_and_real1861(oracle):
+    g = golden("lc_synth20000.npz")
+    ll = oracle.loglike_batch(g["t"], g["f"], g["s"], g["params"], g["mag"], g["magerr"], 8)
+    assert same(ll, g["logl"])
+    tm = oracle.light_curve_batch(g["t"], g["params"], 8)
+    assert same(tm.sum(1), g["tsum"]) and same(tm[:, :16], g["thead"]) and same(tm[:, -16:], g["ttail"])
+    g = golden("lc_real237957506.npz")
+    assert same(oracle.loglike_batch(g["t"], g["f"], g["s"], g["params"], g["mag"], g["magerr"], 8), g["logl"])
