@@ -30,11 +30,16 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 import numpy as np  # noqa: E402
-import torch  # noqa: E402  (import torch before libhbmi: one HIP runtime)
-import torch.distributed as dist  # noqa: E402
 
 from hb_mcmc_amd import synth  # noqa: E402
-from hb_mcmc_amd.likelihood import HBLikelihood  # noqa: E402
+
+if __name__ == "__main__" and len(sys.argv) == 4 and sys.argv[1] == "--cpu-baseline-child":
+    torch = dist = HBLikelihood = None
+else:
+    import torch  # noqa: E402  (import torch before libhbmi: one HIP runtime)
+    import torch.distributed as dist  # noqa: E402
+
+    from hb_mcmc_amd.likelihood import HBLikelihood  # noqa: E402
 
 METRIC = "log-likelihood evals/sec (walkers×steps/s), 1k-cadence HB light curve"
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md chip table (spec)
@@ -66,6 +71,25 @@ def cpu_threads() -> int:
     return max(1, min(n, 64))
 
 
+def cpu_baseline_child(n, target_s):
+    """Runs in a torch-free child process (no second OpenMP runtime, no HIP
+    threads): the reference likelihood3.c (oracle/_ref) or the oracle port."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as orc
+    impl = orc.Reference() if orc.reference_available() else orc.Oracle()
+    t, f, s = synth.dataset(n, impl.light_curve)
+    print(json.dumps(cpu_baseline(t, f, s, target_s)), flush=True)
+
+
+def run_cpu_baseline(n, target_s):
+    import subprocess
+    r = subprocess.run([sys.executable, os.path.abspath(__file__), "--cpu-baseline-child", str(n), str(target_s)],
+                       capture_output=True, text=True, timeout=600)
+    if r.returncode != 0:
+        return {"error": r.stderr[-400:]}
+    return json.loads(r.stdout.strip().splitlines()[-1])
+
+
 def cpu_baseline(t, f, s, target_s):
     """Reference likelihood3.c (oracle/_ref) or the oracle port, OpenMP over walkers."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -76,6 +100,7 @@ def cpu_baseline(t, f, s, target_s):
     impl = orc.Reference() if kind == "reference" else orc.Oracle()
     nth = cpu_threads()
     mag, err = synth.MAG_DEFAULT, synth.MAGERR_DEFAULT
+    impl.loglike_batch(t, f, s, synth.walkers(nth, seed=4241), mag, err, nth)  # spin up the thread pool
     pilot = synth.walkers(8 * nth, seed=4242)
     t0 = time.perf_counter()
     impl.loglike_batch(t, f, s, pilot, mag, err, nth)
@@ -200,7 +225,7 @@ def main():
             "kernel_only_evals_per_s": w / ((eval_ms + prep_ms) * 1e-3),
         }
         if world == 1 and not a.no_cpu_baseline:
-            line["cpu_baseline"] = cpu_baseline(t, f, s, a.cpu_seconds)
+            line["cpu_baseline"] = run_cpu_baseline(n, a.cpu_seconds)
         print(json.dumps(line), flush=True)
     L.close()
     if world > 1:
@@ -208,4 +233,7 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    if len(sys.argv) == 4 and sys.argv[1] == "--cpu-baseline-child":
+        cpu_baseline_child(int(sys.argv[2]), float(sys.argv[3]))
+    else:
+        main()

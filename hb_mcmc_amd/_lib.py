@@ -11,7 +11,7 @@ import subprocess
 import threading
 
 PKG = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(PKG, "lib", "libhbmi.so")
+LIB_PATH = os.environ.get("HBMI_LIB") or os.path.join(PKG, "lib", "libhbmi.so")  # override: experiments only
 CSRC = os.path.join(PKG, "csrc")
 
 _D = C.c_double

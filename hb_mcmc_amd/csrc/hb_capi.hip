@@ -72,7 +72,7 @@ struct hb_ctx {
   MagArgs mags{};
   double* d_t = nullptr;
   double* d_f = nullptr;
-  double* d_s = nullptr;
+  double* d_s = nullptr;          // 1 / max(sigma, 1e-5)
   // per-walker workspace
   int cap = 0;
   WalkerConst* d_wc = nullptr;
@@ -151,8 +151,10 @@ extern "C" hb_ctx* hb_create(const double* t, const double* f, const double* sig
 
   if (hipSetDevice(device) != hipSuccess) { set_err_msg("hb_create: hipSetDevice failed"); return nullptr; }
   std::vector<double> s(sigma, sigma + n);
-  for (long i = 0; i < n; ++i)
+  for (long i = 0; i < n; ++i) {
     if (s[i] < 1.e-5) s[i] = 1.e-5;  // likelihood3.c:824-827, applied once
+    s[i] = 1.0 / s[i];               // the kernel multiplies by 1/sigma
+  }
   const size_t bytes = sizeof(double) * (size_t)n;
   if (hipMalloc(&c->d_t, bytes) != hipSuccess || hipMalloc(&c->d_f, bytes) != hipSuccess ||
       hipMalloc(&c->d_s, bytes) != hipSuccess) {

@@ -23,6 +23,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "hb_math.hpp"
+
 namespace hbdev {
 
 // physical constants, likelihood3.h:4-10
@@ -65,7 +67,9 @@ struct alignas(16) WalkerConst {
   double blend, tune;
   double chi2_extra;             // ((Gmag - G_obs)/sigma_G)^2 (USE_GMAG=1)
   double roche;                  // 1.0 if RocheOverflow(), else 0.0
-  double pad[6];
+  double mA, mB;                 // mean anomaly M = fma(t, DAY, mB) * mA (hot loop)
+  double rsum;                   // Rbig + Rsml
+  double pad[3];
 };
 static_assert(sizeof(WalkerConst) == 40 * 8, "WalkerConst layout");
 
@@ -79,7 +83,7 @@ __device__ __forceinline__ double sq(double x) { return x * x; }
 // routine for |x/2pi| >= 2^50, which folded light curves never reach.
 __device__ __forceinline__ double fmod_twopi(double x) {
   const double y = kTwoPi;
-  double q = trunc(x / y);
+  double q = trunc(x * 0.15915494309189533577);  // 1/(2 pi); off-by-one fixed below
   if (!(fabs(q) < 1125899906842624.0)) return fmod(x, y);  // 2^50 (also NaN/inf)
   double r = fma(-q, y, x);
   if (x >= 0.0) {
@@ -93,13 +97,32 @@ __device__ __forceinline__ double fmod_twopi(double x) {
   return r;
 }
 
+// Branch-free fmod(x, 2*PI), exact for |x| < 2^19 (the caller checks the
+// range and reruns other lanes through fmod_twopi).
+__device__ __forceinline__ double fmod_twopi_fast(double x) {
+  const double y = kTwoPi;
+  double q = trunc(x * 0.15915494309189533577);
+  const double r0 = fma(-q, y, x);
+  const bool pos = x >= 0.0;
+  double adj = 0.0;
+  adj = (pos & (r0 < 0.0)) ? -1.0 : adj;
+  adj = (pos & (r0 >= y)) ? 1.0 : adj;
+  adj = (!pos & (r0 > 0.0)) ? 1.0 : adj;
+  adj = (!pos & (r0 <= -y)) ? -1.0 : adj;
+  q += adj;
+  double r = fma(-q, y, x);
+  r = (r == 0.0) ? copysign(0.0, x) : r;
+  return r;
+}
+
 // sign(sin(M)) for M = fmod(., 2*PI) in (-2PI_d, 2PI_d), without a sine.
 // PI_d < pi < nextafter(PI_d), so sin(M) > 0 exactly on (0, PI_d] and on
 // (-2PI_d, -PI_d) (likelihood3.c:155-157 only uses the sign).
 __device__ __forceinline__ double sign_sin_reduced(double m) {
-  if (m == 0.0) return 0.0;
-  if (m > 0.0) return (m <= kPi) ? 1.0 : -1.0;
-  return (m < -kPi) ? 1.0 : -1.0;
+  const double pos = (m <= kPi) ? 1.0 : -1.0;
+  const double neg = (m < -kPi) ? 1.0 : -1.0;
+  const double sg = (m > 0.0) ? pos : neg;
+  return (m == 0.0) ? 0.0 : sg;
 }
 
 // order-preserving uint64 key of a double (non-NaN)
@@ -333,7 +356,12 @@ __device__ inline void hb_prepare_walker(const double* __restrict__ p, const dou
   const double f1 = (st.r1 * kRsun) / peri;
   const double f2 = (st.r2 * kRsun) / peri;
   w.roche = ((lobe_fraction(q12) < f1) || (lobe_fraction(1.0 / q12) < f2)) ? 1.0 : 0.0;
-  for (int k = 0; k < 6; ++k) w.pad[k] = 0.0;
+  // hot-loop mean anomaly: (t DAY - T0 DAY) * (2 pi / P), two roundings
+  // like the reference's three (likelihood3.c:149-152)
+  w.mA = kTwoPi / w.Pc;
+  w.mB = -w.T0c;
+  w.rsum = w.rbig + w.rsml;
+  for (int k = 0; k < 3; ++k) w.pad[k] = 0.0;
 }
 
 // ------------------------------------------------------------------------
@@ -354,6 +382,12 @@ __device__ __forceinline__ double overlap_area(double ra, double rb, double dc, 
   const bool inner = (d <= dc) & (d >= ra - rb);
   if (outer | inner) area = overlap_partial(ra, rb, d, inner);
   return area;
+}
+
+// area * Norm_k / (pi R_k^2) for the star in front; out of line (rare)
+__device__ __noinline__ double eclipse_term(const WalkerConst* w, double dR, double zz) {
+  const double area = overlap_area(w->rbig, w->rsml, w->dcrit, dR);
+  return area * (zz < 0.0 ? w->ecl2 : w->ecl1);
 }
 
 // ------------------------------------------------------------------------
@@ -377,10 +411,10 @@ __device__ __forceinline__ Orbit hb_orbit(double t, const WalkerConst& w) {
   double s, c;
 #pragma unroll
   for (int it = 0; it < 5; ++it) {
-    sincos(E, &s, &c);
+    sincos_small(E, &s, &c);
     E = E - ((E - e * s) - m) / (1.0 - e * c);
   }
-  sincos(E, &s, &c);
+  sincos_small(E, &s, &c);
   const double den = 1.0 - e * c;
   const double inv = 1.0 / den;
   Orbit o;
@@ -395,6 +429,8 @@ __device__ __forceinline__ Orbit hb_orbit(double t, const WalkerConst& w) {
   o.zz = o.su * w.si;
   return o;
 }
+
+__device__ __noinline__ double hb_cadence_flux_slow(double t, const WalkerConst* w);
 
 __device__ __forceinline__ double hb_cadence_flux(double t, const WalkerConst& w) {
   const Orbit o = hb_orbit(t, w);
@@ -416,6 +452,100 @@ __device__ __forceinline__ double hb_cadence_flux(double t, const WalkerConst& w
     v -= area * (o.zz < 0.0 ? w.ecl2 : w.ecl1);
   }
   return v;
+}
+
+// reference-order path for lanes outside the fast sincos/fmod domain
+__device__ __noinline__ double hb_cadence_flux_slow(double t, const WalkerConst* w) {
+  return hb_cadence_flux(t, *w);
+}
+
+// ------------------------------------------------------------------------
+// K cadences at once, branch-free: the K Kepler chains interleave in one
+// basic block (ILP for the fp64 dependency chains).  Lanes whose angles
+// leave the fast sincos/fmod domain set `bad`; the caller reruns them
+// through hb_cadence_flux (ocml path) under one wave-uniform branch.
+// ------------------------------------------------------------------------
+template <int K>
+__device__ __forceinline__ void hb_cadence_flux_k(const double (&t)[K], const WalkerConst& w,
+                                                  double (&v)[K], bool& bad) {
+  const double e = w.e;
+  double m[K], E[K], s[K], c[K];
+  bool ok = true;
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const double mraw = fma(t[k], kDay, w.mB) * w.mA;
+    ok &= sincos_fast_ok(mraw);
+    m[k] = fmod_twopi_fast(mraw);
+    const double sg = sign_sin_reduced(m[k]);
+    E[k] = (sg == 0.0) ? m[k] : m[k] + w.e085 * sg;
+  }
+  // Newton on E - e sin E = M, 5 steps (likelihood3.c:160).  Step 1 evaluates
+  // sin/cos directly; later steps rotate (s, c) by the previous step when the
+  // whole wave's steps are below kRotMax (wave-uniform branch), otherwise
+  // they re-evaluate directly.  The 6th evaluation (final E) likewise.
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    ok &= sincos_fast_ok(E[k]);
+    sincos_fast(E[k], &s[k], &c[k]);
+  }
+  double d[K];
+#pragma unroll
+  for (int it = 0; it < 5; ++it) {
+    bool small = true;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      d[k] = fast_div((E[k] - e * s[k]) - m[k], 1.0 - e * c[k]);
+      E[k] = E[k] - d[k];
+      small &= fabs(d[k]) <= kRotMax;
+    }
+    if (__all(small)) {
+#pragma unroll
+      for (int k = 0; k < K; ++k) rotate_back(d[k], s[k], c[k]);
+    } else {
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        ok &= sincos_fast_ok(E[k]);
+        sincos_fast(E[k], &s[k], &c[k]);
+      }
+    }
+  }
+  bool need_ecl = false;
+  double dd[K], zz[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const double den = 1.0 - e * c[k];
+    const double inv = fast_rcp(den);
+    const double cnu = (c[k] - e) * inv;
+    const double snu = w.sq1me2 * s[k] * inv;
+    const double cu = w.cw * cnu - w.sw * snu;
+    const double su = w.sw * cnu + w.cw * snu;
+    const double b = (1.0 + e * cnu) * w.inv1me2;
+    const double sci = su * w.ci;
+    dd[k] = den * sqrt(cu * cu + sci * sci);  // projected separation / a
+    zz[k] = su * w.si;
+    const double c2 = (cu - su) * (cu + su);
+    const double s3 = su * (3.0 - 4.0 * su * su);
+    const double c4 = 2.0 * c2 * c2 - 1.0;
+    const double b2 = b * b;
+    const double b3 = b2 * b;
+    // values stay ~1 like the reference's Amag1 + Amag2 (one sign, one
+    // exponent: the median radix-select resolves them in one digit pass)
+    double val = w.kconst + w.kb * cu;
+    val += b2 * (w.kr0 + w.kr2 * c2 + w.krs * su);
+    val += b3 * (w.kam2 + w.kc21 * c2);
+    val += (b2 * b2) * (w.ks1 * su + w.ks3 * s3);
+    val += (b3 * b2) * (w.kam3 + w.kc22 * c2 + w.kc4 * c4);
+    v[k] = val;
+    need_ecl |= (dd[k] * w.aR < w.rsum) & (zz[k] != 0.0);
+  }
+  bad = !ok;
+  if (__any(need_ecl)) {
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const double dR = dd[k] * w.aR;
+      if ((dR < w.rsum) & (zz[k] != 0.0)) v[k] -= eclipse_term(&w, dR, zz[k]);
+    }
+  }
 }
 
 }  // namespace hbdev

@@ -31,6 +31,8 @@ struct EvalPlan {
   long n = 0;
   long kth = 0;        // 0-based rank of the subtracted "median"
   int nw = 1;          // waves per walker
+  int vpt = 0;         // >0: one-wave path, cadences per lane (register keys)
+  size_t slab_bytes = 0;  // template slab / histogram bytes (one-wave path)
   bool lds = true;     // template in LDS (else HBM scratch slab)
   size_t lds_bytes = 0;
 };

@@ -24,6 +24,16 @@
 
 using namespace hbdev;
 
+#ifndef HB_K
+#define HB_K 2  // cadences interleaved per lane in the model loop
+#endif
+#ifndef HB_ABLATE_MODEL
+#define HB_ABLATE_MODEL 0
+#endif
+#ifndef HB_ABLATE_SELECT
+#define HB_ABLATE_SELECT 0
+#endif
+
 namespace hbk {
 
 // ---------------------------------------------------------------------------
@@ -64,6 +74,59 @@ __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
   for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
   return v;
+}
+
+// Model flux for cadences tid, tid+NT, ... : HB_K interleaved cadences per lane
+// per iteration (ILP for the fp64 Kepler chains), next iteration's times
+// prefetched; values go to vals[], min/max order keys returned per lane.
+template <int NT>
+__device__ __forceinline__ void model_pass(const double* __restrict__ t, long n, const WalkerConst& w,
+                                           double* vals, int tid, uint64_t& kmn_out, uint64_t& kmx_out) {
+  constexpr int K = HB_K;
+  uint64_t kmn = ~0ull, kmx = 0ull;
+  const long last = n - 1;
+  double tk[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const long i = (long)k * NT + tid;
+    tk[k] = t[i < last ? i : last];
+  }
+  for (long base = 0; base < n; base += (long)K * NT) {
+    double tn[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const long i = base + (long)(K + k) * NT + tid;
+      tn[k] = t[i < last ? i : last];
+    }
+    double v[K];
+    bool bad;
+#if HB_ABLATE_MODEL  // experiment builds only: trivial model, same data flow
+#pragma unroll
+    for (int k = 0; k < K; ++k) v[k] = tk[k] * w.kb + w.kr0;
+    bad = false;
+#else
+    hb_cadence_flux_k<K>(tk, w, v, bad);
+#endif
+    if (__any(bad)) {  // out-of-domain angles: reference-order ocml path
+      if (bad) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) v[k] = hb_cadence_flux_slow(tk[k], &w);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const long i = base + (long)k * NT + tid;
+      if (i < n) {
+        vals[i] = v[k];
+        const uint64_t key = dkey(v[k]);
+        kmn = key < kmn ? key : kmn;
+        kmx = key > kmx ? key : kmx;
+      }
+      tk[k] = tn[k];
+    }
+  }
+  kmn_out = kmn;
+  kmx_out = kmx;
 }
 
 // k-th smallest (0-based) of vals[0..n) by radix select; every thread of the
@@ -171,7 +234,7 @@ __device__ __forceinline__ double block_sum(double v, SelShared* sh) {
 // ---------------------------------------------------------------------------
 template <int NW, bool LDS>
 __global__ __launch_bounds__(64 * NW) void hb_eval_kernel(
-    const double* __restrict__ t, const double* __restrict__ f, const double* __restrict__ sg,
+    const double* __restrict__ t, const double* __restrict__ f, const double* __restrict__ isg,
     long n, long kth, const WalkerConst* __restrict__ wcs, double* __restrict__ logl,
     double* __restrict__ tmpl_out, double* __restrict__ scratch, int mode) {
   constexpr int NT = 64 * NW;
@@ -183,31 +246,18 @@ __global__ __launch_bounds__(64 * NW) void hb_eval_kernel(
                      : scratch + (size_t)wv * (size_t)n;
   const WalkerConst& w = wcs[wv];
 
-  // 1. model flux, two independent cadences per iteration for ILP
-  uint64_t kmn = ~0ull, kmx = 0ull;
-  for (long i0 = tid; i0 < n; i0 += 2 * NT) {
-    const long i1 = i0 + NT;
-    const bool ok1 = i1 < n;
-    const double ta = t[i0];
-    const double tb = t[ok1 ? i1 : i0];
-    const double va = hb_cadence_flux(ta, w);
-    const double vb = hb_cadence_flux(tb, w);
-    vals[i0] = va;
-    uint64_t ka = dkey(va);
-    kmn = ka < kmn ? ka : kmn;
-    kmx = ka > kmx ? ka : kmx;
-    if (ok1) {
-      vals[i1] = vb;
-      uint64_t kb = dkey(vb);
-      kmn = kb < kmn ? kb : kmn;
-      kmx = kb > kmx ? kb : kmx;
-    }
-  }
+  // 1. model flux for every cadence
+  uint64_t kmn, kmx;
+  model_pass<NT>(t, n, w, vals, tid, kmn, kmx);
   __syncthreads();
   block_minmax<NW>(kmn, kmx, sh);
 
   // 2. median (element of rank kth in ascending order)
+#if HB_ABLATE_SELECT  // experiment builds only: no median selection
+  const double med = dval(kmn);
+#else
   const double med = block_select<NW>(vals, n, kth, kmn, kmx, sh);
+#endif
 
   // 3. normalise, blend, chi^2
   const double blend = w.blend, one_m_blend = 1.0 - w.blend, tune = w.tune;
@@ -223,11 +273,194 @@ __global__ __launch_bounds__(64 * NW) void hb_eval_kernel(
   for (long i = tid; i < n; i += NT) {
     double m = (vals[i] - med) + 1.0;
     m = (blend + m * one_m_blend) * tune;
-    const double r = (m - f[i]) / sg[i];
+    const double r = (m - f[i]) * isg[i];  // isg = 1/max(sigma, 1e-5), hb_create
     acc += r * r;
   }
   const double chi2 = block_sum<NW>(acc, sh);
   if (tid == 0) {
+    double c = chi2 + w.chi2_extra;
+    if (w.roche != 0.0) c = kBig;
+    logl[wv] = -c / 2.0;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// One-wave-per-walker path (N <= 64*VPT): keys in VGPRs, the LDS template slab
+// reused as a histogram (11-bit first digit), exact rank among <= 64
+// survivors.  kth is the 0-based rank of likelihood3.c:97-101.
+// ---------------------------------------------------------------------------
+constexpr int kSelBits = 11;
+constexpr int kCandMax = 64;
+
+template <int VPT>
+__device__ double wave_select(const uint64_t (&key)[VPT], uint32_t kth, uint64_t kmin, uint64_t kmax,
+                              uint32_t* hist, uint64_t* cand) {
+  const int lane = threadIdx.x;
+  if (kmin == kmax) return dval(kmin);
+  int hi = 63 - __builtin_clzll(kmin ^ kmax);
+  uint64_t mask = (hi == 63) ? 0ull : ~((2ull << hi) - 1ull);
+  uint64_t prefix = kmin & mask;
+  uint32_t kk = kth;
+  uint32_t cnt = 0;
+  while (true) {
+    const int width = hi + 1 < kSelBits ? hi + 1 : kSelBits;
+    const int shift = hi + 1 - width;
+    const uint32_t nb = 1u << width, dm = nb - 1u;
+    for (uint32_t b = lane; b < nb; b += 64) hist[b] = 0u;
+    __syncthreads();
+#pragma unroll
+    for (int v = 0; v < VPT; ++v)
+      if ((key[v] & mask) == prefix) atomicAdd(&hist[(uint32_t)(key[v] >> shift) & dm], 1u);
+    __syncthreads();
+    // every lane owns nb/64 consecutive bins (nb <= 2048 -> <= 32 = 8 x uint4)
+    const uint32_t per = nb >= 64 ? nb / 64 : 1u;
+    const uint32_t b0 = (uint32_t)lane * per;
+    uint32_t g[8];  // per-group (4-bin) sums, compile-time indexed
+    uint32_t local = 0;
+    if (per >= 4) {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        g[q] = 0;
+        if ((uint32_t)q * 4 < per) {
+          const uint4 h4 = *reinterpret_cast<const uint4*>(&hist[b0 + 4 * q]);
+          g[q] = h4.x + h4.y + h4.z + h4.w;
+        }
+        local += g[q];
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) g[q] = 0;
+      for (uint32_t j = 0; j < per; ++j)
+        if (b0 + j < nb) local += hist[b0 + j];
+    }
+    uint32_t incl = local;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const uint32_t o = __shfl_up(incl, off, 64);
+      if (lane >= off) incl += o;
+    }
+    const uint32_t excl = incl - local;
+    const unsigned long long own = __ballot(excl <= kk && kk < incl);
+    const int owner = __ffsll((long long)own) - 1;
+    uint32_t bin = 0, before = 0, c = 0;
+    if (lane == owner) {
+      before = excl;
+      bin = b0;
+      if (per >= 4) {  // pick the 4-bin group, then the bin: no dependent LDS chain
+        uint32_t acc = excl;
+        int grp = 0;
+        bool stop = false;
+#pragma unroll
+        for (int q = 0; q < 7; ++q) {  // the rank lies in this lane: group <= 7
+          stop |= !((uint32_t)(q + 1) * 4 < per && kk >= acc + g[q]);
+          if (!stop) { acc += g[q]; grp = q + 1; }
+        }
+        const uint4 h4 = *reinterpret_cast<const uint4*>(&hist[b0 + 4 * grp]);
+        before = acc;
+        bin = b0 + 4 * grp;
+        c = h4.x;
+        if (kk >= before + c) { before += c; ++bin; c = h4.y;
+          if (kk >= before + c) { before += c; ++bin; c = h4.z;
+            if (kk >= before + c) { before += c; ++bin; c = h4.w; } } }
+      } else {
+        c = hist[bin];
+        while (kk >= before + c) {
+          before += c;
+          ++bin;
+          c = hist[bin];
+        }
+      }
+    }
+    bin = __shfl(bin, owner, 64);
+    before = __shfl(before, owner, 64);
+    cnt = __shfl(c, owner, 64);
+    kk -= before;
+    prefix |= (uint64_t)bin << shift;
+    mask |= (uint64_t)dm << shift;
+    hi = shift - 1;
+    if (cnt <= (uint32_t)kCandMax || hi < 0) break;
+    __syncthreads();  // histogram reads done before the next clear
+  }
+  if (hi < 0) return dval(prefix);
+  // compact the cnt survivors, then rank them exactly
+  uint32_t basec = 0;
+#pragma unroll
+  for (int v = 0; v < VPT; ++v) {
+    const bool m = (key[v] & mask) == prefix;
+    const unsigned long long bal = __ballot(m);
+    if (m) cand[basec + __popcll(bal & ((1ull << lane) - 1ull))] = key[v];
+    basec += (uint32_t)__popcll(bal);
+  }
+  __syncthreads();
+  const uint64_t mine = (uint32_t)lane < cnt ? cand[lane] : ~0ull;
+  uint32_t r = 0;
+  for (uint32_t j = 0; j < cnt; ++j) {
+    const uint64_t o = cand[j];
+    r += (o < mine) | ((o == mine) & (j < (uint32_t)lane));
+  }
+  const unsigned long long hit = __ballot((uint32_t)lane < cnt && r == kk);
+  const int who = __ffsll((long long)hit) - 1;
+  const uint64_t ans = __shfl(mine, who, 64);
+  return dval(ans);
+}
+
+template <int VPT>
+__global__ __launch_bounds__(64) void hb_eval_wave_kernel(
+    const double* __restrict__ t, const double* __restrict__ f, const double* __restrict__ isg,
+    long n, long kth, const WalkerConst* __restrict__ wcs, double* __restrict__ logl,
+    double* __restrict__ tmpl_out, int mode, int slab_bytes) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int lane = threadIdx.x;
+  const int wv = blockIdx.x;
+  double* vals = reinterpret_cast<double*>(smem);
+  uint32_t* hist = reinterpret_cast<uint32_t*>(smem);
+  uint64_t* cand = reinterpret_cast<uint64_t*>(smem + slab_bytes);
+  const WalkerConst& w = wcs[wv];
+
+  uint64_t kmn, kmx;
+  model_pass<64>(t, n, w, vals, lane, kmn, kmx);
+  kmn = wave_min_u64(kmn);
+  kmx = wave_max_u64(kmx);
+  __syncthreads();
+  uint64_t key[VPT];
+#pragma unroll
+  for (int v = 0; v < VPT; ++v) {
+    const long i = (long)v * 64 + lane;
+    key[v] = i < n ? dkey(vals[i]) : ~0ull;  // padding sorts last, never selected
+  }
+  __syncthreads();  // the slab becomes the histogram
+#if HB_ABLATE_SELECT
+  const double med = dval(kmn);
+#else
+  const double med = wave_select<VPT>(key, (uint32_t)kth, kmn, kmx, hist, cand);
+#endif
+
+  const double blend = w.blend, one_m_blend = 1.0 - w.blend, tune = w.tune;
+  if (mode == 1) {
+    double* o = tmpl_out + (size_t)wv * (size_t)n;
+#pragma unroll
+    for (int v = 0; v < VPT; ++v) {
+      const long i = (long)v * 64 + lane;
+      if (i < n) {
+        const double m = (dval(key[v]) - med) + 1.0;
+        o[i] = (blend + m * one_m_blend) * tune;
+      }
+    }
+    return;
+  }
+  double acc = 0.0;
+#pragma unroll
+  for (int v = 0; v < VPT; ++v) {
+    const long i = (long)v * 64 + lane;
+    if (i < n) {
+      double m = (dval(key[v]) - med) + 1.0;
+      m = (blend + m * one_m_blend) * tune;
+      const double r = (m - f[i]) * isg[i];
+      acc += r * r;
+    }
+  }
+  const double chi2 = wave_sum(acc);
+  if (lane == 0) {
     double c = chi2 + w.chi2_extra;
     if (w.roche != 0.0) c = kBig;
     logl[wv] = -c / 2.0;
@@ -379,10 +612,29 @@ static hipError_t launch_eval_t(const EvalPlan& pl, const double* t, const doubl
   return hipGetLastError();
 }
 
+template <int VPT>
+static hipError_t launch_wave_t(const EvalPlan& pl, const double* t, const double* f, const double* sg,
+                                const WalkerConst* wc, int nwalk, double* logl, double* tmpl, int mode,
+                                hipStream_t s) {
+  hipLaunchKernelGGL(hb_eval_wave_kernel<VPT>, dim3(nwalk), dim3(64), pl.lds_bytes, s, t, f, sg, pl.n, pl.kth,
+                     wc, logl, tmpl, mode, (int)pl.slab_bytes);
+  return hipGetLastError();
+}
+
 hipError_t launch_eval(const EvalPlan& pl, const double* t, const double* f, const double* sg,
                        const WalkerConst* wc, int nwalk, double* logl, double* tmpl, double* scratch,
                        int mode, hipStream_t s) {
   if (nwalk <= 0) return hipSuccess;
+  switch (pl.vpt) {
+    case 0: break;
+    case 1: return launch_wave_t<1>(pl, t, f, sg, wc, nwalk, logl, tmpl, mode, s);
+    case 2: return launch_wave_t<2>(pl, t, f, sg, wc, nwalk, logl, tmpl, mode, s);
+    case 4: return launch_wave_t<4>(pl, t, f, sg, wc, nwalk, logl, tmpl, mode, s);
+    case 8: return launch_wave_t<8>(pl, t, f, sg, wc, nwalk, logl, tmpl, mode, s);
+    case 16: return launch_wave_t<16>(pl, t, f, sg, wc, nwalk, logl, tmpl, mode, s);
+    case 32: return launch_wave_t<32>(pl, t, f, sg, wc, nwalk, logl, tmpl, mode, s);
+    default: return hipErrorInvalidValue;
+  }
 #define HB_CASE(NWV)                                                                              \
   case NWV:                                                                                       \
     return pl.lds ? launch_eval_t<NWV, true>(pl, t, f, sg, wc, nwalk, logl, tmpl, scratch, mode, s) \
@@ -426,6 +678,17 @@ EvalPlan make_plan(long n) {
   EvalPlan pl;
   pl.n = n;
   pl.kth = (n % 2 == 0) ? n / 2 : n / 2 + 1;  // likelihood3.c:97-99
+  if (n <= 64 * 32) {  // one wave per walker, keys in registers
+    int vpt = 1;
+    while ((long)vpt * 64 < n) vpt <<= 1;
+    pl.vpt = vpt;
+    pl.nw = 1;
+    pl.lds = true;
+    const size_t slab = (size_t)n * 8 > (size_t)(4u << kSelBits) ? (size_t)n * 8 : (size_t)(4u << kSelBits);
+    pl.slab_bytes = (slab + 15) & ~(size_t)15;
+    pl.lds_bytes = pl.slab_bytes + 8 * kCandMax;
+    return pl;
+  }
   const size_t lds_cap = 163840;
   const size_t need = sizeof(SelShared) + (size_t)n * sizeof(double);
   if (need <= lds_cap) {
