@@ -1,0 +1,38 @@
+"""Copy rocprofv3 outputs from gpurun_out/ into profiles/ (tracked) and derive
+per-launch HBM traffic for bench.py's roofline.traffic.
+
+    python scripts/summarize_prof.py TAG NCAD WALKERS
+
+HBM bytes per launch of hb_eval_* = (2 x FETCH_SIZE + WRITE_SIZE) [KiB] x 1024,
+FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM (gfx950 tallies 128-B requests
+at 64 B).  Counters were collected in separate --pmc passes.
+"""
+import csv, glob, json, os, shutil, sys
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+tag, ncad, walkers = sys.argv[1], int(sys.argv[2]), int(sys.argv[3])
+prof = os.path.join(ROOT, "profiles")
+src = os.path.join(ROOT, "gpurun_out")
+stats = glob.glob(os.path.join(src, f"prof_{tag}", "*kernel_stats.csv"))
+if stats:
+    shutil.copy(stats[0], os.path.join(prof, f"{tag}_kernel_stats.csv"))
+    print("kernel stats:", open(stats[0]).read()[:1500])
+vals = {}
+for f in glob.glob(os.path.join(src, f"pmc_{tag}", "*", "run_counter_collection.csv")):
+    for r in csv.DictReader(open(f)):
+        k = r["Kernel_Name"]
+        kern = "eval" if "hb_eval" in k else "prep" if "hb_prep" in k else None
+        if kern:
+            vals.setdefault(kern, {}).setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
+summary = {kern: {c: sum(v) / len(v) for c, v in d.items()} for kern, d in vals.items()}
+out = {"tag": tag, "ncad": ncad, "walkers": walkers, "per_dispatch_mean": summary}
+ev = summary.get("eval", {})
+if "FETCH_SIZE" in ev and "WRITE_SIZE" in ev:
+    hbm = (2 * ev["FETCH_SIZE"] + ev["WRITE_SIZE"]) * 1024
+    out["eval_hbm_bytes_per_launch"] = hbm
+    tj_path = os.path.join(prof, "pmc_traffic.json")
+    tj = json.load(open(tj_path)) if os.path.exists(tj_path) else {}
+    tj[f"N{ncad}_W{walkers}"] = {"hbm_bytes_per_launch": hbm, "source": f"profiles/{tag}_pmc_summary.json",
+                                 "formula": "(2*FETCH_SIZE + WRITE_SIZE)*1024, separate --pmc passes"}
+    json.dump(tj, open(tj_path, "w"), indent=1)
+json.dump(out, open(os.path.join(prof, f"{tag}_pmc_summary.json"), "w"), indent=1)
+print(json.dumps(out, indent=1)[:3000])

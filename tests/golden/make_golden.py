@@ -271,6 +271,12 @@ def sampler_fixture():
             fh.readline()
             out = np.loadtxt(fh)
         temps = np.array([np.loadtxt(os.path.join(tmp, "debug", f"temp_{j}_log.txt")) for j in range(50)])
+        lc_t, lc_f, lc_e = read_folded_lc(os.path.join(FOLDED, "127079833_new.txt"))
+        files = {}
+        for rel in (f"data/pars/par.{suf}.dat", f"data/subpars/subpar.{suf}.dat",
+                    f"data/lightcurves/mcmc_lightcurves/{suf}.out", "debug/temp_0_log.txt", "debug/temp_49_log.txt"):
+            with open(os.path.join(tmp, rel), "rb") as fh:
+                files[rel] = fh.read()
         # keep the exact text of the two main outputs as byte arrays for a textual compare
         with open(os.path.join(data, "chains", f"chain.{suf}.dat"), "rb") as fh:
             chain_txt = np.frombuffer(fh.read(), dtype=np.uint8)
@@ -278,7 +284,9 @@ def sampler_fixture():
             logl_txt = np.frombuffer(fh.read(), dtype=np.uint8)
         save("sampler_127079833.npz", niter=np.array([1200]), log10p_arg=np.array(["0.5021"]), run=np.array([0]),
              chain=chain, logl=logl, par=par, subpar=subpar, out=out, temps=temps, chain_txt=chain_txt,
-             logl_txt=logl_txt, stdout=np.array([r.stdout]))
+             logl_txt=logl_txt, stdout=np.array([r.stdout]), lc_t=lc_t, lc_f=lc_f, lc_e=lc_e,
+             file_names=np.array(list(files.keys())),
+             **{f"file{i}": np.frombuffer(v, dtype=np.uint8) for i, v in enumerate(files.values())})
     finally:
         shutil.rmtree(tmp, ignore_errors=True)
 
@@ -298,5 +306,13 @@ def main():
     sampler_fixture()
 
 
+def sampler_only():
+    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "all", "ref"], check=True)
+    sampler_fixture()
+
+
 if __name__ == "__main__":
-    main()
+    if len(sys.argv) > 1 and sys.argv[1] == "sampler":
+        sampler_only()
+    else:
+        main()
