@@ -26,6 +26,8 @@
 #include <functional>
 #include <mutex>
 #include <thread>
+#include <memory>
+#include <utility>
 
 #include "../../include/hb_sampler.h"
 #include "../../include/hbmi.h"
@@ -319,55 +321,392 @@ double now_s() {
 extern "C" double hb_ran2_parallel(long* idum, void* st) { return ran2p(idum, (RNG_Vars*)st); }
 extern "C" double hb_gasdev2_parallel(long* idum, void* st) { return gasdevp(idum, (RNG_Vars*)st); }
 
-extern "C" int hb_mcmc_run(const hb_mcmc_cfg* cfg, const double* t, const double* fl_data, const double* sigma,
-                           long n, hb_loglik_fn loglik, hb_model_fn model, void* user, hb_mcmc_result* res) {
-  if (!cfg || !loglik || cfg->nchains < 2 || cfg->npast < 2 || n < 2) return -1;
-  const int W = cfg->nchains, NPAST = cfg->npast;
-  const long NITER = cfg->niter;
-  if (cfg->ladder == 0 && W > 2000) return -2;  // 1.4^i overflows: the reference would hang
+// ---------------------------------------------------------------------------
+// Output files of mcmc_wrapper2.c (:110-173, :593-681), fed by slot.
+// ---------------------------------------------------------------------------
+struct hb_writer {
+  Files files;
+  int W = 0;
+  std::mutex mu;  // big-jump log lines come from the Hastings worker threads
+};
+
+extern "C" hb_writer* hb_writer_open(const char* root, const char* run_id, int run, int W) {
+  if (!root || !root[0] || W < 1) return nullptr;
+  hb_writer* w = new hb_writer();
+  w->W = W;
+  if (!open_files(w->files, root, run_id ? run_id : "run", run, W)) {
+    delete w;
+    return nullptr;
+  }
+  return w;
+}
+
+// iteration block of :593-649 (chain / logL / per-temperature logs); x_slots
+// and logl_slots are the post-swap states by temperature slot (slot 0 = cold)
+extern "C" int hb_writer_step(hb_writer* w, long iter, const double* logl_slots, const double* x_slots) {
+  if (!w) return -1;
+  Files& fl = w->files;
+  fprintf(fl.chain, "%ld %.12g ", iter / 10, logl_slots[0]);
+  for (int i = 0; i < kNp; ++i) fprintf(fl.chain, "%.12g ", x_slots[i]);
+  fprintf(fl.chain, "\n");
+  fprintf(fl.logl, "%ld ", iter / 10);
+  for (int i = 0; i < w->W; ++i) {
+    fprintf(fl.logl, "%.12g ", logl_slots[i]);
+    for (int jj = 0; jj < kNp; ++jj) fprintf(fl.temps[i], "%lf\t", x_slots[(size_t)i * kNp + jj]);
+    fprintf(fl.temps[i], "\n");
+  }
+  fprintf(fl.logl, "\n");
+  return 0;
+}
+
+extern "C" int hb_writer_lc(hb_writer* w, const double* t, const double* f, const double* m, long n) {
+  if (!w) return -1;
+  write_lc(w->files, t, f, m, n);
+  return 0;
+}
+
+// which = 0: subpar (every 100 iterations), 1: final par file
+extern "C" int hb_writer_pars(hb_writer* w, int which, const double* x) {
+  if (!w) return -1;
+  write_pars(which ? w->files.parname : w->files.subparname, x);
+  return 0;
+}
+
+extern "C" void hb_writer_close(hb_writer* w) {
+  if (!w) return;
+  Files& fl = w->files;
+  fclose(fl.log);
+  fclose(fl.chain);
+  fclose(fl.logl);
+  for (FILE* f : fl.temps) fclose(f);
+  if (fl.swap) fclose(fl.swap);
+  delete w;
+}
+
+// ---------------------------------------------------------------------------
+// The sampler state, owned by temperature SLOT.  The reference keeps chain
+// states by chain id and permutes index[] on a swap (:768-817); here slot j
+// holds the state of the chain currently at temperature j (plus that chain's
+// id and logL), so a contiguous slot range [lo, hi) can live on one rank and
+// a swap only moves the two chains' 21-double records.  With lo = 0, hi = W
+// this is exactly the single-process sampler.
+// ---------------------------------------------------------------------------
+constexpr int kRec = kNp + 2;  // x[21], logL, chain id
+
+struct hb_sampler {
+  int W = 0, NPAST = 0, lo = 0, hi = 0, nl = 0;
+  long NITER = 0;
+  double log_lc_period = 0, LC_PERIOD = 0;
+  Prior pr;
+  double sigma_p[kNp];
+  std::vector<double> temp;                    // W (the whole ladder)
+  std::vector<long> seeds;                     // nl
+  std::vector<RNG_Vars> states;                // nl
+  std::vector<double> x, logL, logP;           // nl x 21, nl, nl
+  std::vector<int> cid;                        // nl: chain id at the slot
+  std::vector<double> y, logPy, alpha2;        // proposals
+  std::vector<int> jump, jtype;
+  std::vector<double> hist;                    // nl x NPAST x 21
+  std::vector<const double*> hrow;
+  std::vector<int> acc_arr, DEacc_arr, DEtrial_arr;
+  long acc = 0, DEacc = 0, DEtrial = 0, atrial = 0, cold_acc = 0, nswap = 0;
+  std::vector<int> perm;                        // W, scratch of swap()
+  std::vector<double> Lperm;                    // W
+  std::vector<double> old;                      // nl x kRec, scratch of apply_perm()
+  hb_writer* log = nullptr;
+  Pool* pool = nullptr;
+  ~hb_sampler() { delete pool; }
+};
+
+extern "C" hb_sampler* hb_sampler_create(const hb_mcmc_cfg* cfg, int slot_lo, int slot_hi) {
+  if (!cfg || cfg->nchains < 2 || cfg->npast < 2) return nullptr;
+  const int W = cfg->nchains;
+  if (cfg->ladder == 0 && W > 2000) return nullptr;  // 1.4^i overflows: the reference would hang
+  if (slot_lo < 0 || slot_hi > W || slot_lo >= slot_hi) return nullptr;
+  hb_sampler* s = new hb_sampler();
+  s->W = W;
+  s->NPAST = cfg->npast;
+  s->NITER = cfg->niter;
+  s->lo = slot_lo;
+  s->hi = slot_hi;
+  s->nl = slot_hi - slot_lo;
   int nth = cfg->nthreads;
   if (nth <= 0) {
     const unsigned hw = std::thread::hardware_concurrency();
     nth = hw == 0 ? 1 : (int)(hw > 16 ? 16 : hw);
   }
-  Pool pool(nth);
-  std::mutex log_mu;
-  const double log_lc_period = cfg->log10_period;
-  const double LC_PERIOD = pow(10., log_lc_period);
-  srand((unsigned)NITER);  // :86
+  s->pool = new Pool(nth);
+  s->log_lc_period = cfg->log10_period;
+  s->LC_PERIOD = pow(10., s->log_lc_period);
+  srand((unsigned)s->NITER);  // :86 (every rank replays the same swap draws)
+  const int nl = s->nl;
 
-  std::vector<long> seeds(W);
-  std::vector<RNG_Vars> states(W);
-  for (int i = 0; i < W; ++i) {  // :88-106
-    seeds[i] = i + cfg->run;
-    memset(&states[i], 0, sizeof(RNG_Vars));
-    states[i].idum2 = 123456789;
-  }
-  Prior pr;
-  set_limits(pr.limited, pr.limits, pr.gp, LC_PERIOD);  // :195
-  double sigma_p[kNp];
-  initialize_proposals(sigma_p, nullptr);  // :198
-
-  // random initial state from chain 0's stream (USE_RAND_PARS=1, :233-252)
-  std::vector<double> x((size_t)W * kNp), xmap(kNp);
+  // chain 0's stream draws the initial states of ALL chains (USE_RAND_PARS=1,
+  // :233-252); every rank replays it and keeps its own slots
+  RNG_Vars st0;
+  memset(&st0, 0, sizeof st0);
+  st0.idum2 = 123456789;
+  long seed0 = 0 + cfg->run;
+  set_limits(s->pr.limited, s->pr.limits, s->pr.gp, s->LC_PERIOD);  // :195
+  initialize_proposals(s->sigma_p, nullptr);                           // :198
+  s->x.resize((size_t)nl * kNp);
   for (int i = 0; i < kNp; ++i)
     for (int j = 0; j < W; ++j) {
-      const double u = ran2p(&seeds[0], &states[0]);
-      double v = pr.limits[i].lo + u * (pr.limits[i].hi - pr.limits[i].lo);
-      if (i == 2) v = log_lc_period;
-      if (i == 6) v = fmod(v, LC_PERIOD);
-      x[(size_t)j * kNp + i] = v;
+      const double u = ran2p(&seed0, &st0);
+      double v = s->pr.limits[i].lo + u * (s->pr.limits[i].hi - s->pr.limits[i].lo);
+      if (i == 2) v = s->log_lc_period;
+      if (i == 6) v = fmod(v, s->LC_PERIOD);
+      if (j >= slot_lo && j < slot_hi) s->x[(size_t)(j - slot_lo) * kNp + i] = v;
     }
-
-  std::vector<double> temp(W);
-  std::vector<int> index(W);
-  const double dtemp = 1.4;  // :331-339
-  temp[0] = 1.0;
-  index[0] = 0;
-  for (int i = 1; i < W; ++i) {
-    temp[i] = (cfg->ladder == 1 && i % 50 == 0) ? 1.0 : temp[i - 1] * dtemp;
-    index[i] = i;
+  s->seeds.resize(nl);
+  s->states.resize(nl);
+  for (int jl = 0; jl < nl; ++jl) {  // :88-106
+    s->seeds[jl] = slot_lo + jl + cfg->run;
+    memset(&s->states[jl], 0, sizeof(RNG_Vars));
+    s->states[jl].idum2 = 123456789;
   }
+  if (slot_lo == 0) {  // chain 0 continues its stream after the initial draws
+    s->seeds[0] = seed0;
+    s->states[0] = st0;
+  }
+
+  s->temp.resize(W);
+  s->temp[0] = 1.0;  // :331-339
+  for (int i = 1; i < W; ++i) s->temp[i] = (cfg->ladder == 1 && i % 50 == 0) ? 1.0 : s->temp[i - 1] * 1.4;
+
+  s->logL.assign(nl, 0.0);
+  s->logP.assign(nl, 0.0);
+  s->cid.resize(nl);
+  for (int jl = 0; jl < nl; ++jl) s->cid[jl] = slot_lo + jl;
+  s->y.resize((size_t)nl * kNp);
+  s->logPy.resize(nl);
+  s->alpha2.resize(nl);
+  s->jump.resize(nl);
+  s->jtype.resize(nl);
+  s->hist.assign((size_t)nl * s->NPAST * kNp, 0.0);
+  s->hrow.resize((size_t)nl * s->NPAST);
+  for (size_t r = 0; r < s->hrow.size(); ++r) s->hrow[r] = &s->hist[r * kNp];
+  s->acc_arr.assign(nl, 0);
+  s->DEacc_arr.assign(nl, 0);
+  s->DEtrial_arr.assign(nl, 0);
+  s->perm.resize(W);
+  s->Lperm.resize(W);
+  s->old.resize((size_t)nl * kRec);
+  return s;
+}
+
+extern "C" void hb_sampler_destroy(hb_sampler* s) { delete s; }
+
+extern "C" int hb_sampler_attach_log(hb_sampler* s, hb_writer* w) {
+  if (!s) return -1;
+  s->log = w;
+  return 0;
+}
+
+// current states / logL / chain ids of the owned slots
+extern "C" int hb_sampler_get(const hb_sampler* s, double* x_out, double* logl_out, int* cid_out) {
+  if (!s) return -1;
+  if (x_out) memcpy(x_out, s->x.data(), sizeof(double) * s->x.size());
+  if (logl_out) memcpy(logl_out, s->logL.data(), sizeof(double) * s->nl);
+  if (cid_out) memcpy(cid_out, s->cid.data(), sizeof(int) * s->nl);
+  return 0;
+}
+
+// logL of the current states (the reference's recompute at :488, which only
+// changes anything at iteration 0)
+extern "C" int hb_sampler_set_logl(hb_sampler* s, const double* logl) {
+  if (!s || !logl) return -1;
+  memcpy(s->logL.data(), logl, sizeof(double) * s->nl);
+  return 0;
+}
+
+// proposals of the owned slots (:386-485); y_out: nl x 21
+extern "C" int hb_sampler_propose(hb_sampler* s, long iter, double* y_out) {
+  if (!s) return -1;
+  const int NPAST = s->NPAST, lo = s->lo;
+  s->pool->run(s->nl, [&](int jl) {
+    RNG_Vars* st = &s->states[jl];
+    long* sd = &s->seeds[jl];
+    const int j = lo + jl;
+    const int chain_id = s->cid[jl];
+    const double* xc = &s->x[(size_t)jl * kNp];
+    double* yj = &s->y[(size_t)jl * kNp];
+    const double a = ran2p(sd, st);
+    const double jscale = pow(10., -6. + 6. * a);
+    int jmp = 0, jt = 0;
+    if ((ran2p(sd, st) < 0.5) && (iter > NPAST)) jmp = 1;
+    if (jmp == 0) {
+      gaussian_step(xc, sd, s->sigma_p, jscale, s->temp[j], yj, st);
+      jt = 1;
+    }
+    if (jmp == 1) {
+      if (chain_id == 0) s->DEtrial_arr[jl]++;
+      de_step(xc, sd, &s->hrow[(size_t)jl * NPAST], NPAST, yj, st);
+      jt = 2;
+      double dx_mag = 0;
+      for (int i = 0; i < kNp; ++i) dx_mag += (xc[i] - yj[i]) * (xc[i] - yj[i]);
+      if (dx_mag < 1e-6) {
+        gaussian_step(xc, sd, s->sigma_p, jscale, s->temp[j], yj, st);
+        jt = 1;
+      }
+    }
+    apply_walls(yj, s->pr);
+    if (yj[1] > yj[0]) {  // "order the masses" (:470-475): y[1] = y[0], as written
+      yj[1] = yj[0];
+      yj[0] = yj[1];
+    }
+    yj[2] = s->log_lc_period;
+    yj[6] = fmod(yj[6], s->LC_PERIOD);
+    s->logP[jl] = log_prior(xc, s->pr);
+    s->logPy[jl] = log_prior(yj, s->pr);
+    s->jump[jl] = jmp;
+    s->jtype[jl] = jt;
+    s->alpha2[jl] = ran2p(sd, st);  // drawn after the likelihood calls in the reference; same stream order
+  });
+  if (y_out) memcpy(y_out, s->y.data(), sizeof(double) * s->y.size());
+  return 0;
+}
+
+// Hastings test and history (:492-546) for the owned slots; logly: nl
+extern "C" int hb_sampler_accept(hb_sampler* s, long iter, const double* logly) {
+  if (!s || !logly) return -1;
+  const int NPAST = s->NPAST, lo = s->lo;
+  const int k = (int)(iter - (iter / NPAST) * NPAST);
+  s->pool->run(s->nl, [&](int jl) {
+    const int j = lo + jl;
+    const int chain_id = s->cid[jl];
+    double* xc = &s->x[(size_t)jl * kNp];
+    const double* yj = &s->y[(size_t)jl * kNp];
+    const double H = exp((logly[jl] - s->logL[jl]) / s->temp[j] + (s->logPy[jl] - s->logP[jl]));
+    if (s->alpha2[jl] <= H) {
+      if ((s->logL[jl] / logly[jl] <= 0.5) && (iter > 10000) && (j <= 5) && s->log) {
+        std::lock_guard<std::mutex> lk(s->log->mu);
+        log_big_jump(s->log->files.log, iter, chain_id, H, s->alpha2[jl], s->temp[j], s->logL[jl], logly[jl],
+                     s->logP[jl], s->logPy[jl], xc, yj, s->jtype[jl]);
+      }
+      if (chain_id == 0) s->acc_arr[jl]++;
+      memcpy(xc, yj, sizeof(double) * kNp);
+      s->logL[jl] = logly[jl];
+      if ((s->jump[jl] == 1) && (chain_id == 0)) s->DEacc_arr[jl]++;
+    }
+    memcpy(&s->hist[((size_t)jl * NPAST + k) * kNp], xc, sizeof(double) * kNp);
+  });
+  // statistics of the swap loop (:554-558): acc_arr is cleared every step,
+  // the DE counters only every 100 steps (:640), so DEacc/DEtrial add up
+  // running totals -- reproduced as written
+  for (int jl = 0; jl < s->nl; ++jl) {
+    s->acc += s->acc_arr[jl];
+    s->cold_acc += s->acc_arr[jl];
+    s->DEacc += s->DEacc_arr[jl];
+    s->DEtrial += s->DEtrial_arr[jl];
+    s->acc_arr[jl] = 0;
+  }
+  return 0;
+}
+
+// Tempering swaps (ptmcmc, :768-817), W sequential attempts on glibc rand().
+// logl_all: logL by slot for ALL W slots; every rank replays the same draws
+// on the same values and so reaches the same permutation.  perm_out[j] = the
+// slot whose chain sits at slot j afterwards; logl_perm_out (optional) the
+// permuted logL.  Returns the number of accepted swaps.
+extern "C" int hb_sampler_swap(hb_sampler* s, const double* logl_all, int* perm_out, double* logl_perm_out) {
+  if (!s || !logl_all) return -1;
+  const int W = s->W;
+  int* p = s->perm.data();
+  double* L = s->Lperm.data();
+  for (int j = 0; j < W; ++j) {
+    p[j] = j;
+    L[j] = logl_all[j];
+  }
+  int n = 0;
+  for (int i = 0; i < W; ++i) {
+    const int b = (int)(((double)rand() / (RAND_MAX)) * ((double)(W - 1)));
+    const int a = b + 1;
+    const double heat1 = s->temp[a], heat2 = s->temp[b];
+    const double dlogL = L[b] - L[a];
+    const double Hs = (heat2 - heat1) / (heat2 * heat1);
+    const double al = exp(dlogL * Hs);
+    const double be = ((double)rand() / (RAND_MAX));
+    if (al >= be) {
+      std::swap(p[a], p[b]);
+      std::swap(L[a], L[b]);
+      ++n;
+    }
+  }
+  s->nswap += n;
+  if (perm_out) memcpy(perm_out, p, sizeof(int) * W);
+  if (logl_perm_out) memcpy(logl_perm_out, L, sizeof(double) * W);
+  return n;
+}
+
+// record {x[21], logL, chain id} of an owned slot
+extern "C" int hb_sampler_pack(const hb_sampler* s, int slot, double* rec) {
+  if (!s || slot < s->lo || slot >= s->hi) return -1;
+  const int jl = slot - s->lo;
+  memcpy(rec, &s->x[(size_t)jl * kNp], sizeof(double) * kNp);
+  rec[kNp] = s->logL[jl];
+  rec[kNp + 1] = (double)s->cid[jl];
+  return 0;
+}
+
+// Moves the chains to their slots after swap(): owned slot j takes the chain
+// of slot perm[j]; when that slot is owned by another rank its record comes
+// from remote[(j - lo) * 23 ...] (filled by the caller's exchange).
+extern "C" int hb_sampler_apply_perm(hb_sampler* s, const int* perm, const double* remote) {
+  if (!s || !perm) return -1;
+  const int nl = s->nl, lo = s->lo, hi = s->hi;
+  for (int jl = 0; jl < nl; ++jl) hb_sampler_pack(s, lo + jl, &s->old[(size_t)jl * kRec]);
+  for (int jl = 0; jl < nl; ++jl) {
+    const int src = perm[lo + jl];
+    const double* r;
+    if (src >= lo && src < hi) {
+      r = &s->old[(size_t)(src - lo) * kRec];
+    } else {
+      if (!remote) return -2;
+      r = &remote[(size_t)jl * kRec];
+    }
+    memcpy(&s->x[(size_t)jl * kNp], r, sizeof(double) * kNp);
+    s->logL[jl] = r[kNp];
+    s->cid[jl] = (int)r[kNp + 1];
+  }
+  return 0;
+}
+
+// running statistics of the owned slots: {acc, DEacc, DEtrial, atrial,
+// cold_acc, nswap}; end_iter() does :590 and the 100-step reset of :639-641
+extern "C" int hb_sampler_stats(const hb_sampler* s, long* out6) {
+  if (!s || !out6) return -1;
+  out6[0] = s->acc;
+  out6[1] = s->DEacc;
+  out6[2] = s->DEtrial;
+  out6[3] = s->atrial;
+  out6[4] = s->cold_acc;
+  out6[5] = s->nswap;
+  return 0;
+}
+
+extern "C" int hb_sampler_end_iter(hb_sampler* s, long iter) {
+  if (!s) return -1;
+  s->atrial++;
+  if (iter % 100 == 0) {
+    s->acc = s->atrial = 0;
+    for (int jl = 0; jl < s->nl; ++jl) s->DEtrial_arr[jl] = s->DEacc_arr[jl] = s->acc_arr[jl] = 0;
+  }
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
+// Single-process driver (all W slots local): the mcmc_wrapper2.c main loop.
+// ---------------------------------------------------------------------------
+extern "C" int hb_mcmc_run(const hb_mcmc_cfg* cfg, const double* t, const double* fl_data, const double* sigma,
+                           long n, hb_loglik_fn loglik, hb_model_fn model, void* user, hb_mcmc_result* res) {
+  if (!cfg || !loglik || cfg->nchains < 2 || cfg->npast < 2 || n < 2) return -1;
+  if (cfg->ladder == 0 && cfg->nchains > 2000) return -2;
+  const int W = cfg->nchains;
+  const long NITER = cfg->niter;
+  std::unique_ptr<hb_sampler, void (*)(hb_sampler*)> sp(hb_sampler_create(cfg, 0, W), hb_sampler_destroy);
+  if (!sp) return -1;
+  hb_sampler* s = sp.get();
 
   double t_loglik = 0.;
   long n_evals = 0;
@@ -379,175 +718,66 @@ extern "C" int hb_mcmc_run(const hb_mcmc_cfg* cfg, const double* t, const double
     return rc;
   };
 
-  std::vector<double> logLx(W), logPx(W);
+  std::vector<double> xmap(kNp);
   double logLmap;
-  if (eval(x.data(), 1, &logLmap)) return -3;  // :342 (chain 0's state)
-  for (int i = 0; i < W; ++i) logLx[i] = logLmap;
-  for (int i = 0; i < kNp; ++i) xmap[i] = x[i];  // xmap is uninitialised in the reference; only printed after updates
+  if (eval(s->x.data(), 1, &logLmap)) return -3;  // :342 (chain 0's state)
+  memcpy(xmap.data(), s->x.data(), sizeof(double) * kNp);  // uninitialised in the reference; only printed after updates
   if (cfg->verbose) printf("initial chi2 and likelihood %lf \t %lf\n", -2 * logLmap, logLmap);
 
-  Files files;
+  std::unique_ptr<hb_writer, void (*)(hb_writer*)> wr(nullptr, hb_writer_close);
   if (cfg->out_root && cfg->out_root[0]) {
-    if (!open_files(files, cfg->out_root, cfg->run_id ? cfg->run_id : "run", cfg->run, W)) return -4;
+    wr.reset(hb_writer_open(cfg->out_root, cfg->run_id, cfg->run, W));
+    if (!wr) return -4;
+    hb_sampler_attach_log(s, wr.get());
   }
-  std::vector<double> model_buf(model ? n : 0);
-
-  // history[j][k][:] (NPAST x 21 per temperature slot)
-  std::vector<double> hist((size_t)W * NPAST * kNp, 0.0);
-  std::vector<const double*> hrow((size_t)W * NPAST);
-  for (size_t r = 0; r < hrow.size(); ++r) hrow[r] = &hist[r * kNp];
-
-  std::vector<int> acc_arr(W, 0), DEacc_arr(W, 0), DEtrial_arr(W, 0);
-  std::vector<double> y((size_t)W * kNp), logLy(W), logPy(W), alpha2(W), xcur((size_t)W * kNp);
-  std::vector<int> jump(W), jtype(W);
-  long acc = 0, DEacc = 0, DEtrial = 0, atrial = 0;
-  long cold_acc = 0, nswap = 0;
+  std::vector<double> model_buf(model ? n : 0), logly(W), lx(W);
   const double t_start = now_s();
 
   for (long iter = 0; iter < NITER; ++iter) {
-    const int k = (int)(iter - (iter / NPAST) * NPAST);
-    // ---- proposals (:386-485), one RNG stream per temperature slot j ----
-    pool.run(W, [&](int j) {
-      RNG_Vars* st = &states[j];
-      long* sd = &seeds[j];
-      const int chain_id = index[j];
-      const double* xc = &x[(size_t)chain_id * kNp];
-      double* yj = &y[(size_t)j * kNp];
-      const double a = ran2p(sd, st);
-      const double jscale = pow(10., -6. + 6. * a);
-      int jmp = 0, jt = 0;
-      if ((ran2p(sd, st) < 0.5) && (iter > NPAST)) jmp = 1;
-      if (jmp == 0) {
-        gaussian_step(xc, sd, sigma_p, jscale, temp[j], yj, st);
-        jt = 1;
-      }
-      if (jmp == 1) {
-        if (chain_id == 0) DEtrial_arr[j]++;
-        de_step(xc, sd, &hrow[(size_t)j * NPAST], NPAST, yj, st);
-        jt = 2;
-        double dx_mag = 0;
-        for (int i = 0; i < kNp; ++i) dx_mag += (xc[i] - yj[i]) * (xc[i] - yj[i]);
-        if (dx_mag < 1e-6) {
-          gaussian_step(xc, sd, sigma_p, jscale, temp[j], yj, st);
-          jt = 1;
-        }
-      }
-      apply_walls(yj, pr);
-      if (yj[1] > yj[0]) {  // "order the masses" (:470-475): y[1] = y[0], as written
-        const double keep = yj[1];
-        (void)keep;
-        yj[1] = yj[0];
-        yj[0] = yj[1];
-      }
-      yj[2] = log_lc_period;
-      yj[6] = fmod(yj[6], LC_PERIOD);
-      logPx[chain_id] = log_prior(xc, pr);
-      logPy[j] = log_prior(yj, pr);
-      jump[j] = jmp;
-      jtype[j] = jt;
-      alpha2[j] = ran2p(sd, st);  // drawn after the likelihood calls in the reference; same stream order
-    });
-    // ---- likelihoods: one batch (two at iteration 0) ----
-    if (iter == 0) {
-      for (int j = 0; j < W; ++j)
-        memcpy(&xcur[(size_t)j * kNp], &x[(size_t)index[j] * kNp], sizeof(double) * kNp);
-      std::vector<double> lx(W);
-      if (eval(xcur.data(), W, lx.data())) return -3;
-      for (int j = 0; j < W; ++j) logLx[index[j]] = lx[j];
+    hb_sampler_propose(s, iter, nullptr);
+    if (iter == 0) {  // every chain's current state (see header)
+      if (eval(s->x.data(), W, lx.data())) return -3;
+      hb_sampler_set_logl(s, lx.data());
     }
-    if (eval(y.data(), W, logLy.data())) return -3;
-    // ---- Hastings test and history (:492-546) ----
-    pool.run(W, [&](int j) {
-      const int chain_id = index[j];
-      double* xc = &x[(size_t)chain_id * kNp];
-      const double* yj = &y[(size_t)j * kNp];
-      const double H = exp((logLy[j] - logLx[chain_id]) / temp[j] + (logPy[j] - logPx[chain_id]));
-      if (alpha2[j] <= H) {
-        if ((logLx[chain_id] / logLy[j] <= 0.5) && (iter > 10000) && (j <= 5) && files.on) {
-          std::lock_guard<std::mutex> lk(log_mu);
-          log_big_jump(files.log, iter, chain_id, H, alpha2[j], temp[j], logLx[chain_id], logLy[j],
-                       logPx[chain_id], logPy[j], xc, yj, jtype[j]);
-        }
-        if (chain_id == 0) acc_arr[j]++;
-        memcpy(xc, yj, sizeof(double) * kNp);
-        logLx[chain_id] = logLy[j];
-        if ((jump[j] == 1) && (chain_id == 0)) DEacc_arr[j]++;
-      }
-      memcpy(&hist[((size_t)j * NPAST + k) * kNp], xc, sizeof(double) * kNp);
-    });
-    // ---- statistics and tempering swaps (:554-563) ----
-    for (int i = 0; i < W; ++i) {
-      acc += acc_arr[i];
-      cold_acc += acc_arr[i];
-      DEacc += DEacc_arr[i];
-      DEtrial += DEtrial_arr[i];
-      acc_arr[i] = 0;
-      // ptmcmc (:768-817)
-      const int b = (int)(((double)rand() / (RAND_MAX)) * ((double)(W - 1)));
-      const int a = b + 1;
-      const int olda = index[a], oldb = index[b];
-      const double heat1 = temp[a], heat2 = temp[b];
-      const double dlogL = logLx[oldb] - logLx[olda];
-      const double Hs = (heat2 - heat1) / (heat2 * heat1);
-      const double al = exp(dlogL * Hs);
-      const double be = ((double)rand() / (RAND_MAX));
-      if (al >= be) {
-        index[a] = oldb;
-        index[b] = olda;
-        ++nswap;
-      }
-    }
-    if (logLx[index[0]] > logLmap) {  // :565-572
-      memcpy(xmap.data(), &x[(size_t)index[0] * kNp], sizeof(double) * kNp);
-      logLmap = logLx[index[0]];
+    if (eval(s->y.data(), W, logly.data())) return -3;
+    hb_sampler_accept(s, iter, logly.data());
+    hb_sampler_swap(s, s->logL.data(), nullptr, nullptr);
+    hb_sampler_apply_perm(s, s->perm.data(), nullptr);
+    if (s->logL[0] > logLmap) {  // :565-572
+      memcpy(xmap.data(), s->x.data(), sizeof(double) * kNp);
+      logLmap = s->logL[0];
     }
     if (cfg->verbose && iter % 1000 == 0) {  // :575-589
-      printf("%ld/%ld logL=%.10g acc=%.3g DEacc=%.3g", iter, NITER, logLx[index[0]], (double)(acc) / ((double)atrial),
-             (double)DEacc / (double)DEtrial);
+      printf("%ld/%ld logL=%.10g acc=%.3g DEacc=%.3g", iter, NITER, s->logL[0], (double)(s->acc) / ((double)s->atrial),
+             (double)s->DEacc / (double)s->DEtrial);
       printf("\n");
       printf("Parameter values: \n");
-      for (int i = 0; i < 5; ++i) printf("%lf\t", x[(size_t)index[W > 10 ? 10 : W - 1] * kNp + i]);
+      for (int i = 0; i < 5; ++i) printf("%lf\t", s->x[(size_t)(W > 10 ? 10 : W - 1) * kNp + i]);
       printf("\n");
     }
-    atrial++;
-    if ((iter % 100 == 0) && files.on) {  // :593-649
-      fprintf(files.chain, "%ld %.12g ", iter / 10, logLx[index[0]]);
-      for (int i = 0; i < kNp; ++i) fprintf(files.chain, "%.12g ", x[(size_t)index[0] * kNp + i]);
-      fprintf(files.chain, "\n");
-      fprintf(files.logl, "%ld ", iter / 10);
-      for (int i = 0; i < W; ++i) {
-        fprintf(files.logl, "%.12g ", logLx[index[i]]);
-        for (int jj = 0; jj < kNp; ++jj) fprintf(files.temps[i], "%lf\t", x[(size_t)index[i] * kNp + jj]);
-        fprintf(files.temps[i], "\n");
-      }
-      fprintf(files.logl, "\n");
-      acc = atrial = 0;
-      for (int i = 0; i < W; ++i) DEtrial_arr[i] = DEacc_arr[i] = acc_arr[i] = 0;
+    if ((iter % 100 == 0) && wr) {  // :593-649
+      hb_writer_step(wr.get(), iter, s->logL.data(), s->x.data());
       if (model) {
         if (model(user, xmap.data(), model_buf.data())) return -5;
-        write_lc(files, t, fl_data, model_buf.data(), n);
+        hb_writer_lc(wr.get(), t, fl_data, model_buf.data(), n);
       }
-      write_pars(files.subparname, &x[(size_t)index[0] * kNp]);
+      hb_writer_pars(wr.get(), 0, s->x.data());
     }
+    hb_sampler_end_iter(s, iter);
   }
-  if (files.on) {  // :655-681
+  if (wr) {  // :655-681
     if (model) {
       if (model(user, xmap.data(), model_buf.data())) return -5;
-      write_lc(files, t, fl_data, model_buf.data(), n);
+      hb_writer_lc(wr.get(), t, fl_data, model_buf.data(), n);
     }
-    write_pars(files.parname, &x[(size_t)index[0] * kNp]);
-    fclose(files.log);
-    fclose(files.chain);
-    fclose(files.logl);
-    for (FILE* f : files.temps) fclose(f);
-    if (files.swap) fclose(files.swap);
+    hb_writer_pars(wr.get(), 1, s->x.data());
   }
   (void)sigma;
   if (res) {
     memcpy(res->xmap, xmap.data(), sizeof(double) * kNp);
     res->logLmap = logLmap;
-    res->accepted = cold_acc;
-    res->swaps = nswap;
+    res->accepted = s->cold_acc;
+    res->swaps = s->nswap;
     res->seconds_total = now_s() - t_start;
     res->seconds_loglik = t_loglik;
     res->loglik_evals = n_evals;

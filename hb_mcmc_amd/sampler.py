@@ -43,8 +43,142 @@ def _declare(lib):
     lib.hb_ran2_parallel.argtypes = [C.POINTER(C.c_long), C.c_void_p]
     lib.hb_gasdev2_parallel.restype = C.c_double
     lib.hb_gasdev2_parallel.argtypes = [C.POINTER(C.c_long), C.c_void_p]
+    vp, pd, pi = C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_int)
+    for name, res, args in (
+            ("hb_sampler_create", vp, [C.POINTER(MCMCConfig), C.c_int, C.c_int]),
+            ("hb_sampler_destroy", None, [vp]),
+            ("hb_sampler_attach_log", C.c_int, [vp, vp]),
+            ("hb_sampler_get", C.c_int, [vp, pd, pd, pi]),
+            ("hb_sampler_set_logl", C.c_int, [vp, pd]),
+            ("hb_sampler_propose", C.c_int, [vp, C.c_long, pd]),
+            ("hb_sampler_accept", C.c_int, [vp, C.c_long, pd]),
+            ("hb_sampler_swap", C.c_int, [vp, pd, pi, pd]),
+            ("hb_sampler_pack", C.c_int, [vp, C.c_int, pd]),
+            ("hb_sampler_apply_perm", C.c_int, [vp, pi, pd]),
+            ("hb_sampler_stats", C.c_int, [vp, C.POINTER(C.c_long)]),
+            ("hb_sampler_end_iter", C.c_int, [vp, C.c_long]),
+            ("hb_writer_open", vp, [C.c_char_p, C.c_char_p, C.c_int, C.c_int]),
+            ("hb_writer_step", C.c_int, [vp, C.c_long, pd, pd]),
+            ("hb_writer_lc", C.c_int, [vp, pd, pd, pd, C.c_long]),
+            ("hb_writer_pars", C.c_int, [vp, C.c_int, pd]),
+            ("hb_writer_close", None, [vp])):
+        fn = getattr(lib, name)
+        fn.restype, fn.argtypes = res, args
     lib._hb_sampler_declared = True
     return lib
+
+
+REC = 23  # HB_SAMPLER_REC: x[21], logL, chain id
+
+
+def _pd(a):
+    return a.ctypes.data_as(C.POINTER(C.c_double))
+
+
+def _ok(rc, what):
+    if rc != 0:
+        raise _lib.HBMIError(f"{what} failed ({rc})")
+
+
+class SlotSampler:
+    """The phase API of include/hb_sampler.h for temperature slots [lo, hi)
+    of an `nchains` ladder (one rank's share; lo=0, hi=nchains = everything)."""
+
+    def __init__(self, niter, nchains, log10_period, lo, hi, run=0, npast=500, ladder=0, nthreads=0):
+        self.lib = _declare(_lib.lib())
+        self.cfg = MCMCConfig(int(niter), int(nchains), int(npast), int(run), float(log10_period), int(ladder),
+                              int(nthreads), 0, b"", b"run")
+        self.W, self.lo, self.hi, self.nl = int(nchains), int(lo), int(hi), int(hi) - int(lo)
+        self._h = self.lib.hb_sampler_create(C.byref(self.cfg), self.lo, self.hi)
+        if not self._h:
+            raise _lib.HBMIError("hb_sampler_create rejected the configuration")
+        self.y = np.empty((self.nl, 21))
+        self.perm = np.empty(self.W, dtype=np.int32)
+        self.logl_perm = np.empty(self.W)
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self.lib.hb_sampler_destroy(self._h)
+            self._h = None
+
+    __del__ = close
+
+    def get(self):
+        x, ll, cid = np.empty((self.nl, 21)), np.empty(self.nl), np.empty(self.nl, dtype=np.int32)
+        _ok(self.lib.hb_sampler_get(self._h, _pd(x), _pd(ll), cid.ctypes.data_as(C.POINTER(C.c_int))),
+            "hb_sampler_get")
+        return x, ll, cid
+
+    def set_logl(self, logl):
+        logl = np.ascontiguousarray(logl, dtype=np.float64)
+        _ok(self.lib.hb_sampler_set_logl(self._h, _pd(logl)), "hb_sampler_set_logl")
+
+    def propose(self, it):
+        _ok(self.lib.hb_sampler_propose(self._h, int(it), _pd(self.y)), "hb_sampler_propose")
+        return self.y
+
+    def accept(self, it, logly):
+        logly = np.ascontiguousarray(logly, dtype=np.float64)
+        _ok(self.lib.hb_sampler_accept(self._h, int(it), _pd(logly)), "hb_sampler_accept")
+
+    def swap(self, logl_all):
+        logl_all = np.ascontiguousarray(logl_all, dtype=np.float64)
+        n = self.lib.hb_sampler_swap(self._h, _pd(logl_all), self.perm.ctypes.data_as(C.POINTER(C.c_int)),
+                                     _pd(self.logl_perm))
+        if n < 0:
+            raise _lib.HBMIError("hb_sampler_swap failed")
+        return self.perm, self.logl_perm
+
+    def pack(self, slots):
+        out = np.empty((len(slots), REC))
+        for i, j in enumerate(slots):
+            _ok(self.lib.hb_sampler_pack(self._h, int(j), _pd(out[i])), "hb_sampler_pack")
+        return out
+
+    def apply_perm(self, perm, remote=None):
+        perm = np.ascontiguousarray(perm, dtype=np.int32)
+        rp = None if remote is None else _pd(np.ascontiguousarray(remote, dtype=np.float64))
+        _ok(self.lib.hb_sampler_apply_perm(self._h, perm.ctypes.data_as(C.POINTER(C.c_int)), rp),
+            "hb_sampler_apply_perm")
+
+    def stats(self):
+        out = (C.c_long * 6)()
+        _ok(self.lib.hb_sampler_stats(self._h, out), "hb_sampler_stats")
+        return dict(zip(("acc", "DEacc", "DEtrial", "atrial", "cold_acc", "nswap"), out[:]))
+
+    def end_iter(self, it):
+        _ok(self.lib.hb_sampler_end_iter(self._h, int(it)), "hb_sampler_end_iter")
+
+
+class Writer:
+    """The reference's output files (mcmc_wrapper2.c:110-173, :593-681)."""
+
+    def __init__(self, root, run_id, run, nchains):
+        self.lib = _declare(_lib.lib())
+        self._h = self.lib.hb_writer_open(str(root).encode(), str(run_id).encode(), int(run), int(nchains))
+        if not self._h:
+            raise _lib.HBMIError(f"cannot open the output tree under {root}")
+
+    def attach(self, sampler: SlotSampler):
+        _ok(self.lib.hb_sampler_attach_log(sampler._h, self._h), "hb_sampler_attach_log")
+
+    def step(self, it, logl_slots, x_slots):
+        a = np.ascontiguousarray(logl_slots, dtype=np.float64)
+        b = np.ascontiguousarray(x_slots, dtype=np.float64)
+        _ok(self.lib.hb_writer_step(self._h, int(it), _pd(a), _pd(b)), "hb_writer_step")
+
+    def light_curve(self, t, f, m):
+        t, f, m = (np.ascontiguousarray(v, dtype=np.float64) for v in (t, f, m))
+        _ok(self.lib.hb_writer_lc(self._h, _pd(t), _pd(f), _pd(m), len(t)), "hb_writer_lc")
+
+    def pars(self, final, x):
+        x = np.ascontiguousarray(x, dtype=np.float64)
+        _ok(self.lib.hb_writer_pars(self._h, int(bool(final)), _pd(x)), "hb_writer_pars")
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self.lib.hb_writer_close(self._h)
+            self._h = None
 
 
 def run_mcmc(t, flux, sigma, niter, run_id, log10_period, run=0, nchains=50, npast=500, ladder=0, nthreads=0,

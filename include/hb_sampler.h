@@ -55,6 +55,43 @@ typedef struct hb_mcmc_result {
 int hb_mcmc_run(const hb_mcmc_cfg *cfg, const double *t, const double *flux, const double *sigma, long n,
                 hb_loglik_fn loglik, hb_model_fn model, void *user, hb_mcmc_result *result);
 
+/* ---- Phase API: the same sampler split into the steps of one iteration, so
+ * that the temperature slots can be sharded over ranks (one GPU each).  A
+ * sampler owns slots [slot_lo, slot_hi) of the cfg->nchains ladder; chain
+ * states live with their slot and move on a tempering swap.  Per iteration:
+ *   propose -> (likelihood of the nl proposals) -> accept -> all-gather logL
+ *   by slot -> swap (every rank replays the same rand() draws) -> exchange
+ *   the records of chains that crossed a rank boundary -> apply_perm ->
+ *   end_iter.
+ * With slot_lo = 0, slot_hi = nchains this IS hb_mcmc_run's loop. */
+typedef struct hb_sampler hb_sampler;
+typedef struct hb_writer hb_writer;
+#define HB_SAMPLER_REC 23 /* record of one chain: x[21], logL, chain id */
+
+hb_sampler *hb_sampler_create(const hb_mcmc_cfg *cfg, int slot_lo, int slot_hi);
+void hb_sampler_destroy(hb_sampler *s);
+int hb_sampler_attach_log(hb_sampler *s, hb_writer *w);  /* big-jump log (:520-528) */
+/* states (nl x 21), logL (nl), chain ids (nl) of the owned slots; NULL skips */
+int hb_sampler_get(const hb_sampler *s, double *x, double *logl, int *chain_id);
+int hb_sampler_set_logl(hb_sampler *s, const double *logl);         /* iteration 0 */
+int hb_sampler_propose(hb_sampler *s, long iter, double *y_out);     /* nl x 21 */
+int hb_sampler_accept(hb_sampler *s, long iter, const double *logly);/* nl */
+/* logl_all: W values by slot; perm_out[j] = source slot of slot j (W ints) */
+int hb_sampler_swap(hb_sampler *s, const double *logl_all, int *perm_out, double *logl_perm_out);
+int hb_sampler_pack(const hb_sampler *s, int slot, double *rec);      /* owned slot */
+/* remote: nl records, entry (j - slot_lo) read only where perm[j] is not owned */
+int hb_sampler_apply_perm(hb_sampler *s, const int *perm, const double *remote);
+/* {acc, DEacc, DEtrial, atrial, cold_acc, nswap} of the owned slots */
+int hb_sampler_stats(const hb_sampler *s, long *out6);
+int hb_sampler_end_iter(hb_sampler *s, long iter);
+
+/* Output files (mcmc_wrapper2.c:110-173, :593-681), written by one rank. */
+hb_writer *hb_writer_open(const char *root, const char *run_id, int run, int nchains);
+int hb_writer_step(hb_writer *w, long iter, const double *logl_slots, const double *x_slots);
+int hb_writer_lc(hb_writer *w, const double *t, const double *flux, const double *model, long n);
+int hb_writer_pars(hb_writer *w, int final_par, const double *x);
+void hb_writer_close(hb_writer *w);
+
 /* The reference's random streams, exposed for tests (mcmc_wrapper2.c:894-974). */
 double hb_ran2_parallel(long *idum, void *rng_state /* struct RNG_Vars */);
 double hb_gasdev2_parallel(long *idum, void *rng_state);

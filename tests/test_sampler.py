@@ -74,21 +74,25 @@ def test_sampler_bookkeeping_bit_exact_with_oracle_likelihood(oracle, tmp_path):
 
 def run_cli(tmp, niter=1200):
     exe = os.path.join(ROOT, "hb_mcmc_amd", "lib", "hb_mcmc")
-    g = golden("sampler_127079833.npz")
-    d = os.path.join(tmp, "data", "lightcurves", "folded_lightcurves")
-    os.makedirs(d, exist_ok=True)
-    from hb_mcmc_amd.hbio import write_folded_lc
-
-    write_folded_lc(os.path.join(d, "127079833_new.txt"), g["lc_t"], g["lc_f"], g["lc_e"])
+    g = stage_input(tmp)
     r = subprocess.run([exe, str(niter), "127079833", "0.5021", "0", "--root", tmp], capture_output=True,
                        text=True, timeout=900)
     assert r.returncode == 0, r.stderr
     return g, r.stdout
 
 
-@pytest.mark.gpu
-def test_sampler_bookkeeping_gpu_likelihood(tmp_path):
-    g, stdout = run_cli(str(tmp_path))
+def stage_input(tmp):
+    g = golden("sampler_127079833.npz")
+    d = os.path.join(tmp, "data", "lightcurves", "folded_lightcurves")
+    os.makedirs(d, exist_ok=True)
+    from hb_mcmc_amd.hbio import write_folded_lc
+
+    write_folded_lc(os.path.join(d, "127079833_new.txt"), g["lc_t"], g["lc_f"], g["lc_e"])
+    return g
+
+
+def assert_gpu_run_matches_reference(tmp_path, g):
+    """States/bookkeeping exact, logL within 1e-10 relative of the reference trace."""
     out = read_outputs(str(tmp_path))
     ref_chain, ref_logl = g["chain"], g["logl"]
     assert out["chain"].shape == ref_chain.shape and out["logl"].shape == ref_logl.shape
@@ -105,3 +109,9 @@ def test_sampler_bookkeeping_gpu_likelihood(tmp_path):
     for rel in (f"data/pars/par.{SUF}.dat", f"data/subpars/subpar.{SUF}.dat"):
         with open(os.path.join(str(tmp_path), rel), "rb") as fh:
             assert fh.read() == files[rel], rel
+
+
+@pytest.mark.gpu
+def test_sampler_bookkeeping_gpu_likelihood(tmp_path):
+    g, stdout = run_cli(str(tmp_path))
+    assert_gpu_run_matches_reference(tmp_path, g)
