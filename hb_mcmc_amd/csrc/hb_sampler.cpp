@@ -174,6 +174,42 @@ void de_step(const double* x, long* seed, const double* const* hist, int npast, 
   }
 }
 
+// glibc's rand() (random_r TYPE_3: r[k] = r[k-31] + r[k-3] mod 2^32, output
+// r[k] >> 1, seeded by srandom_r's Schrage recurrence and 310 discarded
+// outputs), held per sampler.  The reference calls the process-global
+// rand() after srand(NITER) (:86, :778-812); a private copy of the same
+// sequence cannot be perturbed by a library (RCCL's lazy communicator setup,
+// say) that calls rand() in between.  Checked against libc by test_sampler.py.
+class GlibcRand {
+ public:
+  explicit GlibcRand(unsigned seed = 1) { srand(seed); }
+  void srand(unsigned seed) {
+    if (seed == 0) seed = 1;
+    int32_t word = (int32_t)seed;
+    r_[0] = (uint32_t)word;
+    for (int i = 1; i < 31; ++i) {
+      const int32_t hi = word / 127773, lo = word % 127773;
+      word = 16807 * lo - 2836 * hi;
+      if (word < 0) word += 2147483647;
+      r_[i] = (uint32_t)word;
+    }
+    for (int i = 31; i < 34; ++i) r_[i] = r_[i - 31];
+    k_ = 34;
+    for (int i = 0; i < 310; ++i) next();
+  }
+  int rand() { return (int)(next() >> 1); }
+
+ private:
+  uint32_t next() {  // ring of 34: r[k-31] = r[(k+3) % 34], r[k-3] = r[(k+31) % 34]
+    const uint32_t v = r_[(k_ + 3) % 34] + r_[(k_ + 31) % 34];
+    r_[k_ % 34] = v;
+    ++k_;
+    return v;
+  }
+  uint32_t r_[34];
+  long k_ = 0;
+};
+
 struct Files {
   FILE* chain = nullptr;
   FILE* logl = nullptr;
@@ -320,6 +356,11 @@ double now_s() {
 
 extern "C" double hb_ran2_parallel(long* idum, void* st) { return ran2p(idum, (RNG_Vars*)st); }
 extern "C" double hb_gasdev2_parallel(long* idum, void* st) { return gasdevp(idum, (RNG_Vars*)st); }
+extern "C" int hb_rand_stream(unsigned seed, int n, int* out) {
+  GlibcRand g(seed);
+  for (int i = 0; i < n; ++i) out[i] = g.rand();
+  return 0;
+}
 
 // ---------------------------------------------------------------------------
 // Output files of mcmc_wrapper2.c (:110-173, :593-681), fed by slot.
@@ -410,6 +451,7 @@ struct hb_sampler {
   std::vector<const double*> hrow;
   std::vector<int> acc_arr, DEacc_arr, DEtrial_arr;
   long acc = 0, DEacc = 0, DEtrial = 0, atrial = 0, cold_acc = 0, nswap = 0;
+  GlibcRand rng;                                // the swap draws (srand(NITER), :86)
   std::vector<int> perm;                        // W, scratch of swap()
   std::vector<double> Lperm;                    // W
   std::vector<double> old;                      // nl x kRec, scratch of apply_perm()
@@ -438,7 +480,7 @@ extern "C" hb_sampler* hb_sampler_create(const hb_mcmc_cfg* cfg, int slot_lo, in
   s->pool = new Pool(nth);
   s->log_lc_period = cfg->log10_period;
   s->LC_PERIOD = pow(10., s->log_lc_period);
-  srand((unsigned)s->NITER);  // :86 (every rank replays the same swap draws)
+  s->rng.srand((unsigned)s->NITER);  // :86 (every rank replays the same swap draws)
   const int nl = s->nl;
 
   // chain 0's stream draws the initial states of ALL chains (USE_RAND_PARS=1,
@@ -620,13 +662,13 @@ extern "C" int hb_sampler_swap(hb_sampler* s, const double* logl_all, int* perm_
   }
   int n = 0;
   for (int i = 0; i < W; ++i) {
-    const int b = (int)(((double)rand() / (RAND_MAX)) * ((double)(W - 1)));
+    const int b = (int)(((double)s->rng.rand() / (RAND_MAX)) * ((double)(W - 1)));
     const int a = b + 1;
     const double heat1 = s->temp[a], heat2 = s->temp[b];
     const double dlogL = L[b] - L[a];
     const double Hs = (heat2 - heat1) / (heat2 * heat1);
     const double al = exp(dlogL * Hs);
-    const double be = ((double)rand() / (RAND_MAX));
+    const double be = ((double)s->rng.rand() / (RAND_MAX));
     if (al >= be) {
       std::swap(p[a], p[b]);
       std::swap(L[a], L[b]);

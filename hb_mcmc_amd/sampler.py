@@ -43,6 +43,8 @@ def _declare(lib):
     lib.hb_ran2_parallel.argtypes = [C.POINTER(C.c_long), C.c_void_p]
     lib.hb_gasdev2_parallel.restype = C.c_double
     lib.hb_gasdev2_parallel.argtypes = [C.POINTER(C.c_long), C.c_void_p]
+    lib.hb_rand_stream.restype = C.c_int
+    lib.hb_rand_stream.argtypes = [C.c_uint, C.c_int, C.POINTER(C.c_int)]
     vp, pd, pi = C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_int)
     for name, res, args in (
             ("hb_sampler_create", vp, [C.POINTER(MCMCConfig), C.c_int, C.c_int]),

@@ -95,6 +95,8 @@ void hb_writer_close(hb_writer *w);
 /* The reference's random streams, exposed for tests (mcmc_wrapper2.c:894-974). */
 double hb_ran2_parallel(long *idum, void *rng_state /* struct RNG_Vars */);
 double hb_gasdev2_parallel(long *idum, void *rng_state);
+/* n draws of glibc's rand() after srand(seed), from the sampler's private copy */
+int hb_rand_stream(unsigned seed, int n, int *out);
 
 #ifdef __cplusplus
 }

@@ -52,6 +52,23 @@ def test_rng_streams_match_reference_algorithm():
     assert all(0 < x < 1 for x in v) and len(set(v)) == 3
 
 
+def test_private_rand_is_glibc_rand():
+    """The swap draws come from a private copy of glibc's rand(): same sequence
+    as libc after srand(seed), for the seeds the CLI uses (NITER) and edges."""
+    import ctypes as C
+
+    from hb_mcmc_amd import _lib, sampler
+
+    lib = sampler._declare(_lib.lib())
+    libc = C.CDLL("libc.so.6")
+    for seed in (0, 1, 1200, 50000, 123456789, 2**31 - 1, 2**31 + 5, 2**32 - 1):
+        libc.srand(C.c_uint(seed))
+        want = [libc.rand() for _ in range(2000)]
+        got = (C.c_int * 2000)()
+        lib.hb_rand_stream(seed, 2000, got)
+        assert list(got) == want, seed
+
+
 @pytest.mark.slow
 def test_sampler_bookkeeping_bit_exact_with_oracle_likelihood(oracle, tmp_path):
     from hb_mcmc_amd.sampler import run_mcmc
