@@ -3,7 +3,7 @@
 Workload (BASELINE.json configs[1]): a synthetic
 1024-cadence heartbeat-binary light curve, 4096 walkers per GPU.  One "step"
 = one batched log-likelihood over the rank's walkers (two launches: per-walker
-constants + the one-workgroup-per-walker model/median/chi^2 kernel), followed,
+constants + the one-wave-per-walker model/median/chi^2 kernel), followed,
 when N > 1, by the RCCL all-gather of every walker's logL (what the tempering
 swap of mcmc_wrapper2.c:554-563 needs).  Inputs are resident in HBM before the
 timed region; the walker batches rotate over 4 pre-generated sets.
@@ -13,7 +13,7 @@ timed region; the walker batches rotate over 4 pre-generated sets.
 
 Rank 0 prints ONE JSON line.  `value` = evals over all ranks / max-over-ranks
 wall time of the K timed steps.  `roofline` prices the dominant kernel
-(hb_eval_kernel) with algorithmic bytes B(N) = 24 N + 176 per eval (SURVEY.md
+(hb_eval_wave_kernel at N <= 2048, else hb_eval_kernel) with algorithmic bytes B(N) = 24 N + 176 per eval (SURVEY.md
 8(d)) over its HIP-event-timed duration; `cpu_baseline` times the reference
 likelihood3.c (oracle/_ref, else the oracle port) on the host cores on a
 bounded sample of the same workload.
@@ -196,6 +196,8 @@ def main():
             except Exception:
                 traffic = None
         flops_conv = 600.0 * n  # SURVEY.md 8(d) counting convention
+        # the eval plan (hb_kernels.hip make_plan): one wave per walker up to 2048 cadences
+        kernel_name = "hb_eval_wave_kernel" if L.waves_per_walker == 1 else "hb_eval_kernel"
         line = {
             "metric": METRIC,
             "value": value,
@@ -217,7 +219,7 @@ def main():
                        "note": "reference sampler spends 2 evals per walker-step (mcmc_wrapper2.c:488-489)"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "hb_eval_kernel", "kernel_ms": eval_ms, "prep_kernel_ms": prep_ms,
+                         "kernel": kernel_name, "kernel_ms": eval_ms, "prep_kernel_ms": prep_ms,
                          "bytes_per_eval": bytes_per_eval},
             "fp64": {"achieved_tflops": flops_conv * w / (eval_ms * 1e-3) / 1e12, "peak_tflops": FP64_PEAK_TFLOPS,
                      "frac": flops_conv * w / (eval_ms * 1e-3) / 1e12 / FP64_PEAK_TFLOPS,

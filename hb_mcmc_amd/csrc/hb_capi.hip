@@ -57,10 +57,67 @@ static int set_err_msg(const std::string& m, int code = -1) {
 
 extern "C" const char* hb_last_error(void) { return g_err.c_str(); }
 
+// ---------------------------------------------------------------------------
+// one-time runtime setup, transparent to the caller's glibc rand() sequence
+// ---------------------------------------------------------------------------
+// The HIP runtime's first code-object load runs amd_comgr actions that call
+// srand() once and rand() ~85 times (measured on the MI355X box with
+// scripts/probes/rand_probe.c).  The reference sampler seeds rand() with
+// srand(NITER) (mcmc_wrapper2.c:86) BEFORE its first loglikelihood() call
+// (:342) and draws its tempering swaps from it (:778-812), so a drop-in that
+// let the runtime touch that state would change the reference's own trace.
+// All runtime initialisation therefore happens once, here, under a private
+// random() table: initstate() switches rand()/random() to it, setstate()
+// hands the caller's table back untouched.  Every code object of libhbmi,
+// and the runtime's blit kernels behind hipMemcpy/hipMemset, are loaded on
+// every visible device inside that window.
+__global__ void hb_capi_anchor_kernel() {}
+
+namespace {
+std::once_flag g_rt_once;
+int g_ndev = 0;
+
+void runtime_init() {
+  std::call_once(g_rt_once, [] {
+    static char priv[128];
+    char* prev = initstate(20260101u, priv, sizeof priv);
+    int n = 0;
+    if (hipGetDeviceCount(&n) == hipSuccess && n > 0) {
+      int cur = 0;
+      (void)hipGetDevice(&cur);
+      for (int d = 0; d < n; ++d) {
+        if (hipSetDevice(d) != hipSuccess) continue;
+        (void)hipFree(nullptr);  // context creation
+        (void)hbk::preload_code_object();  // hb_kernels.hip's code object
+        hipFuncAttributes a;
+        (void)hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&hb_capi_anchor_kernel));  // this file's (hipCUB)
+        // the runtime's own blit kernels (copy/fill) load on first use, also through comgr
+        double h[64] = {0}, *d0 = nullptr, *d1 = nullptr;
+        if (hipMalloc(&d0, sizeof h) == hipSuccess && hipMalloc(&d1, sizeof h) == hipSuccess) {
+          (void)hipMemcpy(d0, h, sizeof h, hipMemcpyHostToDevice);
+          (void)hipMemcpy(d1, d0, sizeof h, hipMemcpyDeviceToDevice);
+          (void)hipMemcpy(h, d1, sizeof h, hipMemcpyDeviceToHost);
+          (void)hipMemset(d0, 0, sizeof h);
+          (void)hipMemcpyAsync(d1, h, sizeof h, hipMemcpyHostToDevice, nullptr);
+          (void)hipMemcpyAsync(h, d1, sizeof h, hipMemcpyDeviceToHost, nullptr);
+          (void)hipMemsetAsync(d1, 0, sizeof h, nullptr);
+          (void)hipDeviceSynchronize();
+        }
+        if (d0) (void)hipFree(d0);
+        if (d1) (void)hipFree(d1);
+      }
+      (void)hipSetDevice(cur);
+      g_ndev = n;
+    }
+    (void)hipGetLastError();
+    setstate(prev);
+  });
+}
+}  // namespace
+
 extern "C" int hb_device_available(void) {
-  int n = 0;
-  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
-  return n > 0 ? 1 : 0;
+  runtime_init();
+  return g_ndev > 0 ? 1 : 0;
 }
 
 // ---------------------------------------------------------------------------
@@ -132,8 +189,9 @@ extern "C" hb_ctx* hb_create(const double* t, const double* f, const double* sig
     set_err_msg("hb_create: null array");
     return nullptr;
   }
-  int ndev = 0;
-  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
+  runtime_init();
+  const int ndev = g_ndev;
+  if (ndev <= 0) {
     set_err_msg("hb_create: no HIP device available (libhbmi has no CPU fallback)");
     return nullptr;
   }

@@ -59,6 +59,8 @@ enum ProbeOp {
 };
 
 EvalPlan make_plan(long n);
+// forces the load of hb_kernels.hip's code object on the current device
+hipError_t preload_code_object();
 hipError_t launch_prep(const double* d_params, int nwalk, const MagArgs& ma, hbdev::WalkerConst* d_wc,
                        hipStream_t s);
 hipError_t launch_eval(const EvalPlan& pl, const double* t, const double* f, const double* sg,

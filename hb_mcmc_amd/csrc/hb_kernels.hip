@@ -785,6 +785,11 @@ hipError_t launch_median(double* d_a, long n, long kth, hipStream_t s) {
 }
 
 // Choose waves-per-walker and template storage for N cadences.
+hipError_t preload_code_object() {
+  hipFuncAttributes a;
+  return hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&hb_prep_kernel));
+}
+
 EvalPlan make_plan(long n) {
   EvalPlan pl;
   pl.n = n;

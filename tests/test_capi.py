@@ -85,3 +85,27 @@ def test_no_cpu_fallback_without_device():
         pytest.skip("a GPU is present")
     with pytest.raises(_lib.HBMIError, match="no HIP device"):
         HBLikelihood(np.arange(8.0), np.ones(8), np.full(8, 1e-3))
+
+
+def build_probe(tmp, name):
+    src = os.path.join(ROOT, "scripts", "probes", name + ".c")
+    exe = os.path.join(str(tmp), name)
+    lib = os.path.join(ROOT, "hb_mcmc_amd", "lib")
+    subprocess.run(["gcc", "-O1", "-o", exe, src, "-L" + lib, "-lhbmi", "-Wl,-rpath," + lib,
+                    "-Wl,-rpath-link,/opt/rocm/lib", "-lpthread"], check=True)
+    return exe
+
+
+def test_rand_isolation_probe_links(tmp_path):
+    """The probe links against every drop-in symbol it calls (no GPU needed to link)."""
+    assert os.path.exists(build_probe(tmp_path, "rand_isolation"))
+
+
+@pytest.mark.gpu
+def test_dropin_leaves_callers_rand_sequence_alone(tmp_path):
+    """The HIP runtime's first code-object load calls srand()/rand() (amd_comgr);
+    libhbmi isolates that, so a caller seeded with srand() -- the reference
+    sampler, mcmc_wrapper2.c:86 -- sees its exact sequence."""
+    r = subprocess.run([build_probe(tmp_path, "rand_isolation")], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "rand sequence preserved" in r.stdout

@@ -132,3 +132,22 @@ def assert_gpu_run_matches_reference(tmp_path, g):
 def test_sampler_bookkeeping_gpu_likelihood(tmp_path):
     g, stdout = run_cli(str(tmp_path))
     assert_gpu_run_matches_reference(tmp_path, g)
+
+
+@pytest.mark.gpu
+def test_reference_sampler_relinked_against_libhbmi(tmp_path):
+    """The reference's OWN sampler (src/mcmc_wrapper2.c, unmodified, built by
+    `make -C oracle dropin`) linked against libhbmi.so instead of
+    likelihood3.c: its 2 x 50 x 1200 scalar loglikelihood() calls, from 25
+    OpenMP threads, all run through the drop-in entry point on the GPU."""
+    exe = os.path.join(ROOT, "oracle", "_ref", "hb_mcmc_ref_hbmi")
+    if not os.path.exists(exe):
+        pytest.skip("oracle/_ref/hb_mcmc_ref_hbmi is built from /root/reference in the development container")
+    g = stage_input(str(tmp_path))
+    for sub in ("subpars", "pars", "chains", "logL", "log", "lightcurves/mcmc_lightcurves"):
+        os.makedirs(os.path.join(str(tmp_path), "data", sub), exist_ok=True)
+    os.makedirs(os.path.join(str(tmp_path), "debug"), exist_ok=True)
+    r = subprocess.run([exe, "1200", "127079833", "0.5021", "0"], cwd=str(tmp_path),
+                       env=dict(os.environ, HBREF_ROOT=str(tmp_path)), capture_output=True, text=True, timeout=900)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert_gpu_run_matches_reference(tmp_path, g)
