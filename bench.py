@@ -55,6 +55,11 @@ def parse():
     ap.add_argument("--ncad", type=int, default=1024)
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline sample length")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--timer", choices=("hip", "torch"), default="hip",
+                    help="hip: libhbmi's fence-free HIP events (hb_timer_*); torch: torch.cuda.Event")
+    ap.add_argument("--event-every", type=int, default=10,
+                    help="bracket every k-th timed step's kernels with HIP events (an event pair costs "
+                         "~5 us of stream time on this runtime; 1 = every step)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
                     help="per-launch HBM bytes measured by rocprofv3 --pmc (see profiles/README.md)")
     return ap.parse_args()
@@ -120,6 +125,33 @@ def cpu_baseline(t, f, s, target_s):
             "value_1core": len(one) / dt1}
 
 
+class _HipEvent:
+    """HIP event without the system-scope release fence (include/hbmi.h hb_timer_*),
+    recorded on the stream the kernels are launched on."""
+
+    def __init__(self):
+        from hb_mcmc_amd import _lib
+        self._lib = _lib.lib()
+        self.h = self._lib.hb_timer_create()
+        if not self.h:
+            raise RuntimeError("hb_timer_create failed")
+
+    def record(self, stream):
+        import ctypes as C
+        self._lib.hb_timer_record(self.h, C.c_void_p(stream.cuda_stream))
+
+    def elapsed_time(self, other):
+        return float(self._lib.hb_timer_elapsed_ms(self.h, other.h))
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            self._lib.hb_timer_destroy(self.h)
+
+
+def make_event(kind):
+    return _HipEvent() if kind == "hip" else torch.cuda.Event(enable_timing=True)
+
+
 def main():
     a = parse()
     rank = int(os.environ.get("RANK", "0"))
@@ -161,19 +193,21 @@ def main():
     for k in range(a.warmup):
         step(k)
     torch.cuda.synchronize()
-    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(a.steps)]
+    evs = [[make_event(a.timer) for _ in range(3)] for _ in range(a.steps)]
+    ev_on = [k % max(1, a.event_every) == 0 for k in range(a.steps)]
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for k in range(a.steps):
-        step(k, evs[k])
+        step(k, evs[k] if ev_on[k] else None)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     wall = time.perf_counter() - t0
-    prep_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
-    eval_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in evs]))
+    timed = [e for e, on in zip(evs, ev_on) if on]
+    prep_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in timed]))
+    eval_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in timed]))
     if world > 1:
         tt = torch.tensor([wall, eval_ms, prep_ms], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -220,6 +254,7 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": kernel_name, "kernel_ms": eval_ms, "prep_kernel_ms": prep_ms,
+                         "kernel_event_samples": len(timed), "kernel_timer": a.timer,
                          "bytes_per_eval": bytes_per_eval},
             "fp64": {"achieved_tflops": flops_conv * w / (eval_ms * 1e-3) / 1e12, "peak_tflops": FP64_PEAK_TFLOPS,
                      "frac": flops_conv * w / (eval_ms * 1e-3) / 1e12 / FP64_PEAK_TFLOPS,

@@ -56,6 +56,12 @@ def _declare(lib):
     lib.hb_ctx_template_in_lds.argtypes = [_VP]
     lib.hb_last_error.restype = C.c_char_p
     lib.hb_device_available.restype = _I
+    lib.hb_timer_create.restype = _VP
+    lib.hb_timer_record.restype = _I
+    lib.hb_timer_record.argtypes = [_VP, _VP]
+    lib.hb_timer_elapsed_ms.restype = C.c_float
+    lib.hb_timer_elapsed_ms.argtypes = [_VP, _VP]
+    lib.hb_timer_destroy.argtypes = [_VP]
     # likelihood3.h drop-in symbols
     lib.loglikelihood.restype = _D
     lib.loglikelihood.argtypes = [_PD, _PD, _PD, _L, _PD, _PD, _PD]

@@ -120,6 +120,28 @@ extern "C" int hb_device_available(void) {
   return g_ndev > 0 ? 1 : 0;
 }
 
+extern "C" void* hb_timer_create(void) {
+  runtime_init();
+  hipEvent_t e = nullptr;
+  if (hipEventCreateWithFlags(&e, hipEventDisableSystemFence) != hipSuccess) return nullptr;
+  return (void*)e;
+}
+extern "C" int hb_timer_record(void* t, void* stream) {
+  if (!t) return -1;
+  HB_TRY(hipEventRecord((hipEvent_t)t, (hipStream_t)stream), "hipEventRecord");
+  return 0;
+}
+extern "C" float hb_timer_elapsed_ms(void* a, void* b) {
+  if (!a || !b) return -1.f;
+  if (hipEventSynchronize((hipEvent_t)b) != hipSuccess) return -1.f;
+  float ms = -1.f;
+  if (hipEventElapsedTime(&ms, (hipEvent_t)a, (hipEvent_t)b) != hipSuccess) return -1.f;
+  return ms;
+}
+extern "C" void hb_timer_destroy(void* t) {
+  if (t) (void)hipEventDestroy((hipEvent_t)t);
+}
+
 // ---------------------------------------------------------------------------
 // context
 // ---------------------------------------------------------------------------

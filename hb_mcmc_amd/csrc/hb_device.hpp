@@ -469,6 +469,7 @@ template <int K>
 __device__ __forceinline__ void hb_cadence_flux_k(const double (&t)[K], const WalkerConst& w,
                                                   double (&v)[K], bool& bad) {
   const double e = w.e;
+  const double aR2 = w.aR * w.aR, rsum2 = w.rsum * w.rsum;
   double m[K], E[K], s[K], c[K];
   bool ok = true;
 #pragma unroll
@@ -521,7 +522,7 @@ __device__ __forceinline__ void hb_cadence_flux_k(const double (&t)[K], const Wa
     const double su = w.sw * cnu + w.cw * snu;
     const double b = (1.0 + e * cnu) * w.inv1me2;
     const double sci = su * w.ci;
-    dd[k] = den * sqrt(cu * cu + sci * sci);  // projected separation / a
+    dd[k] = den * den * (cu * cu + sci * sci);  // (projected separation / a)^2; sqrt only on eclipse lanes
     zz[k] = su * w.si;
     const double c2 = (cu - su) * (cu + su);
     const double s3 = su * (3.0 - 4.0 * su * su);
@@ -536,14 +537,15 @@ __device__ __forceinline__ void hb_cadence_flux_k(const double (&t)[K], const Wa
     val += (b2 * b2) * (w.ks1 * su + w.ks3 * s3);
     val += (b3 * b2) * (w.kam3 + w.kc22 * c2 + w.kc4 * c4);
     v[k] = val;
-    need_ecl |= (dd[k] * w.aR < w.rsum) & (zz[k] != 0.0);
+    // squared test: a lane within an ulp of tangency may go either way, where
+    // the overlap area (~eps^1.5) is zero to working precision
+    need_ecl |= (dd[k] * aR2 < rsum2) & (zz[k] != 0.0);
   }
   bad = !ok;
   if (__any(need_ecl)) {
 #pragma unroll
     for (int k = 0; k < K; ++k) {
-      const double dR = dd[k] * w.aR;
-      if ((dR < w.rsum) & (zz[k] != 0.0)) v[k] -= eclipse_term(&w, dR, zz[k]);
+      if ((dd[k] * aR2 < rsum2) & (zz[k] != 0.0)) v[k] -= eclipse_term(&w, sqrt(dd[k]) * w.aR, zz[k]);
     }
   }
 }

@@ -19,6 +19,9 @@
 
 namespace hbdev {
 
+// v_rcp_f64 is good to ~2^-24 (2.5e8 ulp, scripts/probes/rcp_probe.hip on
+// the MI355X); one Newton step gives <= 11 ulp, two give the correctly
+// rounded reciprocal on every probed input.
 __device__ __forceinline__ double fast_rcp(double d) {
   double y = __builtin_amdgcn_rcp(d);
   double r = fma(-d, y, 1.0);
@@ -28,9 +31,13 @@ __device__ __forceinline__ double fast_rcp(double d) {
   return y;
 }
 
-// n / d for normal, moderate d (|d| in [2^-900, 2^900]); ~1 ulp
+// n / d for normal, moderate d (|d| in [2^-900, 2^900]).  Seed + ONE Newton
+// step + the residual correction: the correction squares the quotient's
+// error, and the probe found the result correctly rounded (== n / d) for all
+// 4.2M inputs with d in [0.005, 2] -- the Kepler/orbit denominators.
 __device__ __forceinline__ double fast_div(double n, double d) {
-  const double y = fast_rcp(d);
+  double y = __builtin_amdgcn_rcp(d);
+  y = fma(fma(-d, y, 1.0), y, y);
   const double q = n * y;
   return fma(fma(-d, q, n), y, q);
 }

@@ -161,6 +161,14 @@ const char *hb_last_error(void);
 /* 1 if a HIP device is usable, 0 otherwise (never falls back to the CPU). */
 int hb_device_available(void);
 
+/* ---- measurement helpers (bench.py): HIP events recorded on the caller's
+ * stream without the system-scope release fence a default event record
+ * performs, so a bracket costs the stream as little as possible. ---- */
+void *hb_timer_create(void);
+int hb_timer_record(void *timer, void *stream);
+float hb_timer_elapsed_ms(void *start, void *stop); /* synchronises on stop; <0 on error */
+void hb_timer_destroy(void *timer);
+
 #ifdef __cplusplus
 }
 #endif
