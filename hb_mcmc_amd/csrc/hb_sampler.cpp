@@ -444,6 +444,7 @@ struct hb_sampler {
   std::vector<long> seeds;                     // nl
   std::vector<RNG_Vars> states;                // nl
   std::vector<double> x, logL, logP;           // nl x 21, nl, nl
+  std::vector<char> logP_ok;                   // logP[jl] == log_prior(x[jl]) (cache; the state is unchanged)
   std::vector<int> cid;                        // nl: chain id at the slot
   std::vector<double> y, logPy, alpha2;        // proposals
   std::vector<int> jump, jtype;
@@ -454,7 +455,8 @@ struct hb_sampler {
   GlibcRand rng;                                // the swap draws (srand(NITER), :86)
   std::vector<int> perm;                        // W, scratch of swap()
   std::vector<double> Lperm;                    // W
-  std::vector<double> old;                      // nl x kRec, scratch of apply_perm()
+  std::vector<double> old, oldP;                // nl x kRec, nl: scratch of apply_perm()
+  std::vector<char> oldP_ok;
   hb_writer* log = nullptr;
   Pool* pool = nullptr;
   ~hb_sampler() { delete pool; }
@@ -518,6 +520,7 @@ extern "C" hb_sampler* hb_sampler_create(const hb_mcmc_cfg* cfg, int slot_lo, in
 
   s->logL.assign(nl, 0.0);
   s->logP.assign(nl, 0.0);
+  s->logP_ok.assign(nl, 0);
   s->cid.resize(nl);
   for (int jl = 0; jl < nl; ++jl) s->cid[jl] = slot_lo + jl;
   s->y.resize((size_t)nl * kNp);
@@ -599,7 +602,10 @@ extern "C" int hb_sampler_propose(hb_sampler* s, long iter, double* y_out) {
     }
     yj[2] = s->log_lc_period;
     yj[6] = fmod(yj[6], s->LC_PERIOD);
-    s->logP[jl] = log_prior(xc, s->pr);
+    if (!s->logP_ok[jl]) {  // :444 recomputes it every step; the value only changes with the state
+      s->logP[jl] = log_prior(xc, s->pr);
+      s->logP_ok[jl] = 1;
+    }
     s->logPy[jl] = log_prior(yj, s->pr);
     s->jump[jl] = jmp;
     s->jtype[jl] = jt;
@@ -629,6 +635,7 @@ extern "C" int hb_sampler_accept(hb_sampler* s, long iter, const double* logly) 
       if (chain_id == 0) s->acc_arr[jl]++;
       memcpy(xc, yj, sizeof(double) * kNp);
       s->logL[jl] = logly[jl];
+      s->logP[jl] = s->logPy[jl];  // log_prior(y), computed in propose
       if ((s->jump[jl] == 1) && (chain_id == 0)) s->DEacc_arr[jl]++;
     }
     memcpy(&s->hist[((size_t)jl * NPAST + k) * kNp], xc, sizeof(double) * kNp);
@@ -698,14 +705,19 @@ extern "C" int hb_sampler_apply_perm(hb_sampler* s, const int* perm, const doubl
   if (!s || !perm) return -1;
   const int nl = s->nl, lo = s->lo, hi = s->hi;
   for (int jl = 0; jl < nl; ++jl) hb_sampler_pack(s, lo + jl, &s->old[(size_t)jl * kRec]);
+  s->oldP.assign(s->logP.begin(), s->logP.end());
+  s->oldP_ok.assign(s->logP_ok.begin(), s->logP_ok.end());
   for (int jl = 0; jl < nl; ++jl) {
     const int src = perm[lo + jl];
     const double* r;
     if (src >= lo && src < hi) {
       r = &s->old[(size_t)(src - lo) * kRec];
+      s->logP[jl] = s->oldP[src - lo];
+      s->logP_ok[jl] = s->oldP_ok[src - lo];
     } else {
       if (!remote) return -2;
       r = &remote[(size_t)jl * kRec];
+      s->logP_ok[jl] = 0;  // recomputed from the received state
     }
     memcpy(&s->x[(size_t)jl * kNp], r, sizeof(double) * kNp);
     s->logL[jl] = r[kNp];
