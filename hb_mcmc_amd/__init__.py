@@ -6,8 +6,12 @@ heartbeat-binary light-curve log-likelihood path.
 * ``hb_mcmc_amd.likelihood``: Python mirror of the batched API (ctypes).
 * ``hb_mcmc_amd.pyHB``: drop-in for the reference Cython module ``pyHB``.
 * ``hb_mcmc_amd.sampler``: the parallel-tempered MCMC caller (mcmc_wrapper2.c).
-* ``hb_mcmc_amd.dist``: walker sharding over GPUs with an RCCL all-gather.
+* ``hb_mcmc_amd.dist``: temperature slots sharded over GPUs with an RCCL all-gather.
+* ``hb_mcmc_amd.catalog``: catalog-sweep mode (many targets per GPU, one
+  batched launch per size class; targets dealt over GPUs).
 
 Importing the package does not touch the GPU.
 """
 __version__ = "0.1.0"
+
+from ._lib import HBMIError  # noqa: E402,F401

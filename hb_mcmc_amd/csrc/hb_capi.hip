@@ -338,6 +338,208 @@ static int host_batch(hb_ctx* c, const double* params, int w, double* out, void*
   return 0;
 }
 
+// ---------------------------------------------------------------------------
+// catalog mode: many light curves, one batched launch per size class
+// ---------------------------------------------------------------------------
+struct hb_catalog {
+  int device = 0;
+  int ntargets = 0;
+  std::vector<hbk::TargetDesc> tab;
+  std::vector<int> vpt;          // per target
+  double* d_t = nullptr;
+  double* d_f = nullptr;
+  double* d_s = nullptr;         // 1 / max(sigma, 1e-5)
+  hbk::TargetDesc* d_tab = nullptr;
+  // walker layout cache (walkers per target as last seen)
+  std::vector<int> layout;
+  int total = 0;
+  int cap = 0;
+  int* d_wt = nullptr;           // target of each walker
+  int* d_list = nullptr;         // walkers grouped by size class
+  int class_off[7] = {0};        // class c (vpt = 1 << c): list[class_off[c] .. class_off[c+1])
+  size_t class_slab[6] = {0};
+  WalkerConst* d_wc = nullptr;
+  double* d_params = nullptr;    // host-API staging
+  double* d_out = nullptr;
+  std::mutex mu;
+};
+
+extern "C" void hb_catalog_destroy(hb_catalog* c) {
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  for (void* p : {(void*)c->d_t, (void*)c->d_f, (void*)c->d_s, (void*)c->d_tab, (void*)c->d_wt, (void*)c->d_list,
+                  (void*)c->d_wc, (void*)c->d_params, (void*)c->d_out})
+    if (p) (void)hipFree(p);
+  delete c;
+}
+
+extern "C" hb_catalog* hb_catalog_create(int ntargets, const double* const* t, const double* const* f,
+                                         const double* const* sigma, const long* n, const double* mag5,
+                                         const double* magerr4, int device) {
+  if (ntargets <= 0 || !t || !f || !sigma || !n) {
+    set_err_msg("hb_catalog_create: need ntargets >= 1 and non-null arrays");
+    return nullptr;
+  }
+  runtime_init();
+  if (g_ndev <= 0) {
+    set_err_msg("hb_catalog_create: no HIP device available (libhbmi has no CPU fallback)");
+    return nullptr;
+  }
+  if (device < 0 || device >= g_ndev) {
+    set_err_msg("hb_catalog_create: device index out of range");
+    return nullptr;
+  }
+  std::unique_ptr<hb_catalog, void (*)(hb_catalog*)> c(new hb_catalog, hb_catalog_destroy);
+  c->device = device;
+  c->ntargets = ntargets;
+  c->tab.resize(ntargets);
+  c->vpt.resize(ntargets);
+  long total = 0;
+  for (int k = 0; k < ntargets; ++k) {
+    if (n[k] < 2 || n[k] > 64 * 32 || !t[k] || !f[k] || !sigma[k]) {
+      set_err_msg("hb_catalog_create: target " + std::to_string(k) +
+                  " needs 2 <= N <= 2048 cadences (longer light curves: one hb_create context each)");
+      return nullptr;
+    }
+    hbk::TargetDesc& d = c->tab[k];
+    memset(&d, 0, sizeof d);
+    d.off = total;
+    d.n = n[k];
+    d.kth = (n[k] % 2 == 0) ? n[k] / 2 : n[k] / 2 + 1;  // likelihood3.c:97-99
+    d.dist = mag5 ? mag5[5 * k + 0] : 1000.;             // mcmc_wrapper2.c:321-327 fallback
+    d.gmag = mag5 ? mag5[5 * k + 1] : 1.;
+    d.gerr = magerr4 ? magerr4[4 * k + 0] : 1e15;
+    c->vpt[k] = hbk::wave_vpt_for(n[k]);
+    total += n[k];
+  }
+  std::vector<double> ht((size_t)total), hf((size_t)total), hs((size_t)total);
+  for (int k = 0; k < ntargets; ++k) {
+    const long o = c->tab[k].off;
+    for (long i = 0; i < n[k]; ++i) {
+      ht[o + i] = t[k][i];
+      hf[o + i] = f[k][i];
+      const double sg = sigma[k][i] < 1.e-5 ? 1.e-5 : sigma[k][i];  // likelihood3.c:824-827
+      hs[o + i] = 1.0 / sg;
+    }
+  }
+  if (hipSetDevice(device) != hipSuccess) { set_err_msg("hb_catalog_create: hipSetDevice failed"); return nullptr; }
+  const size_t b = sizeof(double) * (size_t)total;
+  if (hipMalloc(&c->d_t, b) != hipSuccess || hipMalloc(&c->d_f, b) != hipSuccess ||
+      hipMalloc(&c->d_s, b) != hipSuccess ||
+      hipMalloc(&c->d_tab, sizeof(hbk::TargetDesc) * ntargets) != hipSuccess) {
+    set_err_msg("hb_catalog_create: hipMalloc failed");
+    return nullptr;
+  }
+  if (hipMemcpy(c->d_t, ht.data(), b, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(c->d_f, hf.data(), b, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(c->d_s, hs.data(), b, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(c->d_tab, c->tab.data(), sizeof(hbk::TargetDesc) * ntargets, hipMemcpyHostToDevice) != hipSuccess) {
+    set_err_msg("hb_catalog_create: upload failed");
+    return nullptr;
+  }
+  return c.release();
+}
+
+extern "C" int hb_catalog_ntargets(const hb_catalog* c) { return c ? c->ntargets : -1; }
+
+// (re)builds the walker -> target map and the per-class walker lists
+static int catalog_layout(hb_catalog* c, const int* walkers, hipStream_t s) {
+  bool same = (int)c->layout.size() == c->ntargets;
+  for (int k = 0; same && k < c->ntargets; ++k) same = c->layout[k] == walkers[k];
+  if (same) return 0;
+  long total = 0;
+  for (int k = 0; k < c->ntargets; ++k) {
+    if (walkers[k] < 0) return set_err_msg("hb_catalog: negative walker count");
+    total += walkers[k];
+  }
+  if (total > (1 << 30)) return set_err_msg("hb_catalog: too many walkers");
+  std::vector<int> wt((size_t)total), list;
+  list.reserve((size_t)total);
+  long w = 0;
+  for (int k = 0; k < c->ntargets; ++k)
+    for (int i = 0; i < walkers[k]; ++i) wt[(size_t)w++] = k;
+  for (int cl = 0; cl < 6; ++cl) {
+    c->class_off[cl] = (int)list.size();
+    long nmax = 0;
+    w = 0;
+    for (int k = 0; k < c->ntargets; ++k) {
+      if (c->vpt[k] == (1 << cl)) {
+        for (int i = 0; i < walkers[k]; ++i) list.push_back((int)(w + i));
+        if (walkers[k] > 0 && c->tab[k].n > nmax) nmax = c->tab[k].n;
+      }
+      w += walkers[k];
+    }
+    c->class_slab[cl] = hbk::wave_slab_bytes(nmax > 0 ? nmax : 2);
+  }
+  c->class_off[6] = (int)list.size();
+  if ((int)total > c->cap) {
+    for (void* p : {(void*)c->d_wt, (void*)c->d_list, (void*)c->d_wc, (void*)c->d_params, (void*)c->d_out})
+      if (p) (void)hipFree(p);
+    c->d_wt = c->d_list = nullptr;
+    c->d_wc = nullptr;
+    c->d_params = c->d_out = nullptr;
+    c->cap = 0;
+    const size_t nw = (size_t)total;
+    if (hipMalloc(&c->d_wt, sizeof(int) * nw) != hipSuccess || hipMalloc(&c->d_list, sizeof(int) * nw) != hipSuccess ||
+        hipMalloc(&c->d_wc, sizeof(WalkerConst) * nw) != hipSuccess ||
+        hipMalloc(&c->d_params, sizeof(double) * 21 * nw) != hipSuccess ||
+        hipMalloc(&c->d_out, sizeof(double) * nw) != hipSuccess)
+      return set_err_msg("hb_catalog: hipMalloc failed");
+    c->cap = (int)total;
+  }
+  if (total > 0) {
+    HB_TRY(hipMemcpyAsync(c->d_wt, wt.data(), sizeof(int) * (size_t)total, hipMemcpyHostToDevice, s), "upload map");
+    HB_TRY(hipMemcpyAsync(c->d_list, list.data(), sizeof(int) * (size_t)total, hipMemcpyHostToDevice, s),
+           "upload lists");
+    HB_TRY(hipStreamSynchronize(s), "hipStreamSynchronize");  // host vectors go out of scope
+  }
+  c->layout.assign(walkers, walkers + c->ntargets);
+  c->total = (int)total;
+  return 0;
+}
+
+static int catalog_run(hb_catalog* c, const double* d_params, double* d_logl, hipStream_t s) {
+  if (c->total == 0) return 0;
+  MagArgs unused{};
+  HB_TRY(hbk::launch_prep(d_params, c->total, unused, c->d_wc, s, c->d_tab, c->d_wt), "prep launch");
+  for (int cl = 0; cl < 6; ++cl) {
+    const int cnt = c->class_off[cl + 1] - c->class_off[cl];
+    HB_TRY(hbk::launch_eval_multi(1 << cl, c->class_slab[cl], c->d_t, c->d_f, c->d_s, c->d_tab, c->d_wt,
+                                  c->d_list + c->class_off[cl], cnt, c->d_wc, d_logl, s),
+           "eval launch");
+  }
+  return 0;
+}
+
+extern "C" int hb_catalog_loglik_dev(hb_catalog* c, const double* d_params, const int* walkers, double* d_logl,
+                                     void* stream) {
+  if (!c || !walkers) return set_err_msg("hb_catalog_loglik_dev: null argument");
+  std::lock_guard<std::mutex> lk(c->mu);
+  HB_TRY(hipSetDevice(c->device), "hipSetDevice");
+  hipStream_t s = (hipStream_t)stream;
+  int rc = catalog_layout(c, walkers, s);
+  if (rc) return rc;
+  return catalog_run(c, d_params, d_logl, s);
+}
+
+extern "C" int hb_catalog_loglik(hb_catalog* c, const double* params, const int* walkers, double* logl,
+                                 void* stream) {
+  if (!c || !walkers) return set_err_msg("hb_catalog_loglik: null argument");
+  std::lock_guard<std::mutex> lk(c->mu);
+  HB_TRY(hipSetDevice(c->device), "hipSetDevice");
+  hipStream_t s = (hipStream_t)stream;
+  int rc = catalog_layout(c, walkers, s);
+  if (rc) return rc;
+  if (c->total == 0) return 0;
+  HB_TRY(hipMemcpyAsync(c->d_params, params, sizeof(double) * 21 * (size_t)c->total, hipMemcpyHostToDevice, s),
+         "upload params");
+  rc = catalog_run(c, c->d_params, c->d_out, s);
+  if (rc) return rc;
+  HB_TRY(hipMemcpyAsync(logl, c->d_out, sizeof(double) * (size_t)c->total, hipMemcpyDeviceToHost, s), "download");
+  HB_TRY(hipStreamSynchronize(s), "hipStreamSynchronize");
+  return 0;
+}
+
 extern "C" int hb_loglik_batch(hb_ctx* c, const double* params, int w, double* logl, void* stream) {
   return host_batch(c, params, w, logl, stream, false);
 }

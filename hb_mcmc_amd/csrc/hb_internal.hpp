@@ -37,6 +37,19 @@ struct EvalPlan {
   size_t lds_bytes = 0;
 };
 
+// One light curve of a catalog (hb_catalog_*): its slice of the concatenated
+// t / f / (1/sigma) arrays and the magnitude data the Gaia term uses.
+struct alignas(16) TargetDesc {
+  long off;      // first cadence in the concatenated arrays
+  long n;        // cadences (2..2048 in the batched path)
+  long kth;      // 0-based median rank (likelihood3.c:97-99)
+  long pad0;
+  double dist;   // mag_data[0] [pc]
+  double gmag;   // mag_data[1]
+  double gerr;   // magerr[0]
+  double pad1;
+};
+
 struct TrajArgs {
   hbdev::WalkerConst w;  // orbit fields only; aR carries a in cm
   double fz1, fz2;       // M2/Mtot, M1/Mtot after the traj() mass swap
@@ -62,7 +75,14 @@ EvalPlan make_plan(long n);
 // forces the load of hb_kernels.hip's code object on the current device
 hipError_t preload_code_object();
 hipError_t launch_prep(const double* d_params, int nwalk, const MagArgs& ma, hbdev::WalkerConst* d_wc,
-                       hipStream_t s);
+                       hipStream_t s, const TargetDesc* tab = nullptr, const int* wt = nullptr);
+// catalog mode: walkers list[0..count) of one size class (cadences per lane
+// vpt), each reading its target's slice through tab[wt[walker]]
+hipError_t launch_eval_multi(int vpt, size_t slab_bytes, const double* t, const double* f, const double* sg,
+                             const TargetDesc* tab, const int* wt, const int* list, int count,
+                             const hbdev::WalkerConst* wc, double* logl, hipStream_t s);
+int wave_vpt_for(long n);  // cadences per lane of the one-wave path, 0 if n > 2048
+size_t wave_slab_bytes(long n);
 hipError_t launch_eval(const EvalPlan& pl, const double* t, const double* f, const double* sg,
                        const hbdev::WalkerConst* wc, int nwalk, double* logl, double* tmpl,
                        double* scratch, int mode, hipStream_t s);

@@ -49,7 +49,9 @@ constexpr int kWcDoubles = (int)(sizeof(WalkerConst) / sizeof(double));
 
 __global__ __launch_bounds__(2 * kPrepWalkers) void hb_prep_kernel(const double* __restrict__ params,
                                                                     int nwalk, MagArgs ma,
-                                                                    WalkerConst* __restrict__ out) {
+                                                                    WalkerConst* __restrict__ out,
+                                                                    const TargetDesc* __restrict__ tab,
+                                                                    const int* __restrict__ wt) {
   __shared__ double sp[kPrepWalkers * kNpars];
   __shared__ double so[kPrepWalkers * kWcDoubles];
   __shared__ double xs[2][16][kPrepWalkers];  // per-star results for the partner: [star][item][walker]
@@ -125,8 +127,15 @@ __global__ __launch_bounds__(2 * kPrepWalkers) void hb_prep_kernel(const double*
     }
   } else {
     // Gaia G term (loglikelihood :834-848) while wave 1 does the eclipse/Roche part
-    const double g = ab_mag(band_flux(673.0, r1 * kRsun, r2 * kRsun, t1, t2, ma.mag[0], p[19]));
-    gr = (g - ma.mag[1]) / ma.magerr[0];
+    double dist = ma.mag[0], gobs = ma.mag[1], gerr = ma.magerr[0];
+    if (tab != nullptr && live) {  // catalog mode: this walker's target
+      const TargetDesc& td = tab[wt[base + j]];
+      dist = td.dist;
+      gobs = td.gmag;
+      gerr = td.gerr;
+    }
+    const double g = ab_mag(band_flux(673.0, r1 * kRsun, r2 * kRsun, t1, t2, dist, p[19]));
+    gr = (g - gobs) / gerr;
     sincos(p[5], &sw_, &cw_);
   }
   __syncthreads();  // star-2 terms are in LDS
@@ -524,14 +533,26 @@ __device__ double wave_select(const uint64_t (&key)[VPT], uint32_t kth, uint64_t
   return dval(ans);
 }
 
-template <int VPT>
+// MULTI (catalog mode): the walker is list[blockIdx.x] and its light curve is
+// its target's slice (tab[wt[walker]]); n and kth come from the descriptor.
+template <int VPT, bool MULTI>
 __global__ __launch_bounds__(64) void hb_eval_wave_kernel(
     const double* __restrict__ t, const double* __restrict__ f, const double* __restrict__ isg,
     long n, long kth, const WalkerConst* __restrict__ wcs, double* __restrict__ logl,
-    double* __restrict__ tmpl_out, int mode, int slab_bytes) {
+    double* __restrict__ tmpl_out, int mode, int slab_bytes, const TargetDesc* __restrict__ tab,
+    const int* __restrict__ wt, const int* __restrict__ list) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int lane = threadIdx.x;
-  const int wv = blockIdx.x;
+  int wv = blockIdx.x;
+  if (MULTI) {
+    wv = list[blockIdx.x];
+    const TargetDesc& td = tab[wt[wv]];
+    t += td.off;
+    f += td.off;
+    isg += td.off;
+    n = td.n;
+    kth = td.kth;
+  }
   double* vals = reinterpret_cast<double*>(smem);
   uint32_t* hist = reinterpret_cast<uint32_t*>(smem);
   uint64_t* cand = reinterpret_cast<uint64_t*>(smem + slab_bytes);
@@ -709,10 +730,10 @@ __global__ __launch_bounds__(1024) void hb_median_kernel(double* __restrict__ a,
 // host launchers
 // ---------------------------------------------------------------------------
 hipError_t launch_prep(const double* d_params, int nwalk, const MagArgs& ma, WalkerConst* d_wc,
-                       hipStream_t s) {
+                       hipStream_t s, const TargetDesc* tab, const int* wt) {
   if (nwalk <= 0) return hipSuccess;
   hipLaunchKernelGGL(hb_prep_kernel, dim3((nwalk + kPrepWalkers - 1) / kPrepWalkers), dim3(2 * kPrepWalkers), 0, s,
-                     d_params, nwalk, ma, d_wc);
+                     d_params, nwalk, ma, d_wc, tab, wt);
   return hipGetLastError();
 }
 
@@ -737,9 +758,34 @@ template <int VPT>
 static hipError_t launch_wave_t(const EvalPlan& pl, const double* t, const double* f, const double* sg,
                                 const WalkerConst* wc, int nwalk, double* logl, double* tmpl, int mode,
                                 hipStream_t s) {
-  hipLaunchKernelGGL(hb_eval_wave_kernel<VPT>, dim3(nwalk), dim3(64), pl.lds_bytes, s, t, f, sg, pl.n, pl.kth,
-                     wc, logl, tmpl, mode, (int)pl.slab_bytes);
+  hipLaunchKernelGGL((hb_eval_wave_kernel<VPT, false>), dim3(nwalk), dim3(64), pl.lds_bytes, s, t, f, sg, pl.n,
+                     pl.kth, wc, logl, tmpl, mode, (int)pl.slab_bytes, nullptr, nullptr, nullptr);
   return hipGetLastError();
+}
+
+template <int VPT>
+static hipError_t launch_multi_t(size_t slab, const double* t, const double* f, const double* sg,
+                                 const TargetDesc* tab, const int* wt, const int* list, int count,
+                                 const WalkerConst* wc, double* logl, hipStream_t s) {
+  const size_t lds = slab + 8 * kCandMax;
+  hipLaunchKernelGGL((hb_eval_wave_kernel<VPT, true>), dim3(count), dim3(64), lds, s, t, f, sg, 0L, 0L, wc, logl,
+                     nullptr, 0, (int)slab, tab, wt, list);
+  return hipGetLastError();
+}
+
+hipError_t launch_eval_multi(int vpt, size_t slab, const double* t, const double* f, const double* sg,
+                             const TargetDesc* tab, const int* wt, const int* list, int count,
+                             const WalkerConst* wc, double* logl, hipStream_t s) {
+  if (count <= 0) return hipSuccess;
+  switch (vpt) {
+    case 1: return launch_multi_t<1>(slab, t, f, sg, tab, wt, list, count, wc, logl, s);
+    case 2: return launch_multi_t<2>(slab, t, f, sg, tab, wt, list, count, wc, logl, s);
+    case 4: return launch_multi_t<4>(slab, t, f, sg, tab, wt, list, count, wc, logl, s);
+    case 8: return launch_multi_t<8>(slab, t, f, sg, tab, wt, list, count, wc, logl, s);
+    case 16: return launch_multi_t<16>(slab, t, f, sg, tab, wt, list, count, wc, logl, s);
+    case 32: return launch_multi_t<32>(slab, t, f, sg, tab, wt, list, count, wc, logl, s);
+    default: return hipErrorInvalidValue;
+  }
 }
 
 hipError_t launch_eval(const EvalPlan& pl, const double* t, const double* f, const double* sg,
@@ -800,18 +846,28 @@ hipError_t preload_code_object() {
   return hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&hb_prep_kernel));
 }
 
+int wave_vpt_for(long n) {
+  if (n > 64 * 32) return 0;
+  int vpt = 1;
+  while ((long)vpt * 64 < n) vpt <<= 1;
+  return vpt;
+}
+
+// the template slab doubles as the 2^kSelBits-bin histogram of the select
+size_t wave_slab_bytes(long n) {
+  const size_t slab = (size_t)n * 8 > (size_t)(4u << kSelBits) ? (size_t)n * 8 : (size_t)(4u << kSelBits);
+  return (slab + 15) & ~(size_t)15;
+}
+
 EvalPlan make_plan(long n) {
   EvalPlan pl;
   pl.n = n;
   pl.kth = (n % 2 == 0) ? n / 2 : n / 2 + 1;  // likelihood3.c:97-99
   if (n <= 64 * 32) {  // one wave per walker, keys in registers
-    int vpt = 1;
-    while ((long)vpt * 64 < n) vpt <<= 1;
-    pl.vpt = vpt;
+    pl.vpt = wave_vpt_for(n);
     pl.nw = 1;
     pl.lds = true;
-    const size_t slab = (size_t)n * 8 > (size_t)(4u << kSelBits) ? (size_t)n * 8 : (size_t)(4u << kSelBits);
-    pl.slab_bytes = (slab + 15) & ~(size_t)15;
+    pl.slab_bytes = wave_slab_bytes(n);
     pl.lds_bytes = pl.slab_bytes + 8 * kCandMax;
     return pl;
   }

@@ -159,6 +159,24 @@ int hb_ctx_template_in_lds(const hb_ctx *ctx);
 /* Last error message of the calling thread ("" if none). */
 const char *hb_last_error(void);
 /* 1 if a HIP device is usable, 0 otherwise (never falls back to the CPU). */
+/* ---- catalog mode (config C5): many independent light curves on one GPU.
+ * Target k: t[k], flux[k], sigma[k] of n[k] cadences (2..2048), magnitude
+ * data mag5[5k..5k+4] / magerr4[4k..4k+3] (NULL: the reference fallback
+ * {1000,1,1,1,1} / 1e15).  All light curves are concatenated in HBM with a
+ * per-target descriptor table; one call evaluates every target's walkers
+ * with one prep launch and one eval launch per cadences-per-lane class
+ * (instead of one small launch per target).  params: sum(walkers[k]) x 21
+ * rows, target 0's walkers first, then target 1's, ...; logl likewise. ---- */
+typedef struct hb_catalog hb_catalog;
+hb_catalog *hb_catalog_create(int ntargets, const double *const *t, const double *const *flux,
+                              const double *const *sigma, const long *n, const double *mag5,
+                              const double *magerr4, int device);
+void hb_catalog_destroy(hb_catalog *cat);
+int hb_catalog_ntargets(const hb_catalog *cat);
+int hb_catalog_loglik(hb_catalog *cat, const double *params, const int *walkers, double *logl, void *stream);
+int hb_catalog_loglik_dev(hb_catalog *cat, const double *d_params, const int *walkers, double *d_logl,
+                          void *stream);
+
 int hb_device_available(void);
 
 /* ---- measurement helpers (bench.py): HIP events recorded on the caller's

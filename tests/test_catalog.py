@@ -1,0 +1,157 @@
+"""Catalog-sweep mode (config C5, hb_mcmc_amd/catalog.py, include/hbmi.h
+hb_catalog_*): many targets on one GPU, one batched launch per size class.
+
+CPU: the lockstep multi-target sampler driven by the oracle likelihood writes,
+for every target, exactly the files the single-target sampler writes for it
+alone (byte for byte); targets are dealt over ranks by cadence count.
+GPU: the batched catalog equals per-target contexts bit for bit and the
+oracle within 1e-10 (every size class N = 2..2048, zero-walker targets, per-
+target magnitude data); the GPU sweep equals the single-target GPU runs.
+"""
+import filecmp
+import os
+
+import numpy as np
+import pytest
+
+from conftest import golden
+
+LOGL_RTOL = 1e-10
+
+
+def synth_target(n, seed, orc, gmag=None):
+    from hb_mcmc_amd import synth
+
+    t, f, s = synth.dataset(n, orc.light_curve)
+    rng = np.random.default_rng(seed)
+    f = f + 1e-4 * rng.standard_normal(n)
+    if gmag is None:
+        return (t, f, s)
+    return (t, f, s, np.array([850.0, gmag, 1, 1, 1]), np.array([0.02, 1e15, 1e15, 1e15]))
+
+
+def tree_files(root):
+    out = []
+    for d, _, fs in os.walk(root):
+        out += [os.path.relpath(os.path.join(d, f), root) for f in fs]
+    return sorted(out)
+
+
+def test_deal_targets_balances_cadences():
+    from hb_mcmc_amd.catalog import deal_targets
+
+    rng = np.random.default_rng(3)
+    ncad = rng.integers(82, 1862, 256)
+    for world in (1, 2, 3, 8):
+        owner = deal_targets(ncad, world)
+        load = np.bincount(owner, weights=ncad, minlength=world)
+        assert len(owner) == 256 and set(owner) <= set(range(world))
+        assert load.max() - load.min() <= ncad.max()
+
+
+def test_catalog_sweep_equals_single_target_runs(tmp_path, oracle):
+    from hb_mcmc_amd.catalog import run_catalog
+    from hb_mcmc_amd.sampler import run_mcmc
+
+    g = golden("sampler_127079833.npz")
+    targets = [(g["lc_t"], g["lc_f"], g["lc_e"]), synth_target(300, 1, oracle), synth_target(97, 2, oracle)]
+    ids, periods = ["127079833", "9001", "9002"], [0.5021, 0.3157, 0.3157]
+    mag, err = np.array([1000.0, 1, 1, 1, 1]), np.full(4, 1e15)
+
+    def ll_multi(P, walkers):
+        out, o = [], 0
+        for k, w in enumerate(walkers):
+            t, f, s = targets[k]
+            out.append(oracle.loglike_batch(t, f, s, P[o:o + w], mag, err, 1) if w else np.empty(0))
+            o += w
+        return np.concatenate(out)
+
+    kw = dict(niter=260, nchains=9, npast=20, run=2)
+    res = run_catalog(targets, run_ids=ids, log10_periods=periods, out_root=str(tmp_path / "cat"), nthreads=2,
+                      loglik_multi=ll_multi, model=lambda k, p: oracle.light_curve(targets[k][0], p), **kw)
+    for k in range(3):
+        t, f, s = targets[k]
+        root = str(tmp_path / "one" / ids[k])
+        ref = run_mcmc(t, f, s, run_id=ids[k], log10_period=periods[k], out_root=root, nthreads=2,
+                       loglik=lambda P, t=t, f=f, s=s: oracle.loglike_batch(t, f, s, P, mag, err, 1),
+                       model=lambda p, t=t: oracle.light_curve(t, p), **kw)
+        croot = str(tmp_path / "cat" / ids[k])
+        files = tree_files(root)
+        assert files == tree_files(croot) and len(files) == 9 + 7
+        for rel in files:
+            assert filecmp.cmp(os.path.join(root, rel), os.path.join(croot, rel), shallow=False), (ids[k], rel)
+        assert np.array_equal(res[k]["xmap"], ref["xmap"]) and res[k]["logLmap"] == ref["logLmap"]
+        assert res[k]["accepted"] == ref["accepted"] and res[k]["swaps"] == ref["swaps"]
+
+
+# ------------------------------------------------------------------ GPU
+@pytest.mark.gpu
+def test_catalog_equals_per_target_contexts_and_oracle(hbmi, oracle):
+    from hb_mcmc_amd import synth
+    from hb_mcmc_amd.catalog import Catalog
+    from hb_mcmc_amd.likelihood import HBLikelihood
+
+    real = [golden("lc_real231937440.npz"), golden("lc_real237957506.npz")]
+    targets = [synth_target(n, i, oracle, gmag=(12.0 + 0.1 * i) if i % 3 == 0 else None)
+               for i, n in enumerate((2, 7, 63, 64, 65, 128, 300, 1024, 2048))]
+    targets += [(r["t"], r["f"], r["s"], r["mag"], r["magerr"]) for r in real]
+    walkers = np.array([3, 5, 0, 64, 1, 17, 33, 128, 9, 40, 24], dtype=np.int32)
+    P = synth.walkers(int(walkers.sum()), seed=11)
+    with Catalog(targets) as cat:
+        got = cat.loglike(P, walkers)
+        again = cat.loglike(P, walkers)
+        # a different layout on the same catalog
+        w2 = walkers[::-1].copy()
+        got2 = cat.loglike(P[:int(w2.sum())], w2)
+    assert np.array_equal(got, again, equal_nan=True)
+    o = 0
+    for k, tg in enumerate(targets):
+        w = int(walkers[k])
+        mag = tg[3] if len(tg) > 3 else synth.MAG_DEFAULT
+        err = tg[4] if len(tg) > 4 else synth.MAGERR_DEFAULT
+        if w:
+            with HBLikelihood(tg[0], tg[1], tg[2], mag, err) as L:
+                single = L.loglike(P[o:o + w])
+            assert np.array_equal(got[o:o + w], single, equal_nan=True), k
+            ref = oracle.loglike_batch(tg[0], tg[1], tg[2], P[o:o + w], mag, err, 8)
+            ok = ~np.isnan(ref)
+            assert np.array_equal(np.isnan(got[o:o + w]), ~ok)
+            rel = np.abs(got[o:o + w][ok] - ref[ok]) / np.maximum(1.0, np.abs(ref[ok]))
+            assert rel.max(initial=0) <= LOGL_RTOL, (k, rel.max())
+        o += w
+    o = 0
+    for k, tg in enumerate(targets):  # the reshuffled layout: target k owns w2[k] rows
+        w = int(w2[k])
+        if w:
+            mag = tg[3] if len(tg) > 3 else synth.MAG_DEFAULT
+            err = tg[4] if len(tg) > 4 else synth.MAGERR_DEFAULT
+            with HBLikelihood(tg[0], tg[1], tg[2], mag, err) as L:
+                assert np.array_equal(got2[o:o + w], L.loglike(P[o:o + w]), equal_nan=True), k
+        o += w
+
+
+@pytest.mark.gpu
+def test_catalog_rejects_long_light_curves(hbmi, oracle):
+    from hb_mcmc_amd import HBMIError
+    from hb_mcmc_amd.catalog import Catalog
+
+    with pytest.raises(HBMIError, match="2048"):
+        Catalog([synth_target(64, 0, oracle), synth_target(2049, 1, oracle)])
+
+
+@pytest.mark.gpu
+def test_gpu_catalog_sweep_equals_single_gpu_runs(hbmi, oracle, tmp_path):
+    from hb_mcmc_amd.catalog import run_catalog
+    from hb_mcmc_amd.sampler import run_mcmc
+
+    g = golden("sampler_127079833.npz")
+    targets = [(g["lc_t"], g["lc_f"], g["lc_e"]), synth_target(500, 4, oracle), synth_target(1500, 5, oracle)]
+    ids, periods = ["127079833", "9004", "9005"], [0.5021, 0.3157, 0.3157]
+    kw = dict(niter=300, nchains=16, npast=50, run=1)
+    run_catalog(targets, run_ids=ids, log10_periods=periods, out_root=str(tmp_path / "cat"), **kw)
+    for k in range(3):
+        root = str(tmp_path / "one" / ids[k])
+        run_mcmc(*targets[k], run_id=ids[k], log10_period=periods[k], out_root=root, **kw)
+        for rel in tree_files(root):
+            assert filecmp.cmp(os.path.join(root, rel), os.path.join(str(tmp_path / "cat" / ids[k]), rel),
+                               shallow=False), (ids[k], rel)
