@@ -155,3 +155,50 @@ def test_gpu_catalog_sweep_equals_single_gpu_runs(hbmi, oracle, tmp_path):
         for rel in tree_files(root):
             assert filecmp.cmp(os.path.join(root, rel), os.path.join(str(tmp_path / "cat" / ids[k]), rel),
                                shallow=False), (ids[k], rel)
+
+
+@pytest.mark.gpu
+def test_catalog_cli_two_ranks_equals_hb_mcmc_cli(hbmi, oracle, tmp_path):
+    """torchrun, 2 ranks: targets dealt by cadence count, each rank sweeps its
+    own (no collective); every target's files equal the hb_mcmc CLI's."""
+    import socket
+    import subprocess
+    import sys
+
+    from conftest import ROOT
+    from hb_mcmc_amd.hbio import write_folded_lc
+
+    g = golden("sampler_127079833.npz")
+    lcs = {"127079833": (g["lc_t"], g["lc_f"], g["lc_e"]), "9007": synth_target(640, 7, oracle)[:3],
+           "9008": synth_target(1200, 8, oracle)[:3]}
+    periods = {"127079833": 0.5021, "9007": 0.3157, "9008": 0.3157}
+    cat_root, one_root = str(tmp_path / "cat"), str(tmp_path / "one")
+    for root in [cat_root] + [os.path.join(one_root, tic) for tic in lcs]:
+        d = os.path.join(root, "data", "lightcurves", "folded_lightcurves")
+        os.makedirs(d, exist_ok=True)
+        for tic, (t, f, e) in lcs.items():
+            write_folded_lc(os.path.join(d, f"{tic}_new.txt"), t, f, e)
+    pfile = str(tmp_path / "periods.txt")
+    with open(pfile, "w") as fh:
+        fh.writelines(f"{tic} {p}\n" for tic, p in periods.items())
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port), "-m", "hb_mcmc_amd.catalog",
+                        "300", "--root", cat_root, "--periods", pfile, "--chains", "12", "--npast", "40"],
+                       capture_output=True, text=True, timeout=600, cwd=ROOT, env=env)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    assert "rank 0 target" in r.stdout and "rank 1 target" in r.stdout
+    exe = os.path.join(ROOT, "hb_mcmc_amd", "lib", "hb_mcmc")
+    for tic, p in periods.items():
+        root = os.path.join(one_root, tic)
+        r1 = subprocess.run([exe, "300", tic, str(p), "0", "--root", root, "--chains", "12", "--npast", "40",
+                             "--quiet"], capture_output=True, text=True, timeout=600)
+        assert r1.returncode == 0, r1.stderr
+        ours = os.path.join(cat_root, tic)
+        files = [rel for rel in tree_files(root) if not rel.startswith(os.path.join("data", "lightcurves", "folded"))]
+        assert len(files) == 12 + 7
+        for rel in files:
+            assert filecmp.cmp(os.path.join(root, rel), os.path.join(ours, rel), shallow=False), (tic, rel)
