@@ -207,6 +207,10 @@ extern "C" hb_ctx* hb_create(const double* t, const double* f, const double* sig
     set_err_msg("hb_create: need N >= 2 cadences (the reference median reads out of bounds for N=1)");
     return nullptr;
   }
+  if (n > (1L << 28)) {  // kernels index cadences with 32-bit ints
+    set_err_msg("hb_create: N > 2^28 cadences is not supported");
+    return nullptr;
+  }
   if (!t || !f || !sigma) {
     set_err_msg("hb_create: null array");
     return nullptr;

@@ -464,44 +464,123 @@ __device__ __noinline__ double hb_cadence_flux_slow(double t, const WalkerConst*
 // basic block (ILP for the fp64 dependency chains).  Lanes whose angles
 // leave the fast sincos/fmod domain set `bad`; the caller reruns them
 // through hb_cadence_flux (ocml path) under one wave-uniform branch.
+//
+// Mean anomaly: q = trunc(x / 2pi), r = x - q 2pi by one FMA.  When q is the
+// true quotient r IS fmod(x, 2pi) (exact), and r lies strictly inside
+// (0, 2pi) on x's side; an off-by-one q lands r on or outside that interval
+// (FMA rounding is monotone), so those lanes -- and r == 0, where the sign of
+// zero matters -- take fmod_twopi_fast under a wave-uniform branch.
+//
+// Newton on E - e sin E = M (likelihood3.c:160): the reference always takes
+// 5 steps; here the wave leaves the loop once every lane's predicted next
+// correction e d^2 / (2 (1 - e cos E)) is below 2^-52 absolute, i.e. the
+// remaining steps would only move E by rounding noise (the
+// parity budget is 1e-12 on the template).  e = 0.23 (the C2 workload)
+// converges in 3 steps, e -> 0.99 keeps all 5.  The step uses the v_rcp_f64
+// seed with one Newton refinement (relative error ~2^-48, which only scales
+// the step and is absorbed by the next one); (sin, cos) follow E by rotation
+// through the step (Taylor to d^11 / d^12, truncation < 3e-18 for |d| <= 0.25)
+// (fewer terms when the wave's steps are below 2^-10 / 2^-22) when the whole
+// wave's steps are small, else by direct evaluation.
+// The light-curve polynomial is written with explicit FMAs (the build uses
+// -ffp-contract=off so that the reference-order paths keep their rounding).
 // ------------------------------------------------------------------------
+constexpr double kRotMaxK = 0.25;
+__device__ __forceinline__ void rotate_back_wide(double d, double z, double& s, double& c) {
+  // sin d = d (1 + z S(z)), cos d = 1 + z C(z), z = d^2
+  const double sp = z * fma(z, fma(z, fma(z, fma(z, -1.0 / 39916800.0, 1.0 / 362880.0), -1.0 / 5040.0),
+                                 1.0 / 120.0), -1.0 / 6.0);
+  const double sd = fma(d, sp, d);
+  const double cd = fma(z, fma(z, fma(z, fma(z, fma(z, fma(z, 1.0 / 479001600.0, -1.0 / 3628800.0),
+                                                        1.0 / 40320.0), -1.0 / 720.0), 1.0 / 24.0), -0.5),
+                        1.0);
+  const double s2 = fma(s, cd, -c * sd);  // sin(E - d) = s cos d - c sin d
+  const double c2 = fma(c, cd, s * sd);   // cos(E - d) = c cos d + s sin d
+  s = s2;
+  c = c2;
+}
+// |d| <= 2^-10: Taylor to d^5 / d^4 (truncation < 2e-20)
+__device__ __forceinline__ void rotate_back_mid(double d, double z, double& s, double& c) {
+  const double sd = fma(d, z * fma(z, 1.0 / 120.0, -1.0 / 6.0), d);
+  const double cd = fma(z, fma(z, 1.0 / 24.0, -0.5), 1.0);
+  const double s2 = fma(s, cd, -c * sd);
+  const double c2 = fma(c, cd, s * sd);
+  s = s2;
+  c = c2;
+}
+// |d| <= 2^-22: sin d = d, cos d = 1 - d^2/2 (truncation < 3e-21)
+__device__ __forceinline__ void rotate_back_tiny(double d, double z, double& s, double& c) {
+  const double cd = fma(z, -0.5, 1.0);
+  const double s2 = fma(s, cd, -c * d);
+  const double c2 = fma(c, cd, s * d);
+  s = s2;
+  c = c2;
+}
+
 template <int K>
 __device__ __forceinline__ void hb_cadence_flux_k(const double (&t)[K], const WalkerConst& w,
                                                   double (&v)[K], bool& bad) {
   const double e = w.e;
   const double aR2 = w.aR * w.aR, rsum2 = w.rsum * w.rsum;
   double m[K], E[K], s[K], c[K];
-  bool ok = true;
+  bool ok = true, exact = false;
 #pragma unroll
   for (int k = 0; k < K; ++k) {
-    const double mraw = fma(t[k], kDay, w.mB) * w.mA;
-    ok &= sincos_fast_ok(mraw);
-    m[k] = fmod_twopi_fast(mraw);
-    const double sg = sign_sin_reduced(m[k]);
-    E[k] = (sg == 0.0) ? m[k] : m[k] + w.e085 * sg;
+    const double x = fma(t[k], kDay, w.mB) * w.mA;
+    ok &= sincos_fast_ok(x);
+    const double q = trunc(x * 0.15915494309189533577);
+    const double r = fma(-q, kTwoPi, x);
+    // r != 0, |r| < 2pi and sign(r) == sign(x), branch-free
+    const bool same_sign = (__double_as_longlong(r) ^ __double_as_longlong(x)) >= 0;
+    const bool inside = same_sign & (fabs(r) < kTwoPi) & (r != 0.0);
+    exact |= !inside;
+    m[k] = r;
+    // sign(sin m) * 0.85 e for m in (-2pi, 2pi) \ {0} (sign_sin_reduced)
+    const bool plus = (fabs(r) <= kPi) != (r < 0.0);
+    E[k] = r + (plus ? w.e085 : -w.e085);
   }
-  // Newton on E - e sin E = M, 5 steps (likelihood3.c:160).  Step 1 evaluates
-  // sin/cos directly; later steps rotate (s, c) by the previous step when the
-  // whole wave's steps are below kRotMax (wave-uniform branch), otherwise
-  // they re-evaluate directly.  The 6th evaluation (final E) likewise.
+  if (__any(exact)) {  // rare: x near a multiple of 2pi, or r == 0
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const double x = fma(t[k], kDay, w.mB) * w.mA;
+      m[k] = fmod_twopi_fast(x);
+      const double sg = sign_sin_reduced(m[k]);
+      E[k] = (sg == 0.0) ? m[k] : m[k] + w.e085 * sg;
+    }
+  }
 #pragma unroll
   for (int k = 0; k < K; ++k) {
     ok &= sincos_fast_ok(E[k]);
     sincos_fast(E[k], &s[k], &c[k]);
   }
-  double d[K];
 #pragma unroll
   for (int it = 0; it < 5; ++it) {
-    bool small = true;
+    bool small = true, mid = true, tiny = true, conv = true;
+    double d[K], z[K];
 #pragma unroll
     for (int k = 0; k < K; ++k) {
-      d[k] = fast_div((E[k] - e * s[k]) - m[k], 1.0 - e * c[k]);
+      const double den = fma(-e, c[k], 1.0);
+      double y = __builtin_amdgcn_rcp(den);
+      y = fma(fma(-den, y, 1.0), y, y);
+      d[k] = ((E[k] - e * s[k]) - m[k]) * y;
       E[k] = E[k] - d[k];
-      small &= fabs(d[k]) <= kRotMax;
+      z[k] = d[k] * d[k];
+      const double ad = fabs(d[k]);
+      small &= ad <= kRotMaxK;
+      mid &= ad <= 0x1p-10;
+      tiny &= ad <= 0x1p-22;
+      conv &= e * z[k] <= 0x1p-51 * den;
     }
-    if (__all(small)) {
+    // rotation degree by the wave's largest step (wave-uniform branches)
+    if (__all(tiny)) {
 #pragma unroll
-      for (int k = 0; k < K; ++k) rotate_back(d[k], s[k], c[k]);
+      for (int k = 0; k < K; ++k) rotate_back_tiny(d[k], z[k], s[k], c[k]);
+    } else if (__all(mid)) {
+#pragma unroll
+      for (int k = 0; k < K; ++k) rotate_back_mid(d[k], z[k], s[k], c[k]);
+    } else if (__all(small)) {
+#pragma unroll
+      for (int k = 0; k < K; ++k) rotate_back_wide(d[k], z[k], s[k], c[k]);
     } else {
 #pragma unroll
       for (int k = 0; k < K; ++k) {
@@ -509,34 +588,38 @@ __device__ __forceinline__ void hb_cadence_flux_k(const double (&t)[K], const Wa
         sincos_fast(E[k], &s[k], &c[k]);
       }
     }
+    if (__all(conv)) break;
   }
   bool need_ecl = false;
   double dd[K], zz[K];
 #pragma unroll
   for (int k = 0; k < K; ++k) {
-    const double den = 1.0 - e * c[k];
+    const double den = fma(-e, c[k], 1.0);
     const double inv = fast_rcp(den);
     const double cnu = (c[k] - e) * inv;
-    const double snu = w.sq1me2 * s[k] * inv;
-    const double cu = w.cw * cnu - w.sw * snu;
-    const double su = w.sw * cnu + w.cw * snu;
-    const double b = (1.0 + e * cnu) * w.inv1me2;
+    const double snu = (w.sq1me2 * s[k]) * inv;
+    const double cu = fma(w.cw, cnu, -w.sw * snu);
+    const double su = fma(w.sw, cnu, w.cw * snu);
+    const double b = fma(e, cnu, 1.0) * w.inv1me2;
     const double sci = su * w.ci;
-    dd[k] = den * den * (cu * cu + sci * sci);  // (projected separation / a)^2; sqrt only on eclipse lanes
+    dd[k] = (den * den) * fma(cu, cu, sci * sci);  // (projected separation / a)^2; sqrt only on eclipse lanes
     zz[k] = su * w.si;
-    const double c2 = (cu - su) * (cu + su);
-    const double s3 = su * (3.0 - 4.0 * su * su);
-    const double c4 = 2.0 * c2 * c2 - 1.0;
+    const double c2 = (cu - su) * (cu + su);          // cos 2u
+    const double su2 = su * su;
+    const double s3 = su * fma(-4.0, su2, 3.0);       // sin 3u
+    const double c4 = fma(2.0 * c2, c2, -1.0);        // cos 4u
     const double b2 = b * b;
-    const double b3 = b2 * b;
+    // b^2 [A2 + b (A3 + b (A4 + b A5))] + kconst + kb cos u
+    const double a5 = fma(w.kc4, c4, fma(w.kc22, c2, w.kam3));
+    const double a4 = fma(w.ks3, s3, w.ks1 * su);
+    const double a3 = fma(w.kc21, c2, w.kam2);
+    const double a2 = fma(w.krs, su, fma(w.kr2, c2, w.kr0));
+    double h = fma(b, a5, a4);
+    h = fma(b, h, a3);
+    h = fma(b, h, a2);
     // values stay ~1 like the reference's Amag1 + Amag2 (one sign, one
     // exponent: the median radix-select resolves them in one digit pass)
-    double val = w.kconst + w.kb * cu;
-    val += b2 * (w.kr0 + w.kr2 * c2 + w.krs * su);
-    val += b3 * (w.kam2 + w.kc21 * c2);
-    val += (b2 * b2) * (w.ks1 * su + w.ks3 * s3);
-    val += (b3 * b2) * (w.kam3 + w.kc22 * c2 + w.kc4 * c4);
-    v[k] = val;
+    v[k] = fma(b2, h, fma(w.kb, cu, w.kconst));
     // squared test: a lane within an ulp of tangency may go either way, where
     // the overlap area (~eps^1.5) is zero to working precision
     need_ecl |= (dd[k] * aR2 < rsum2) & (zz[k] != 0.0);

@@ -27,6 +27,14 @@ using namespace hbdev;
 #ifndef HB_K
 #define HB_K 4  // cadences interleaved per lane in the model loop (4: +1% over 2 on MI355X, 117 VGPRs)
 #endif
+#ifndef HB_WAVES_PER_EU
+#define HB_WAVES_PER_EU 4  // keep the wave kernel at <= 128 VGPRs: 4 waves per SIMD
+#endif
+#if HB_WAVES_PER_EU > 0
+#define HB_WPE_ATTR __attribute__((amdgpu_waves_per_eu(HB_WAVES_PER_EU)))
+#else
+#define HB_WPE_ATTR
+#endif
 #ifndef HB_ABLATE_MODEL
 #define HB_ABLATE_MODEL 0
 #endif
@@ -209,24 +217,21 @@ __device__ __forceinline__ double wave_sum(double v) {
 // per iteration (ILP for the fp64 Kepler chains), next iteration's times
 // prefetched; values go to vals[], min/max order keys returned per lane.
 template <int NT>
-__device__ __forceinline__ void model_pass(const double* __restrict__ t, long n, const WalkerConst& w,
+__device__ __forceinline__ void model_pass(const double* __restrict__ t, int n, const WalkerConst& w,
                                            double* vals, int tid, uint64_t& kmn_out, uint64_t& kmx_out) {
   constexpr int K = HB_K;
-  uint64_t kmn = ~0ull, kmx = 0ull;
-  const long last = n - 1;
+  // running min/max as doubles (v_min/v_max_f64); NaN lanes are tracked and
+  // the order keys recomputed from vals[] in that (never observed) case
+  double vmn = __builtin_inf(), vmx = -__builtin_inf();
+  bool nan = false;
+  const int last = n - 1;
   double tk[K];
 #pragma unroll
-  for (int k = 0; k < K; ++k) {
-    const long i = (long)k * NT + tid;
-    tk[k] = t[i < last ? i : last];
-  }
-  for (long base = 0; base < n; base += (long)K * NT) {
+  for (int k = 0; k < K; ++k) tk[k] = t[min(k * NT + tid, last)];
+  for (int base = 0; base < n; base += K * NT) {
     double tn[K];
 #pragma unroll
-    for (int k = 0; k < K; ++k) {
-      const long i = base + (long)(K + k) * NT + tid;
-      tn[k] = t[i < last ? i : last];
-    }
+    for (int k = 0; k < K; ++k) tn[k] = t[min(base + (K + k) * NT + tid, last)];
     double v[K];
     bool bad;
 #if HB_ABLATE_MODEL  // experiment builds only: trivial model, same data flow
@@ -244,14 +249,26 @@ __device__ __forceinline__ void model_pass(const double* __restrict__ t, long n,
     }
 #pragma unroll
     for (int k = 0; k < K; ++k) {
-      const long i = base + (long)k * NT + tid;
+      const int i = base + k * NT + tid;
       if (i < n) {
         vals[i] = v[k];
-        const uint64_t key = dkey(v[k]);
-        kmn = key < kmn ? key : kmn;
-        kmx = key > kmx ? key : kmx;
+        vmn = fmin(vmn, v[k]);
+        vmx = fmax(vmx, v[k]);
+        nan |= v[k] != v[k];
       }
       tk[k] = tn[k];
+    }
+  }
+  // keys of the extremes; -0.0 / +0.0 compare equal but key apart: take the
+  // outer key of a zero extreme so [kmn, kmx] brackets every key
+  uint64_t kmn = dkey(vmn == 0.0 ? -0.0 : vmn), kmx = dkey(vmx == 0.0 ? 0.0 : vmx);
+  if (__any(nan)) {
+    kmn = ~0ull;
+    kmx = 0ull;
+    for (int i = tid; i < n; i += NT) {
+      const uint64_t key = dkey(vals[i]);
+      kmn = key < kmn ? key : kmn;
+      kmx = key > kmx ? key : kmx;
     }
   }
   kmn_out = kmn;
@@ -374,6 +391,12 @@ __global__ __launch_bounds__(64 * NW) void hb_eval_kernel(
   double* vals = LDS ? reinterpret_cast<double*>(smem + sizeof(SelShared))
                      : scratch + (size_t)wv * (size_t)n;
   const WalkerConst& w = wcs[wv];
+  // Roche overflow replaces chi^2 by 1e15 whatever the template is
+  // (likelihood3.c:866-869): the logL needs no light curve (block-uniform exit)
+  if (mode == 0 && w.roche != 0.0) {
+    if (tid == 0) logl[wv] = -kBig / 2.0;
+    return;
+  }
 
   // 1. model flux for every cadence
   uint64_t kmn, kmx;
@@ -536,7 +559,7 @@ __device__ double wave_select(const uint64_t (&key)[VPT], uint32_t kth, uint64_t
 // MULTI (catalog mode): the walker is list[blockIdx.x] and its light curve is
 // its target's slice (tab[wt[walker]]); n and kth come from the descriptor.
 template <int VPT, bool MULTI>
-__global__ __launch_bounds__(64) void hb_eval_wave_kernel(
+__global__ __launch_bounds__(64) HB_WPE_ATTR void hb_eval_wave_kernel(
     const double* __restrict__ t, const double* __restrict__ f, const double* __restrict__ isg,
     long n, long kth, const WalkerConst* __restrict__ wcs, double* __restrict__ logl,
     double* __restrict__ tmpl_out, int mode, int slab_bytes, const TargetDesc* __restrict__ tab,
@@ -557,6 +580,10 @@ __global__ __launch_bounds__(64) void hb_eval_wave_kernel(
   uint32_t* hist = reinterpret_cast<uint32_t*>(smem);
   uint64_t* cand = reinterpret_cast<uint64_t*>(smem + slab_bytes);
   const WalkerConst& w = wcs[wv];
+  if (mode == 0 && w.roche != 0.0) {  // likelihood3.c:866-869, see hb_eval_kernel
+    if (lane == 0) logl[wv] = -kBig / 2.0;
+    return;
+  }
 
   uint64_t kmn, kmx;
   model_pass<64>(t, n, w, vals, lane, kmn, kmx);
