@@ -441,8 +441,21 @@ __global__ __launch_bounds__(64 * NW) void hb_eval_kernel(
 // reused as a histogram (11-bit first digit), exact rank among <= 64
 // survivors.  kth is the 0-based rank of likelihood3.c:97-101.
 // ---------------------------------------------------------------------------
-constexpr int kSelBits = 11;
-constexpr int kCandMax = 64;
+#ifndef HB_SEL_BITS1
+#define HB_SEL_BITS1 10
+#endif
+#ifndef HB_SEL_BITS2
+#define HB_SEL_BITS2 8
+#endif
+constexpr int kSelBits = HB_SEL_BITS1;   // first digit (whole light curve)
+constexpr int kSelBits2 = HB_SEL_BITS2;  // later digits (the survivors of one bin)
+#ifndef HB_SEL_V
+#define HB_SEL_V 2  // 1: shuffle-based select (previous version)
+#endif
+#ifndef HB_CAND
+#define HB_CAND 64
+#endif
+constexpr int kCandMax = HB_CAND;  // survivors ranked directly (<= 64: one per lane)
 
 template <int VPT>
 __device__ double wave_select(const uint64_t (&key)[VPT], uint32_t kth, uint64_t kmin, uint64_t kmax,
@@ -454,8 +467,10 @@ __device__ double wave_select(const uint64_t (&key)[VPT], uint32_t kth, uint64_t
   uint64_t prefix = kmin & mask;
   uint32_t kk = kth;
   uint32_t cnt = 0;
+  int bits = kSelBits;
   while (true) {
-    const int width = hi + 1 < kSelBits ? hi + 1 : kSelBits;
+    const int width = hi + 1 < bits ? hi + 1 : bits;
+    bits = kSelBits2;
     const int shift = hi + 1 - width;
     const uint32_t nb = 1u << width, dm = nb - 1u;
     for (uint32_t b = lane; b < nb; b += 64) hist[b] = 0u;
@@ -556,6 +571,177 @@ __device__ double wave_select(const uint64_t (&key)[VPT], uint32_t kth, uint64_t
   return dval(ans);
 }
 
+// ---------------------------------------------------------------------------
+// Wave-level primitives without LDS round trips: DPP moves (GCN row_shr /
+// row_bcast / quad_perm / mirrors) and v_readlane.  __shfl* lower to
+// ds_bpermute, one LDS round trip per step; these stay in the VALU.
+// ---------------------------------------------------------------------------
+// inclusive prefix sum over the 64 lanes (all lanes active)
+__device__ __forceinline__ uint32_t wave_scan_incl(uint32_t x) {
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, true);   // row_shr:1
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, true);   // row_shr:2
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, true);   // row_shr:4
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, true);   // row_shr:8
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);  // row_bcast:15 -> rows 1, 3
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);  // row_bcast:31 -> rows 2, 3
+  return x;
+}
+
+template <int CTRL>
+__device__ __forceinline__ uint64_t dpp_u64(uint64_t v) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)v, CTRL, 0xf, 0xf, false);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(v >> 32), CTRL, 0xf, 0xf, false);
+  return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ uint64_t readlane_u64(uint64_t v, int l) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l);
+  return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ double readlane_f64(double v, int l) {
+  return __longlong_as_double((long long)readlane_u64((uint64_t)__double_as_longlong(v), l));
+}
+
+// Butterfly inside each row of 16 (xor 1, xor 2, half mirror, mirror: every
+// lane of a row ends with the same row result, operands commuted only), then
+// the four row results through v_readlane.  Op must be commutative.
+template <class Op>
+__device__ __forceinline__ uint64_t wave_reduce_u64(uint64_t v, Op op) {
+  v = op(v, dpp_u64<0xB1>(v));   // quad_perm [1,0,3,2]
+  v = op(v, dpp_u64<0x4E>(v));   // quad_perm [2,3,0,1]
+  v = op(v, dpp_u64<0x141>(v));  // row_half_mirror
+  v = op(v, dpp_u64<0x140>(v));  // row_mirror
+  return op(op(readlane_u64(v, 0), readlane_u64(v, 16)), op(readlane_u64(v, 32), readlane_u64(v, 48)));
+}
+struct OpMinU64 { __device__ uint64_t operator()(uint64_t a, uint64_t b) const { return a < b ? a : b; } };
+struct OpMaxU64 { __device__ uint64_t operator()(uint64_t a, uint64_t b) const { return a > b ? a : b; } };
+struct OpAddF64 {
+  __device__ uint64_t operator()(uint64_t a, uint64_t b) const {
+    return (uint64_t)__double_as_longlong(__longlong_as_double((long long)a) + __longlong_as_double((long long)b));
+  }
+};
+__device__ __forceinline__ double wave_sum_dpp(double v) {
+  return __longlong_as_double((long long)wave_reduce_u64((uint64_t)__double_as_longlong(v), OpAddF64()));
+}
+
+// One radix pass with 2^B bins over the keys that match `prefix` under
+// `mask`: histogram (LDS atomics), DPP scan of the per-lane bin sums, the
+// owning lane found by ballot, its bin/offset/count read back by v_readlane.
+template <int VPT, int B>
+__device__ __forceinline__ void select_pass(const uint64_t (&key)[VPT], uint32_t* hist, int lane, int& hi,
+                                            uint64_t& mask, uint64_t& prefix, uint32_t& kk, uint32_t& cnt) {
+  static_assert(B >= 8 && B <= 11, "4..32 bins per lane");
+  constexpr int PER = (1 << B) / 64;  // consecutive bins owned by a lane
+  constexpr int Q = PER / 4;          // uint4 per lane
+  const int width = hi + 1 < B ? hi + 1 : B;
+  const int shift = hi + 1 - width;
+  const uint32_t dm = (1u << width) - 1u;
+  uint4* h4 = reinterpret_cast<uint4*>(hist);
+#pragma unroll
+  for (int q = 0; q < Q; ++q) h4[lane * Q + q] = make_uint4(0u, 0u, 0u, 0u);
+  __syncthreads();
+#pragma unroll
+  for (int v = 0; v < VPT; ++v)
+    if ((key[v] & mask) == prefix) atomicAdd(&hist[(uint32_t)(key[v] >> shift) & dm], 1u);
+  __syncthreads();
+  uint32_t h[PER];
+#pragma unroll
+  for (int q = 0; q < Q; ++q) {
+    const uint4 x = h4[lane * Q + q];
+    h[4 * q] = x.x;
+    h[4 * q + 1] = x.y;
+    h[4 * q + 2] = x.z;
+    h[4 * q + 3] = x.w;
+  }
+  uint32_t g[Q];
+  uint32_t local = 0;
+#pragma unroll
+  for (int q = 0; q < Q; ++q) {
+    g[q] = h[4 * q] + h[4 * q + 1] + h[4 * q + 2] + h[4 * q + 3];
+    local += g[q];
+  }
+  const uint32_t incl = wave_scan_incl(local);
+  const uint32_t excl = incl - local;
+  const unsigned long long own = __ballot(excl <= kk && kk < incl);
+  const int owner = __builtin_amdgcn_readfirstlane(__ffsll((long long)own) - 1);
+  // every lane walks its own bins (group of 4, then bin); the owner's is kept
+  uint32_t before = excl;
+  int grp = 0;
+  bool go = true;
+#pragma unroll
+  for (int q = 0; q + 1 < Q; ++q) {
+    go = go && (kk >= before + g[q]);
+    if (go) { before += g[q]; grp = q + 1; }
+  }
+  uint32_t c0 = h[0], c1 = h[1], c2 = h[2], c3 = h[3];
+#pragma unroll
+  for (int q = 1; q < Q; ++q)
+    if (grp == q) { c0 = h[4 * q]; c1 = h[4 * q + 1]; c2 = h[4 * q + 2]; c3 = h[4 * q + 3]; }
+  uint32_t bin = (uint32_t)(lane * PER + 4 * grp), c = c0;
+  if (kk >= before + c) { before += c; ++bin; c = c1;
+    if (kk >= before + c) { before += c; ++bin; c = c2;
+      if (kk >= before + c) { before += c; ++bin; c = c3; } } }
+  bin = (uint32_t)__builtin_amdgcn_readlane((int)bin, owner);
+  before = (uint32_t)__builtin_amdgcn_readlane((int)before, owner);
+  cnt = (uint32_t)__builtin_amdgcn_readlane((int)c, owner);
+  kk -= before;
+  prefix |= (uint64_t)bin << shift;
+  mask |= (uint64_t)dm << shift;
+  hi = shift - 1;
+  __syncthreads();  // histogram reads done before the next clear
+}
+
+template <int VPT>
+__device__ __forceinline__ double wave_select2(const uint64_t (&key)[VPT], uint32_t kth, uint64_t kmin,
+                                               uint64_t kmax, uint32_t* hist, uint64_t* cand) {
+  const int lane = threadIdx.x;
+  if (kmin == kmax) return dval(kmin);
+  int hi = 63 - __builtin_clzll(kmin ^ kmax);
+  uint64_t mask = (hi == 63) ? 0ull : ~((2ull << hi) - 1ull);
+  uint64_t prefix = kmin & mask;
+  uint32_t kk = kth, cnt = 0;
+  select_pass<VPT, kSelBits>(key, hist, lane, hi, mask, prefix, kk, cnt);
+  while (cnt > (uint32_t)kCandMax && hi >= 0) select_pass<VPT, kSelBits2>(key, hist, lane, hi, mask, prefix, kk, cnt);
+  if (hi < 0) return dval(prefix);
+  // compact the cnt survivors, then rank them exactly
+  uint32_t basec = 0;
+#pragma unroll
+  for (int v = 0; v < VPT; ++v) {
+    const bool m = (key[v] & mask) == prefix;
+    const unsigned long long bal = __ballot(m);
+    if (m) cand[basec + __popcll(bal & ((1ull << lane) - 1ull))] = key[v];
+    basec += (uint32_t)__popcll(bal);
+  }
+  __syncthreads();
+  const uint64_t mine = (uint32_t)lane < cnt ? cand[lane] : ~0ull;
+  uint32_t r = 0;
+  for (uint32_t j = 0; j < cnt; ++j) {
+    const uint64_t o = cand[j];
+    r += (o < mine) | ((o == mine) & (j < (uint32_t)lane));
+  }
+  const unsigned long long hit = __ballot((uint32_t)lane < cnt && r == kk);
+  const int who = __builtin_amdgcn_readfirstlane(__ffsll((long long)hit) - 1);
+  return dval(readlane_u64(mine, who));
+}
+
+#ifndef HB_KEY_PERM
+#define HB_KEY_PERM 1
+#endif
+// Cadence held in key slot v of `lane`.  A light curve is smooth, so 64
+// consecutive cadences mostly share one histogram bin and a wave's LDS atomic
+// would serialise on one address; the skewed transpose (lane owns cadences
+// lane*VPT .. lane*VPT+VPT-1, visited in rotated order) gives each atomic
+// instruction 64 cadences spread over the whole light curve, and keeps the
+// ds_read_b64 of the slab at <= 2-way bank conflicts.
+template <int VPT>
+__device__ __forceinline__ int key_index(int v, int lane) {
+#if HB_KEY_PERM
+  return lane * VPT + ((v + lane) & (VPT - 1));
+#else
+  return v * 64 + lane;
+#endif
+}
+
 // MULTI (catalog mode): the walker is list[blockIdx.x] and its light curve is
 // its target's slice (tab[wt[walker]]); n and kth come from the descriptor.
 template <int VPT, bool MULTI>
@@ -587,20 +773,29 @@ __global__ __launch_bounds__(64) HB_WPE_ATTR void hb_eval_wave_kernel(
 
   uint64_t kmn, kmx;
   model_pass<64>(t, n, w, vals, lane, kmn, kmx);
+#if HB_SEL_V == 1
   kmn = wave_min_u64(kmn);
   kmx = wave_max_u64(kmx);
+#else
+  kmn = wave_reduce_u64(kmn, OpMinU64());
+  kmx = wave_reduce_u64(kmx, OpMaxU64());
+#endif
   __syncthreads();
   uint64_t key[VPT];
 #pragma unroll
   for (int v = 0; v < VPT; ++v) {
-    const long i = (long)v * 64 + lane;
+    const int i = key_index<VPT>(v, lane);
     key[v] = i < n ? dkey(vals[i]) : ~0ull;  // padding sorts last, never selected
   }
   __syncthreads();  // the slab becomes the histogram
 #if HB_ABLATE_SELECT
   const double med = dval(kmn);
 #else
+#if HB_SEL_V == 1
   const double med = wave_select<VPT>(key, (uint32_t)kth, kmn, kmx, hist, cand);
+#else
+  const double med = wave_select2<VPT>(key, (uint32_t)kth, kmn, kmx, hist, cand);
+#endif
 #endif
 
   const double blend = w.blend, one_m_blend = 1.0 - w.blend, tune = w.tune;
@@ -608,7 +803,7 @@ __global__ __launch_bounds__(64) HB_WPE_ATTR void hb_eval_wave_kernel(
     double* o = tmpl_out + (size_t)wv * (size_t)n;
 #pragma unroll
     for (int v = 0; v < VPT; ++v) {
-      const long i = (long)v * 64 + lane;
+      const int i = key_index<VPT>(v, lane);
       if (i < n) {
         const double m = (dval(key[v]) - med) + 1.0;
         o[i] = (blend + m * one_m_blend) * tune;
@@ -619,7 +814,7 @@ __global__ __launch_bounds__(64) HB_WPE_ATTR void hb_eval_wave_kernel(
   double acc = 0.0;
 #pragma unroll
   for (int v = 0; v < VPT; ++v) {
-    const long i = (long)v * 64 + lane;
+    const int i = key_index<VPT>(v, lane);
     if (i < n) {
       double m = (dval(key[v]) - med) + 1.0;
       m = (blend + m * one_m_blend) * tune;
@@ -627,7 +822,11 @@ __global__ __launch_bounds__(64) HB_WPE_ATTR void hb_eval_wave_kernel(
       acc += r * r;
     }
   }
+#if HB_SEL_V == 1
   const double chi2 = wave_sum(acc);
+#else
+  const double chi2 = wave_sum_dpp(acc);
+#endif
   if (lane == 0) {
     double c = chi2 + w.chi2_extra;
     if (w.roche != 0.0) c = kBig;
