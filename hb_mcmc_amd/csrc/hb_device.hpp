@@ -480,11 +480,14 @@ __device__ __noinline__ double hb_cadence_flux_slow(double t, const WalkerConst*
 // seed with one Newton refinement (relative error ~2^-48, which only scales
 // the step and is absorbed by the next one); (sin, cos) follow E by rotation
 // through the step (Taylor to d^11 / d^12, truncation < 3e-18 for |d| <= 0.25)
-// (fewer terms when the wave's steps are below 2^-10 / 2^-22) when the whole
+// (fewer terms when the wave's steps are below 2^-9 / 2^-22) when the whole
 // wave's steps are small, else by direct evaluation.
 // The light-curve polynomial is written with explicit FMAs (the build uses
 // -ffp-contract=off so that the reference-order paths keep their rounding).
 // ------------------------------------------------------------------------
+#ifndef HB_RCP_REUSE
+#define HB_RCP_REUSE 0
+#endif
 constexpr double kRotMaxK = 0.25;
 __device__ __forceinline__ void rotate_back_wide(double d, double z, double& s, double& c) {
   // sin d = d (1 + z S(z)), cos d = 1 + z C(z), z = d^2
@@ -499,7 +502,7 @@ __device__ __forceinline__ void rotate_back_wide(double d, double z, double& s, 
   s = s2;
   c = c2;
 }
-// |d| <= 2^-10: Taylor to d^5 / d^4 (truncation < 2e-20)
+// |d| <= 2^-9: Taylor to d^5 / d^4 (truncation < 8e-20)
 __device__ __forceinline__ void rotate_back_mid(double d, double z, double& s, double& c) {
   const double sd = fma(d, z * fma(z, 1.0 / 120.0, -1.0 / 6.0), d);
   const double cd = fma(z, fma(z, 1.0 / 24.0, -0.5), 1.0);
@@ -553,6 +556,9 @@ __device__ __forceinline__ void hb_cadence_flux_k(const double (&t)[K], const Wa
     ok &= sincos_fast_ok(E[k]);
     sincos_fast(E[k], &s[k], &c[k]);
   }
+  double yk[K];           // last Newton step's 1/(1 - e cos E), refined once
+  bool converged = false;
+  (void)converged;
 #pragma unroll
   for (int it = 0; it < 5; ++it) {
     bool small = true, mid = true, tiny = true, conv = true;
@@ -562,12 +568,13 @@ __device__ __forceinline__ void hb_cadence_flux_k(const double (&t)[K], const Wa
       const double den = fma(-e, c[k], 1.0);
       double y = __builtin_amdgcn_rcp(den);
       y = fma(fma(-den, y, 1.0), y, y);
+      yk[k] = y;
       d[k] = ((E[k] - e * s[k]) - m[k]) * y;
       E[k] = E[k] - d[k];
       z[k] = d[k] * d[k];
       const double ad = fabs(d[k]);
       small &= ad <= kRotMaxK;
-      mid &= ad <= 0x1p-10;
+      mid &= ad <= 0x1p-9;
       tiny &= ad <= 0x1p-22;
       conv &= e * z[k] <= 0x1p-51 * den;
     }
@@ -588,14 +595,29 @@ __device__ __forceinline__ void hb_cadence_flux_k(const double (&t)[K], const Wa
         sincos_fast(E[k], &s[k], &c[k]);
       }
     }
-    if (__all(conv)) break;
+    if (__all(conv)) {
+      converged = true;
+      break;
+    }
   }
   bool need_ecl = false;
   double dd[K], zz[K];
 #pragma unroll
   for (int k = 0; k < K; ++k) {
     const double den = fma(-e, c[k], 1.0);
+#if HB_RCP_REUSE
+    // converged: E moved by < 2^-26 since yk was formed, so two refinements
+    // of yk give the reciprocal to working precision without a new v_rcp
+    double inv;
+    if (converged) {
+      inv = fma(fma(-den, yk[k], 1.0), yk[k], yk[k]);
+      inv = fma(fma(-den, inv, 1.0), inv, inv);
+    } else {
+      inv = fast_rcp(den);
+    }
+#else
     const double inv = fast_rcp(den);
+#endif
     const double cnu = (c[k] - e) * inv;
     const double snu = (w.sq1me2 * s[k]) * inv;
     const double cu = fma(w.cw, cnu, -w.sw * snu);

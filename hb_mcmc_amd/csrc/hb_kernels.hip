@@ -35,6 +35,9 @@ using namespace hbdev;
 #else
 #define HB_WPE_ATTR
 #endif
+#ifndef HB_PREP_ABL
+#define HB_PREP_ABL 0  // experiment builds only: 1 no Gaia flux, 2 no star_coef, 3 no radius law
+#endif
 #ifndef HB_ABLATE_MODEL
 #define HB_ABLATE_MODEL 0
 #endif
@@ -52,7 +55,10 @@ namespace hbk {
 // wave-uniform instead of divergent.  The stars swap their results through
 // LDS; parameters and records move through LDS so HBM accesses coalesce.
 // ---------------------------------------------------------------------------
-constexpr int kPrepWalkers = 64;
+#ifndef HB_PREP_W
+#define HB_PREP_W 64
+#endif
+constexpr int kPrepWalkers = HB_PREP_W;  // walkers per prep block (2 lanes each)
 constexpr int kWcDoubles = (int)(sizeof(WalkerConst) / sizeof(double));
 
 __global__ __launch_bounds__(2 * kPrepWalkers) void hb_prep_kernel(const double* __restrict__ params,
@@ -68,6 +74,13 @@ __global__ __launch_bounds__(2 * kPrepWalkers) void hb_prep_kernel(const double*
   const int nb = min(kPrepWalkers, nwalk - base);
   for (int i = tid; i < nb * kNpars; i += 2 * kPrepWalkers) sp[i] = params[(size_t)base * kNpars + i];
   __syncthreads();
+#if HB_PREP_ABL == 4  // experiment builds only: data movement, no math
+  {
+    double* dst = reinterpret_cast<double*>(out) + (size_t)base * kWcDoubles;
+    for (int i = tid; i < nb * kWcDoubles; i += 2 * kPrepWalkers) dst[i] = sp[i % (nb * kNpars)];
+    return;
+  }
+#endif
   const int j = tid & (kPrepWalkers - 1);
   const int star = tid / kPrepWalkers;  // wave-uniform
   const bool live = j < nb;
@@ -75,7 +88,11 @@ __global__ __launch_bounds__(2 * kPrepWalkers) void hb_prep_kernel(const double*
 
   // ---- this wave's star (calc_radii_and_Teffs + get_alpha_beam) ----
   const double m = exp10(p[star]);
+#if HB_PREP_ABL == 3
+  const double r = m + p[7 + star];
+#else
   const double r = exp10(logradius_of_mass(m) + p[7 + star] * radius_spread_of_mass(m));
+#endif
   const double lt = logteff_of_mass(m) + p[17 + star] * teff_spread();
   const double tk = exp10(lt);
   const double lum = sq(r) * sq(sq(tk));
@@ -94,7 +111,13 @@ __global__ __launch_bounds__(2 * kPrepWalkers) void hb_prep_kernel(const double*
   // the same sum in both waves: star-1 luminosity first
   const double lsum = star ? (lumo + lum) : (lum + lumo);
   const double nself = lum / lsum;
+#if HB_PREP_ABL == 2
+  StarCoef c;
+  c.kb = pd * m; c.am1 = mo * e; c.am2 = si * r; c.c21 = ro * ab; c.am3 = p[9 + 2 * star]; c.c22 = p[10 + 2 * star];
+  c.c4 = p[13 + star]; c.s1 = pd; c.s3 = m; c.kref = r;
+#else
   const StarCoef c = star_coef(pd, m, mo, e, si, r, ro, p[9 + 2 * star], p[10 + 2 * star], p[13 + star], ab);
+#endif
   // star 2 sees u + pi: odd harmonics flip sign
   const double sg = star ? -1.0 : 1.0;
   const double terms[12] = {nself * c.am1, nself * c.kb * sg, nself * c.kref, sg * nself * c.kref,
@@ -142,7 +165,11 @@ __global__ __launch_bounds__(2 * kPrepWalkers) void hb_prep_kernel(const double*
       gobs = td.gmag;
       gerr = td.gerr;
     }
+#if HB_PREP_ABL == 1
+    const double g = r1 + r2 + t1 + t2 + dist + p[19];
+#else
     const double g = ab_mag(band_flux(673.0, r1 * kRsun, r2 * kRsun, t1, t2, dist, p[19]));
+#endif
     gr = (g - gobs) / gerr;
     sincos(p[5], &sw_, &cw_);
   }
@@ -724,6 +751,9 @@ __device__ __forceinline__ double wave_select2(const uint64_t (&key)[VPT], uint3
   return dval(readlane_u64(mine, who));
 }
 
+#ifndef HB_PF
+#define HB_PF 0  // 1: request the chi^2 operands before the select (costs VGPR spills)
+#endif
 #ifndef HB_KEY_PERM
 #define HB_KEY_PERM 1
 #endif
@@ -787,6 +817,18 @@ __global__ __launch_bounds__(64) HB_WPE_ATTR void hb_eval_wave_kernel(
     const int i = key_index<VPT>(v, lane);
     key[v] = i < n ? dkey(vals[i]) : ~0ull;  // padding sorts last, never selected
   }
+  // chi^2 operands requested now so that their L2 latency overlaps the
+  // median select (VPT <= 16: 4*VPT more VGPRs while the keys are live)
+  constexpr int PF = (HB_PF && VPT <= 16) ? VPT : 1;
+  double fv[PF], iv[PF];
+  if (HB_PF && VPT <= 16 && mode == 0) {
+#pragma unroll
+    for (int v = 0; v < PF; ++v) {
+      const int i = min(key_index<VPT>(v, lane), (int)n - 1);
+      fv[v] = f[i];
+      iv[v] = isg[i];
+    }
+  }
   __syncthreads();  // the slab becomes the histogram
 #if HB_ABLATE_SELECT
   const double med = dval(kmn);
@@ -818,7 +860,7 @@ __global__ __launch_bounds__(64) HB_WPE_ATTR void hb_eval_wave_kernel(
     if (i < n) {
       double m = (dval(key[v]) - med) + 1.0;
       m = (blend + m * one_m_blend) * tune;
-      const double r = (m - f[i]) * isg[i];
+      const double r = (HB_PF && VPT <= 16) ? (m - fv[v < PF ? v : 0]) * iv[v < PF ? v : 0] : (m - f[i]) * isg[i];
       acc += r * r;
     }
   }
