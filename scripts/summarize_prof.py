@@ -34,5 +34,6 @@ if "FETCH_SIZE" in ev and "WRITE_SIZE" in ev:
     tj[f"N{ncad}_W{walkers}"] = {"hbm_bytes_per_launch": hbm, "source": f"profiles/{tag}_pmc_summary.json",
                                  "formula": "(2*FETCH_SIZE + WRITE_SIZE)*1024, separate --pmc passes"}
     json.dump(tj, open(tj_path, "w"), indent=1)
-json.dump(out, open(os.path.join(prof, f"{tag}_pmc_summary.json"), "w"), indent=1)
+if summary:
+    json.dump(out, open(os.path.join(prof, f"{tag}_pmc_summary.json"), "w"), indent=1)
 print(json.dumps(out, indent=1)[:3000])
