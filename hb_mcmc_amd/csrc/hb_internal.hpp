@@ -23,7 +23,8 @@ struct alignas(16) SelShared {
   int bin;
   uint32_t before;
   uint32_t cnt;
-  uint32_t pad[3];
+  uint32_t ncand;  // survivor counter of the register-key block select
+  uint32_t pad[2];
 };
 static_assert(sizeof(SelShared) % 16 == 0, "LDS carve must stay 16-B aligned");
 
@@ -32,6 +33,7 @@ struct EvalPlan {
   long kth = 0;        // 0-based rank of the subtracted "median"
   int nw = 1;          // waves per walker
   int vpt = 0;         // >0: one-wave path, cadences per lane (register keys)
+  int bvpt = 0;        // >0: NW-wave path with register keys, cadences per thread
   size_t slab_bytes = 0;  // template slab / histogram bytes (one-wave path)
   bool lds = true;     // template in LDS (else HBM scratch slab)
   size_t lds_bytes = 0;

@@ -651,26 +651,17 @@ __device__ __forceinline__ double wave_sum_dpp(double v) {
   return __longlong_as_double((long long)wave_reduce_u64((uint64_t)__double_as_longlong(v), OpAddF64()));
 }
 
-// One radix pass with 2^B bins over the keys that match `prefix` under
-// `mask`: histogram (LDS atomics), DPP scan of the per-lane bin sums, the
-// owning lane found by ballot, its bin/offset/count read back by v_readlane.
-template <int VPT, int B>
-__device__ __forceinline__ void select_pass(const uint64_t (&key)[VPT], uint32_t* hist, int lane, int& hi,
-                                            uint64_t& mask, uint64_t& prefix, uint32_t& kk, uint32_t& cnt) {
-  static_assert(B >= 8 && B <= 11, "4..32 bins per lane");
-  constexpr int PER = (1 << B) / 64;  // consecutive bins owned by a lane
-  constexpr int Q = PER / 4;          // uint4 per lane
-  const int width = hi + 1 < B ? hi + 1 : B;
-  const int shift = hi + 1 - width;
-  const uint32_t dm = (1u << width) - 1u;
-  uint4* h4 = reinterpret_cast<uint4*>(hist);
-#pragma unroll
-  for (int q = 0; q < Q; ++q) h4[lane * Q + q] = make_uint4(0u, 0u, 0u, 0u);
-  __syncthreads();
-#pragma unroll
-  for (int v = 0; v < VPT; ++v)
-    if ((key[v] & mask) == prefix) atomicAdd(&hist[(uint32_t)(key[v] >> shift) & dm], 1u);
-  __syncthreads();
+// Wave-level bin search over a 2^B-bin LDS histogram: the bin holding rank
+// kk, the count before it and its count (uniform across the wave).  Every
+// lane owns PER consecutive bins; DPP scan of the per-lane sums; the owning
+// lane found by ballot walks its bins (group of 4, then bin) and v_readlane
+// broadcasts the result.
+template <int B>
+__device__ __forceinline__ void wave_pick_bin(const uint32_t* hist, int lane, uint32_t kk, uint32_t& bin_out,
+                                              uint32_t& before_out, uint32_t& cnt_out) {
+  constexpr int PER = (1 << B) / 64;
+  constexpr int Q = PER / 4;
+  const uint4* h4 = reinterpret_cast<const uint4*>(hist);
   uint32_t h[PER];
 #pragma unroll
   for (int q = 0; q < Q; ++q) {
@@ -708,9 +699,33 @@ __device__ __forceinline__ void select_pass(const uint64_t (&key)[VPT], uint32_t
   if (kk >= before + c) { before += c; ++bin; c = c1;
     if (kk >= before + c) { before += c; ++bin; c = c2;
       if (kk >= before + c) { before += c; ++bin; c = c3; } } }
-  bin = (uint32_t)__builtin_amdgcn_readlane((int)bin, owner);
-  before = (uint32_t)__builtin_amdgcn_readlane((int)before, owner);
-  cnt = (uint32_t)__builtin_amdgcn_readlane((int)c, owner);
+  bin_out = (uint32_t)__builtin_amdgcn_readlane((int)bin, owner);
+  before_out = (uint32_t)__builtin_amdgcn_readlane((int)before, owner);
+  cnt_out = (uint32_t)__builtin_amdgcn_readlane((int)c, owner);
+}
+
+// One radix pass with 2^B bins over the keys that match `prefix` under
+// `mask`: histogram (LDS atomics), DPP scan of the per-lane bin sums, the
+// owning lane found by ballot, its bin/offset/count read back by v_readlane.
+template <int VPT, int B>
+__device__ __forceinline__ void select_pass(const uint64_t (&key)[VPT], uint32_t* hist, int lane, int& hi,
+                                            uint64_t& mask, uint64_t& prefix, uint32_t& kk, uint32_t& cnt) {
+  static_assert(B >= 8 && B <= 11, "4..32 bins per lane");
+  constexpr int PER = (1 << B) / 64;  // consecutive bins owned by a lane
+  constexpr int Q = PER / 4;          // uint4 per lane
+  const int width = hi + 1 < B ? hi + 1 : B;
+  const int shift = hi + 1 - width;
+  const uint32_t dm = (1u << width) - 1u;
+  uint4* h4 = reinterpret_cast<uint4*>(hist);
+#pragma unroll
+  for (int q = 0; q < Q; ++q) h4[lane * Q + q] = make_uint4(0u, 0u, 0u, 0u);
+  __syncthreads();
+#pragma unroll
+  for (int v = 0; v < VPT; ++v)
+    if ((key[v] & mask) == prefix) atomicAdd(&hist[(uint32_t)(key[v] >> shift) & dm], 1u);
+  __syncthreads();
+  uint32_t bin, before;
+  wave_pick_bin<B>(hist, lane, kk, bin, before, cnt);
   kk -= before;
   prefix |= (uint64_t)bin << shift;
   mask |= (uint64_t)dm << shift;
@@ -751,6 +766,12 @@ __device__ __forceinline__ double wave_select2(const uint64_t (&key)[VPT], uint3
   return dval(readlane_u64(mine, who));
 }
 
+#ifndef HB_RUN_AGG
+#define HB_RUN_AGG 1  // block select: one LDS atomic per run of equal bins in a row of 16 lanes
+#endif
+#ifndef HB_BLOCK_KEYS
+#define HB_BLOCK_KEYS 1  // 0: N > 2048 uses the LDS-walking block select (previous version)
+#endif
 #ifndef HB_PF
 #define HB_PF 0  // 1: request the chi^2 operands before the select (costs VGPR spills)
 #endif
@@ -870,6 +891,186 @@ __global__ __launch_bounds__(64) HB_WPE_ATTR void hb_eval_wave_kernel(
   const double chi2 = wave_sum_dpp(acc);
 #endif
   if (lane == 0) {
+    double c = chi2 + w.chi2_extra;
+    if (w.roche != 0.0) c = kBig;
+    logl[wv] = -c / 2.0;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// NW waves per walker with register keys (2048 < N <= 64*NW*VPT; config C3,
+// N = 20 000).  Like the one-wave kernel, the LDS slab holds the model values
+// only until every thread has its VPT order keys (cadence v*NT + tid: the
+// chi^2 operands stay coalesced); the slab then carries the histogram.  Each
+// radix pass is one LDS histogram of the block's survivors, scanned by wave 0
+// (wave_pick_bin: DPP scan + readlane) and broadcast through SelShared.  The
+// <= 64 survivors are appended (order free: equal keys are equal values) and
+// ranked by wave 0.  Min/max and chi^2 reduce per wave by DPP, across waves
+// through SelShared in wave order (deterministic).
+// ---------------------------------------------------------------------------
+template <int NW, int VPT, int B>
+__device__ __forceinline__ void block_select_pass(const uint64_t (&key)[VPT], uint32_t* hist, SelShared* sh,
+                                                  int tid, int& hi, uint64_t& mask, uint64_t& prefix,
+                                                  uint32_t& kk, uint32_t& cnt) {
+  constexpr int NT = 64 * NW, NB = 1 << B;
+  const int width = hi + 1 < B ? hi + 1 : B;
+  const int shift = hi + 1 - width;
+  const uint32_t dm = (1u << width) - 1u;
+  uint4* h4 = reinterpret_cast<uint4*>(hist);
+  for (int q = tid; q < NB / 4; q += NT) h4[q] = make_uint4(0u, 0u, 0u, 0u);
+  __syncthreads();
+#pragma unroll
+  for (int v = 0; v < VPT; ++v) {
+#if HB_RUN_AGG
+    // neighbouring cadences mostly share a bin: add each run of equal bins
+    // (within a row of 16 lanes: DPP row_shr:1 compares with lane-1) once,
+    // from its first lane, instead of up to 64 same-address LDS atomics
+    const bool m = (key[v] & mask) == prefix;
+    const uint32_t b = m ? ((uint32_t)(key[v] >> shift) & dm) : 0xffffffffu;
+    const uint32_t bp = (uint32_t)__builtin_amdgcn_update_dpp((int)0xfffffffeu, (int)b, 0x111, 0xf, 0xf, false);
+    const bool head = m && (b != bp);
+    const unsigned long long bound = __ballot(head || !m);  // lanes that start a run or hold no key
+    if (head) {
+      const int lane = tid & 63;
+      const unsigned long long after = lane < 63 ? (bound >> (lane + 1)) : 0ull;
+      const uint32_t len = after ? (uint32_t)__builtin_ctzll(after) + 1u : (uint32_t)(64 - lane);
+      atomicAdd(&hist[b], len);
+    }
+#else
+    if ((key[v] & mask) == prefix) atomicAdd(&hist[(uint32_t)(key[v] >> shift) & dm], 1u);
+#endif
+  }
+  __syncthreads();
+  if (tid < 64) {
+    uint32_t bin, before, c;
+    wave_pick_bin<B>(hist, tid, kk, bin, before, c);
+    if (tid == 0) {
+      sh->bin = (int)bin;
+      sh->before = before;
+      sh->cnt = c;
+      sh->ncand = 0u;
+    }
+  }
+  __syncthreads();
+  const uint32_t bin = (uint32_t)sh->bin;
+  kk -= sh->before;
+  cnt = sh->cnt;
+  prefix |= (uint64_t)bin << shift;
+  mask |= (uint64_t)dm << shift;
+  hi = shift - 1;
+}
+
+template <int NW, int VPT>
+__device__ double block_select2(const uint64_t (&key)[VPT], uint32_t kth, uint64_t kmin, uint64_t kmax,
+                                uint32_t* hist, uint64_t* cand, SelShared* sh) {
+  const int tid = threadIdx.x;
+  if (kmin == kmax) return dval(kmin);
+  int hi = 63 - __builtin_clzll(kmin ^ kmax);
+  uint64_t mask = (hi == 63) ? 0ull : ~((2ull << hi) - 1ull);
+  uint64_t prefix = kmin & mask;
+  uint32_t kk = kth, cnt = 0;
+  block_select_pass<NW, VPT, kSelBits>(key, hist, sh, tid, hi, mask, prefix, kk, cnt);
+  while (cnt > (uint32_t)kCandMax && hi >= 0)
+    block_select_pass<NW, VPT, kSelBits2>(key, hist, sh, tid, hi, mask, prefix, kk, cnt);
+  if (hi < 0) return dval(prefix);
+#pragma unroll
+  for (int v = 0; v < VPT; ++v)
+    if ((key[v] & mask) == prefix) cand[atomicAdd(&sh->ncand, 1u)] = key[v];
+  __syncthreads();
+  if (tid < 64) {
+    const uint64_t mine = (uint32_t)tid < cnt ? cand[tid] : ~0ull;
+    uint32_t r = 0;
+    for (uint32_t j = 0; j < cnt; ++j) {
+      const uint64_t o = cand[j];
+      r += (o < mine) | ((o == mine) & (j < (uint32_t)tid));
+    }
+    const unsigned long long hit = __ballot((uint32_t)tid < cnt && r == kk);
+    const int who = __builtin_amdgcn_readfirstlane(__ffsll((long long)hit) - 1);
+    const uint64_t ans = readlane_u64(mine, who);
+    if (tid == 0) sh->ans = ans;
+  }
+  __syncthreads();
+  return dval(sh->ans);
+}
+
+template <int NW, int VPT>
+__global__ __launch_bounds__(64 * NW) HB_WPE_ATTR void hb_eval_block_kernel(
+    const double* __restrict__ t, const double* __restrict__ f, const double* __restrict__ isg, long n,
+    long kth, const WalkerConst* __restrict__ wcs, double* __restrict__ logl, double* __restrict__ tmpl_out,
+    int mode) {
+  constexpr int NT = 64 * NW;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  SelShared* sh = reinterpret_cast<SelShared*>(smem);
+  double* vals = reinterpret_cast<double*>(smem + sizeof(SelShared));
+  uint32_t* hist = reinterpret_cast<uint32_t*>(vals);
+  uint64_t* cand = reinterpret_cast<uint64_t*>(smem + sizeof(SelShared) + (4u << kSelBits));
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int wv = blockIdx.x;
+  const WalkerConst& w = wcs[wv];
+  if (mode == 0 && w.roche != 0.0) {  // likelihood3.c:866-869, see hb_eval_kernel
+    if (tid == 0) logl[wv] = -kBig / 2.0;
+    return;
+  }
+  const int nn = (int)n;
+  uint64_t kmn, kmx;
+  model_pass<NT>(t, nn, w, vals, tid, kmn, kmx);
+  kmn = wave_reduce_u64(kmn, OpMinU64());
+  kmx = wave_reduce_u64(kmx, OpMaxU64());
+  if (lane == 0) {
+    sh->red_min[wave] = kmn;
+    sh->red_max[wave] = kmx;
+  }
+  __syncthreads();
+  kmn = sh->red_min[0];
+  kmx = sh->red_max[0];
+#pragma unroll
+  for (int k = 1; k < NW; ++k) {
+    kmn = sh->red_min[k] < kmn ? sh->red_min[k] : kmn;
+    kmx = sh->red_max[k] > kmx ? sh->red_max[k] : kmx;
+  }
+  uint64_t key[VPT];
+#pragma unroll
+  for (int v = 0; v < VPT; ++v) {
+    const int i = v * NT + tid;
+    key[v] = i < nn ? dkey(vals[i]) : ~0ull;  // padding sorts last, never selected
+  }
+  __syncthreads();  // the slab becomes the histogram
+#if HB_ABLATE_SELECT
+  const double med = dval(kmn);
+#else
+  const double med = block_select2<NW, VPT>(key, (uint32_t)kth, kmn, kmx, hist, cand, sh);
+#endif
+  const double blend = w.blend, one_m_blend = 1.0 - w.blend, tune = w.tune;
+  if (mode == 1) {
+    double* o = tmpl_out + (size_t)wv * (size_t)n;
+#pragma unroll
+    for (int v = 0; v < VPT; ++v) {
+      const int i = v * NT + tid;
+      if (i < nn) {
+        const double m = (dval(key[v]) - med) + 1.0;
+        o[i] = (blend + m * one_m_blend) * tune;
+      }
+    }
+    return;
+  }
+  double acc = 0.0;
+#pragma unroll
+  for (int v = 0; v < VPT; ++v) {
+    const int i = v * NT + tid;
+    if (i < nn) {
+      double m = (dval(key[v]) - med) + 1.0;
+      m = (blend + m * one_m_blend) * tune;
+      const double r = (m - f[i]) * isg[i];
+      acc += r * r;
+    }
+  }
+  acc = wave_sum_dpp(acc);
+  if (lane == 0) sh->red_sum[wave] = acc;
+  __syncthreads();
+  if (tid == 0) {
+    double chi2 = sh->red_sum[0];
+#pragma unroll
+    for (int k = 1; k < NW; ++k) chi2 += sh->red_sum[k];
     double c = chi2 + w.chi2_extra;
     if (w.roche != 0.0) c = kBig;
     logl[wv] = -c / 2.0;
@@ -1005,6 +1206,23 @@ hipError_t launch_prep(const double* d_params, int nwalk, const MagArgs& ma, Wal
   return hipGetLastError();
 }
 
+template <int NW, int VPT>
+static hipError_t launch_block_t(const EvalPlan& pl, const double* t, const double* f, const double* sg,
+                                 const WalkerConst* wc, int nwalk, double* logl, double* tmpl, int mode,
+                                 hipStream_t s) {
+  auto kern = hb_eval_block_kernel<NW, VPT>;
+  static bool attr_set = false;  // per instantiation; benign race (idempotent)
+  if (!attr_set && pl.lds_bytes > 65536) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)pl.lds_bytes);
+    if (e != hipSuccess) return e;
+    attr_set = true;
+  }
+  hipLaunchKernelGGL(kern, dim3(nwalk), dim3(64 * NW), pl.lds_bytes, s, t, f, sg, pl.n, pl.kth, wc, logl, tmpl,
+                     mode);
+  return hipGetLastError();
+}
+
 template <int NW, bool LDS>
 static hipError_t launch_eval_t(const EvalPlan& pl, const double* t, const double* f, const double* sg,
                                 const WalkerConst* wc, int nwalk, double* logl, double* tmpl,
@@ -1069,6 +1287,15 @@ hipError_t launch_eval(const EvalPlan& pl, const double* t, const double* f, con
     case 16: return launch_wave_t<16>(pl, t, f, sg, wc, nwalk, logl, tmpl, mode, s);
     case 32: return launch_wave_t<32>(pl, t, f, sg, wc, nwalk, logl, tmpl, mode, s);
     default: return hipErrorInvalidValue;
+  }
+  if (pl.bvpt > 0) {
+#define HB_BCASE(NWV, V)                                                                    \
+  if (pl.nw == NWV && pl.bvpt == V) return launch_block_t<NWV, V>(pl, t, f, sg, wc, nwalk, logl, tmpl, mode, s);
+    HB_BCASE(4, 8) HB_BCASE(4, 16) HB_BCASE(4, 24) HB_BCASE(4, 32)
+    HB_BCASE(8, 8) HB_BCASE(8, 16) HB_BCASE(8, 24) HB_BCASE(8, 32)
+    HB_BCASE(16, 8) HB_BCASE(16, 16) HB_BCASE(16, 24) HB_BCASE(16, 32)
+#undef HB_BCASE
+    return hipErrorInvalidValue;
   }
 #define HB_CASE(NWV)                                                                              \
   case NWV:                                                                                       \
@@ -1147,7 +1374,13 @@ EvalPlan make_plan(long n) {
     const size_t blocks_per_cu = lds_cap / need;  // LDS-limited residency
     int nw = 1;
     while (nw < 16 && (size_t)nw * blocks_per_cu < 16) nw <<= 1;
+    if (nw < 4) nw = 4;
     pl.nw = nw;
+#if HB_BLOCK_KEYS
+    const long per = (n + 64L * nw - 1) / (64L * nw);  // cadences per thread
+    if (per <= 32 && need >= sizeof(SelShared) + (4u << kSelBits) + 8 * kCandMax)
+      pl.bvpt = per <= 8 ? 8 : per <= 16 ? 16 : per <= 24 ? 24 : 32;
+#endif
   } else {
     pl.lds = false;
     pl.lds_bytes = sizeof(SelShared);

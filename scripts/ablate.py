@@ -8,7 +8,7 @@ res = {os.path.basename(l): [] for l in libs}
 for rnd in range(3):
     for l in libs:
         env = dict(os.environ, HBMI_LIB=l)
-        r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "100", "--warmup", "10",
+        r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", os.environ.get("ABLATE_STEPS", "100"), "--warmup", "10",
                             "--no-cpu-baseline"] + extra, env=env, capture_output=True, text=True, timeout=300)
         if r.returncode != 0:
             print(l, "FAILED", r.stderr[-300:]); continue
