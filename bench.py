@@ -314,8 +314,9 @@ def main():
             except Exception:
                 traffic = None
         flops_conv = 600.0 * n  # SURVEY.md 8(d) counting convention
-        # the eval plan (hb_kernels.hip make_plan): one wave per walker up to 2048 cadences
-        kernel_name = "hb_eval_wave_kernel" if L.waves_per_walker == 1 else "hb_eval_kernel"
+        # the eval plan (hb_kernels.hip make_plan): one wave per walker up to 2048 cadences,
+        # NW waves with register keys above
+        kernel_name = L.eval_kernel
         line = {
             "metric": METRIC,
             "value": value,
@@ -329,7 +330,8 @@ def main():
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (SURVEY.md 8(d): truth = test_likelihoods.c:33-36, t_i = 2P i/N, sigma 1e-3)",
-            "config": {"workload": f"C2: synthetic {n}-cadence HB light curve, {w} walkers per GPU",
+            "config": {"workload": f"{'C3' if n > 2048 else 'C2'}: synthetic {n}-cadence HB light curve, "
+                                   f"{w} walkers per GPU",
                        "ncad": n, "walkers_per_gpu": w, "global_walkers": world * w,
                        "parallelism": f"walker-sharded x{world}, logL all-gather over RCCL" if world > 1
                        else "single GPU",

@@ -271,6 +271,10 @@ extern "C" void hb_destroy(hb_ctx* c) {
 extern "C" long hb_ctx_ncad(const hb_ctx* c) { return c ? c->plan.n : -1; }
 extern "C" int hb_ctx_waves_per_walker(const hb_ctx* c) { return c ? c->plan.nw : -1; }
 extern "C" int hb_ctx_template_in_lds(const hb_ctx* c) { return c ? (c->plan.lds ? 1 : 0) : -1; }
+extern "C" int hb_ctx_eval_kind(const hb_ctx* c) {
+  if (!c) return -1;
+  return c->plan.vpt > 0 ? 0 : c->plan.bvpt > 0 ? 1 : 2;
+}
 
 static int run_batch(hb_ctx* c, const double* d_params, int w, double* d_logl, double* d_tmpl,
                      hipStream_t s) {

@@ -76,6 +76,12 @@ class HBLikelihood:
     def template_in_lds(self) -> bool:
         return bool(self.lib.hb_ctx_template_in_lds(self._h))
 
+    @property
+    def eval_kernel(self) -> str:
+        """Name of the eval kernel this light curve's plan launches."""
+        kind = self.lib.hb_ctx_eval_kind(self._h)
+        return ("hb_eval_wave_kernel", "hb_eval_block_kernel", "hb_eval_kernel")[kind]
+
     def reserve(self, max_walkers: int):
         _lib.check(self.lib.hb_reserve(self._h, int(max_walkers)), "hb_reserve")
 

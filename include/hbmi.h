@@ -155,6 +155,10 @@ int hb_light_curve_batch(hb_ctx *ctx, const double *params, int W, double *out, 
  * whether the template lives in LDS (1) or in an HBM scratch slab (0). */
 int hb_ctx_waves_per_walker(const hb_ctx *ctx);
 int hb_ctx_template_in_lds(const hb_ctx *ctx);
+/* Eval kernel the context launches: 0 hb_eval_wave_kernel (N <= 2048, one wave
+ * per walker), 1 hb_eval_block_kernel (register keys, N <= 32 x 64 x waves),
+ * 2 hb_eval_kernel (LDS-walking select; template in LDS or an HBM slab). */
+int hb_ctx_eval_kind(const hb_ctx *ctx);
 
 /* Last error message of the calling thread ("" if none). */
 const char *hb_last_error(void);

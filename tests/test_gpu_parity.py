@@ -156,6 +156,7 @@ def test_n20000_lds_tiled_path(hbmi):
     g = golden("lc_synth20000.npz")
     with HBLikelihood(g["t"], g["f"], g["s"], g["mag"], g["magerr"]) as L:
         assert L.waves_per_walker == 16 and L.template_in_lds
+        assert L.eval_kernel == "hb_eval_block_kernel"
         ll = L.loglike(g["params"])
         tm = L.light_curve(g["params"])
     close_logl(ll, g["logl"])
@@ -163,6 +164,25 @@ def test_n20000_lds_tiled_path(hbmi):
     assert (np.abs(tm[:, :16] - g["thead"]) <= tol).all()
     assert (np.abs(tm[:, -16:] - g["ttail"]) <= tol).all()
     assert (np.abs(tm.sum(1) - g["tsum"]) <= 20000 * tol[:, 0]).all()
+
+
+@pytest.mark.parametrize("n", [2049, 4001, 6001, 8192, 12000])
+def test_block_kernel_sizes(hbmi, oracle, n):
+    """Register-key block kernel across its (waves, keys-per-thread) classes,
+    odd and even N (median rank likelihood3.c:97-101), templates and logL."""
+    from hb_mcmc_amd import synth
+    from hb_mcmc_amd.likelihood import HBLikelihood
+
+    t, f, s = synth.dataset(n, oracle.light_curve)
+    P = synth.walkers(8, seed=n)
+    with HBLikelihood(t, f, s) as L:
+        assert L.eval_kernel == "hb_eval_block_kernel"
+        ll = L.loglike(P)
+        tm = L.light_curve(P)
+    close_logl(ll, oracle.loglike_batch(t, f, s, P, synth.MAG_DEFAULT, synth.MAGERR_DEFAULT, 8))
+    ref = oracle.light_curve_batch(t, P, 8)
+    tol = lc_tol(P[:, 3])[:, None]
+    assert (np.abs(tm - ref) <= tol).all()
 
 
 def test_real_1861_cadences(hbmi):
