@@ -152,6 +152,7 @@ struct hb_ctx {
   double* d_t = nullptr;
   double* d_f = nullptr;
   double* d_s = nullptr;          // 1 / max(sigma, 1e-5)
+  double2* d_ph = nullptr;        // shared-period phase table, written by every prep launch
   // per-walker workspace
   int cap = 0;
   WalkerConst* d_wc = nullptr;
@@ -241,7 +242,7 @@ extern "C" hb_ctx* hb_create(const double* t, const double* f, const double* sig
   }
   const size_t bytes = sizeof(double) * (size_t)n;
   if (hipMalloc(&c->d_t, bytes) != hipSuccess || hipMalloc(&c->d_f, bytes) != hipSuccess ||
-      hipMalloc(&c->d_s, bytes) != hipSuccess) {
+      hipMalloc(&c->d_s, bytes) != hipSuccess || hipMalloc(&c->d_ph, 2 * bytes) != hipSuccess) {
     set_err_msg("hb_create: hipMalloc failed");
     hb_destroy(c.release());
     return nullptr;
@@ -265,6 +266,7 @@ extern "C" void hb_destroy(hb_ctx* c) {
   if (c->d_t) (void)hipFree(c->d_t);
   if (c->d_f) (void)hipFree(c->d_f);
   if (c->d_s) (void)hipFree(c->d_s);
+  if (c->d_ph) (void)hipFree(c->d_ph);
   delete c;
 }
 
@@ -287,8 +289,9 @@ static int run_batch(hb_ctx* c, const double* d_params, int w, double* d_logl, d
     int rc = hb_reserve(c, w);
     if (rc) return rc;
   }
-  HB_TRY(hbk::launch_prep(d_params, w, c->mags, c->d_wc, s), "hb_prep_kernel");
-  HB_TRY(hbk::launch_eval(c->plan, c->d_t, c->d_f, c->d_s, c->d_wc, w, d_logl, d_tmpl, c->d_scratch,
+  HB_TRY(hbk::launch_prep(d_params, w, c->mags, c->d_wc, s, nullptr, nullptr, c->d_t, c->plan.n, c->d_ph),
+         "hb_prep_kernel");
+  HB_TRY(hbk::launch_eval(c->plan, c->d_t, c->d_ph, c->d_f, c->d_s, c->d_wc, w, d_logl, d_tmpl, c->d_scratch,
                           d_tmpl ? 1 : 0, s),
          "hb_eval_kernel");
   return 0;
@@ -302,7 +305,9 @@ extern "C" int hb_prepare_dev(hb_ctx* c, const double* d_params, int w, void* st
     int rc = hb_reserve(c, w);
     if (rc) return rc;
   }
-  HB_TRY(hbk::launch_prep(d_params, w, c->mags, c->d_wc, (hipStream_t)stream), "hb_prep_kernel");
+  HB_TRY(hbk::launch_prep(d_params, w, c->mags, c->d_wc, (hipStream_t)stream, nullptr, nullptr, c->d_t, c->plan.n,
+                          c->d_ph),
+         "hb_prep_kernel");
   return 0;
 }
 
@@ -312,7 +317,7 @@ extern "C" int hb_evaluate_dev(hb_ctx* c, int w, double* d_out, int mode, void* 
   if (w > c->cap) return set_err_msg("hb_evaluate_dev: W exceeds the prepared workspace");
   if (mode != 0 && mode != 1) return set_err_msg("hb_evaluate_dev: mode must be 0 or 1");
   HB_TRY(hipSetDevice(c->device), "hipSetDevice");
-  HB_TRY(hbk::launch_eval(c->plan, c->d_t, c->d_f, c->d_s, c->d_wc, w, mode == 0 ? d_out : nullptr,
+  HB_TRY(hbk::launch_eval(c->plan, c->d_t, c->d_ph, c->d_f, c->d_s, c->d_wc, w, mode == 0 ? d_out : nullptr,
                           mode == 1 ? d_out : nullptr, c->d_scratch, mode, (hipStream_t)stream),
          "hb_eval_kernel");
   return 0;
@@ -357,6 +362,8 @@ struct hb_catalog {
   double* d_t = nullptr;
   double* d_f = nullptr;
   double* d_s = nullptr;         // 1 / max(sigma, 1e-5)
+  double2* d_ph = nullptr;       // per-target phase tables (concatenated like d_t)
+  int* d_w0 = nullptr;           // first walker of each target in the current layout, -1 if none
   hbk::TargetDesc* d_tab = nullptr;
   // walker layout cache (walkers per target as last seen)
   std::vector<int> layout;
@@ -375,7 +382,8 @@ struct hb_catalog {
 extern "C" void hb_catalog_destroy(hb_catalog* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
-  for (void* p : {(void*)c->d_t, (void*)c->d_f, (void*)c->d_s, (void*)c->d_tab, (void*)c->d_wt, (void*)c->d_list,
+  for (void* p : {(void*)c->d_t, (void*)c->d_f, (void*)c->d_s, (void*)c->d_ph, (void*)c->d_w0, (void*)c->d_tab,
+                  (void*)c->d_wt, (void*)c->d_list,
                   (void*)c->d_wc, (void*)c->d_params, (void*)c->d_out})
     if (p) (void)hipFree(p);
   delete c;
@@ -433,7 +441,8 @@ extern "C" hb_catalog* hb_catalog_create(int ntargets, const double* const* t, c
   if (hipSetDevice(device) != hipSuccess) { set_err_msg("hb_catalog_create: hipSetDevice failed"); return nullptr; }
   const size_t b = sizeof(double) * (size_t)total;
   if (hipMalloc(&c->d_t, b) != hipSuccess || hipMalloc(&c->d_f, b) != hipSuccess ||
-      hipMalloc(&c->d_s, b) != hipSuccess ||
+      hipMalloc(&c->d_s, b) != hipSuccess || hipMalloc(&c->d_ph, 2 * b) != hipSuccess ||
+      hipMalloc(&c->d_w0, sizeof(int) * ntargets) != hipSuccess ||
       hipMalloc(&c->d_tab, sizeof(hbk::TargetDesc) * ntargets) != hipSuccess) {
     set_err_msg("hb_catalog_create: hipMalloc failed");
     return nullptr;
@@ -461,11 +470,13 @@ static int catalog_layout(hb_catalog* c, const int* walkers, hipStream_t s) {
     total += walkers[k];
   }
   if (total > (1 << 30)) return set_err_msg("hb_catalog: too many walkers");
-  std::vector<int> wt((size_t)total), list;
+  std::vector<int> wt((size_t)total), list, w0(c->ntargets);
   list.reserve((size_t)total);
   long w = 0;
-  for (int k = 0; k < c->ntargets; ++k)
+  for (int k = 0; k < c->ntargets; ++k) {
+    w0[k] = walkers[k] > 0 ? (int)w : -1;
     for (int i = 0; i < walkers[k]; ++i) wt[(size_t)w++] = k;
+  }
   for (int cl = 0; cl < 6; ++cl) {
     c->class_off[cl] = (int)list.size();
     long nmax = 0;
@@ -496,6 +507,8 @@ static int catalog_layout(hb_catalog* c, const int* walkers, hipStream_t s) {
     c->cap = (int)total;
   }
   if (total > 0) {
+    HB_TRY(hipMemcpyAsync(c->d_w0, w0.data(), sizeof(int) * (size_t)c->ntargets, hipMemcpyHostToDevice, s),
+           "upload first walkers");
     HB_TRY(hipMemcpyAsync(c->d_wt, wt.data(), sizeof(int) * (size_t)total, hipMemcpyHostToDevice, s), "upload map");
     HB_TRY(hipMemcpyAsync(c->d_list, list.data(), sizeof(int) * (size_t)total, hipMemcpyHostToDevice, s),
            "upload lists");
@@ -509,10 +522,12 @@ static int catalog_layout(hb_catalog* c, const int* walkers, hipStream_t s) {
 static int catalog_run(hb_catalog* c, const double* d_params, double* d_logl, hipStream_t s) {
   if (c->total == 0) return 0;
   MagArgs unused{};
-  HB_TRY(hbk::launch_prep(d_params, c->total, unused, c->d_wc, s, c->d_tab, c->d_wt), "prep launch");
+  HB_TRY(hbk::launch_prep(d_params, c->total, unused, c->d_wc, s, c->d_tab, c->d_wt, c->d_t, 0, c->d_ph, c->d_w0,
+                          c->ntargets),
+         "prep launch");
   for (int cl = 0; cl < 6; ++cl) {
     const int cnt = c->class_off[cl + 1] - c->class_off[cl];
-    HB_TRY(hbk::launch_eval_multi(1 << cl, c->class_slab[cl], c->d_t, c->d_f, c->d_s, c->d_tab, c->d_wt,
+    HB_TRY(hbk::launch_eval_multi(1 << cl, c->class_slab[cl], c->d_t, c->d_ph, c->d_f, c->d_s, c->d_tab, c->d_wt,
                                   c->d_list + c->class_off[cl], cnt, c->d_wc, d_logl, s),
            "eval launch");
   }

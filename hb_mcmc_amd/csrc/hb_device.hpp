@@ -38,7 +38,7 @@ constexpr double kDay = 86400.0;
 constexpr double kBig = 1.e15;
 constexpr int kNpars = 21;
 
-// Per-walker record.  40 doubles = 320 B; read by the cadence kernel with
+// Per-walker record.  44 doubles = 352 B; read by the cadence kernel with
 // wave-uniform (scalar) loads.
 struct alignas(16) WalkerConst {
   // orbit (traj, likelihood3.c:125-185)
@@ -69,9 +69,16 @@ struct alignas(16) WalkerConst {
   double roche;                  // 1.0 if RocheOverflow(), else 0.0
   double mA, mB;                 // mean anomaly M = fma(t, DAY, mB) * mA (hot loop)
   double rsum;                   // Rbig + Rsml
-  double pad[3];
+  // shared-period phase table (hb_prep_kernel): when this walker's period is
+  // the batch's table period (tab = 1), sin/cos of the mean anomaly come from
+  // the per-cadence table (sin, cos)(t DAY 2pi/P) rotated by psi = T0 2pi/P,
+  // and those of the Kepler start E0 = M +- 0.85 e by a rotation through del
+  double cpsi, spsi;             // cos/sin psi
+  double cdel, sdel;             // cos/sin del, del = 0.85 e
+  double tab;                    // 1.0: use the table, 0.0: direct sincos
+  double pad[2];
 };
-static_assert(sizeof(WalkerConst) == 40 * 8, "WalkerConst layout");
+static_assert(sizeof(WalkerConst) == 44 * 8, "WalkerConst layout");
 
 // ------------------------------------------------------------------------
 // small helpers
@@ -361,7 +368,12 @@ __device__ inline void hb_prepare_walker(const double* __restrict__ p, const dou
   w.mA = kTwoPi / w.Pc;
   w.mB = -w.T0c;
   w.rsum = w.rbig + w.rsml;
-  for (int k = 0; k < 3; ++k) w.pad[k] = 0.0;
+  w.cpsi = 1.0;
+  w.spsi = 0.0;
+  w.cdel = 1.0;
+  w.sdel = 0.0;
+  w.tab = 0.0;  // the scalar drop-in paths evaluate sin/cos directly
+  for (int k = 0; k < 2; ++k) w.pad[k] = 0.0;
 }
 
 // ------------------------------------------------------------------------
@@ -521,12 +533,12 @@ __device__ __forceinline__ void rotate_back_tiny(double d, double z, double& s, 
 }
 
 template <int K>
-__device__ __forceinline__ void hb_cadence_flux_k(const double (&t)[K], const WalkerConst& w,
-                                                  double (&v)[K], bool& bad) {
+__device__ __forceinline__ void hb_cadence_flux_k(const double (&t)[K], const double2 (&ph)[K], bool tab,
+                                                  const WalkerConst& w, double (&v)[K], bool& bad) {
   const double e = w.e;
   const double aR2 = w.aR * w.aR, rsum2 = w.rsum * w.rsum;
   double m[K], E[K], s[K], c[K];
-  bool ok = true, exact = false;
+  bool ok = true, exact = false, plus[K];
 #pragma unroll
   for (int k = 0; k < K; ++k) {
     const double x = fma(t[k], kDay, w.mB) * w.mA;
@@ -539,8 +551,18 @@ __device__ __forceinline__ void hb_cadence_flux_k(const double (&t)[K], const Wa
     exact |= !inside;
     m[k] = r;
     // sign(sin m) * 0.85 e for m in (-2pi, 2pi) \ {0} (sign_sin_reduced)
-    const bool plus = (fabs(r) <= kPi) != (r < 0.0);
-    E[k] = r + (plus ? w.e085 : -w.e085);
+    plus[k] = (fabs(r) <= kPi) != (r < 0.0);
+    E[k] = r + (plus[k] ? w.e085 : -w.e085);
+  }
+  if (tab) {  // walker-uniform: E0 = M + sg del by rotations of the table entry
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const double sx = fma(ph[k].x, w.cpsi, -(ph[k].y * w.spsi));  // sin(phi - psi)
+      const double cx = fma(ph[k].y, w.cpsi, ph[k].x * w.spsi);     // cos(phi - psi)
+      const double sd = plus[k] ? w.sdel : -w.sdel;
+      s[k] = fma(sx, w.cdel, cx * sd);
+      c[k] = fma(cx, w.cdel, -(sx * sd));
+    }
   }
   if (__any(exact)) {  // rare: x near a multiple of 2pi, or r == 0
 #pragma unroll
@@ -550,11 +572,14 @@ __device__ __forceinline__ void hb_cadence_flux_k(const double (&t)[K], const Wa
       const double sg = sign_sin_reduced(m[k]);
       E[k] = (sg == 0.0) ? m[k] : m[k] + w.e085 * sg;
     }
+    tab = false;  // recompute (s, c) directly below
   }
+  if (!tab) {
 #pragma unroll
-  for (int k = 0; k < K; ++k) {
-    ok &= sincos_fast_ok(E[k]);
-    sincos_fast(E[k], &s[k], &c[k]);
+    for (int k = 0; k < K; ++k) {
+      ok &= sincos_fast_ok(E[k]);
+      sincos_fast(E[k], &s[k], &c[k]);
+    }
   }
   double yk[K];           // last Newton step's 1/(1 - e cos E), refined once
   bool converged = false;

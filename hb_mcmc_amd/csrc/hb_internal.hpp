@@ -76,16 +76,23 @@ enum ProbeOp {
 EvalPlan make_plan(long n);
 // forces the load of hb_kernels.hip's code object on the current device
 hipError_t preload_code_object();
+// ph (optional): the shared-period phase table of the batch, (sin, cos)(t_i
+// DAY 2pi/P) for P = the period of the light curve's first walker (walker 0,
+// or catalog target k's w0[k]), written here and read by the eval launch;
+// walkers with another period get tab = 0
 hipError_t launch_prep(const double* d_params, int nwalk, const MagArgs& ma, hbdev::WalkerConst* d_wc,
-                       hipStream_t s, const TargetDesc* tab = nullptr, const int* wt = nullptr);
+                       hipStream_t s, const TargetDesc* tab = nullptr, const int* wt = nullptr,
+                       const double* t = nullptr, long n = 0, double2* ph = nullptr, const int* w0 = nullptr,
+                       int ntargets = 0);
 // catalog mode: walkers list[0..count) of one size class (cadences per lane
 // vpt), each reading its target's slice through tab[wt[walker]]
-hipError_t launch_eval_multi(int vpt, size_t slab_bytes, const double* t, const double* f, const double* sg,
+hipError_t launch_eval_multi(int vpt, size_t slab_bytes, const double* t, const double2* ph, const double* f,
+                             const double* sg,
                              const TargetDesc* tab, const int* wt, const int* list, int count,
                              const hbdev::WalkerConst* wc, double* logl, hipStream_t s);
 int wave_vpt_for(long n);  // cadences per lane of the one-wave path, 0 if n > 2048
 size_t wave_slab_bytes(long n);
-hipError_t launch_eval(const EvalPlan& pl, const double* t, const double* f, const double* sg,
+hipError_t launch_eval(const EvalPlan& pl, const double* t, const double2* ph, const double* f, const double* sg,
                        const hbdev::WalkerConst* wc, int nwalk, double* logl, double* tmpl,
                        double* scratch, int mode, hipStream_t s);
 hipError_t launch_traj(const double* d_times, int nt, const TrajArgs& ta, double* d, double* z1,

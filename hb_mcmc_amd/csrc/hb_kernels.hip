@@ -65,7 +65,10 @@ __global__ __launch_bounds__(2 * kPrepWalkers) void hb_prep_kernel(const double*
                                                                     int nwalk, MagArgs ma,
                                                                     WalkerConst* __restrict__ out,
                                                                     const TargetDesc* __restrict__ tab,
-                                                                    const int* __restrict__ wt) {
+                                                                    const int* __restrict__ wt,
+                                                                    const double* __restrict__ tcad, int ncad,
+                                                                    double2* __restrict__ ph,
+                                                                    const int* __restrict__ w0, int ntargets) {
   __shared__ double sp[kPrepWalkers * kNpars];
   __shared__ double so[kPrepWalkers * kWcDoubles];
   __shared__ double xs[2][16][kPrepWalkers];  // per-star results for the partner: [star][item][walker]
@@ -73,6 +76,31 @@ __global__ __launch_bounds__(2 * kPrepWalkers) void hb_prep_kernel(const double*
   const int base = blockIdx.x * kPrepWalkers;
   const int nb = min(kPrepWalkers, nwalk - base);
   for (int i = tid; i < nb * kNpars; i += 2 * kPrepWalkers) sp[i] = params[(size_t)base * kNpars + i];
+  // Shared-period phase table (WalkerConst::tab): per light curve, for the
+  // period of its first walker in this batch, ph[i] = (sin, cos)(t_i DAY 2pi/Pc0).
+  // Single context: walker 0, cadences [0, ncad).  Catalog: target k's first
+  // walker w0[k] (-1: no walkers), its slice of the concatenated arrays.
+  if (ph) {
+    if (tab == nullptr) {
+      const double mA0 = kTwoPi / (exp10(params[2]) * kDay);
+      for (int i = blockIdx.x * blockDim.x + tid; i < ncad; i += gridDim.x * blockDim.x) {
+        double sv, cv;
+        sincos((tcad[i] * kDay) * mA0, &sv, &cv);
+        ph[i] = make_double2(sv, cv);
+      }
+    } else {
+      for (int k = blockIdx.x; k < ntargets; k += gridDim.x) {
+        if (w0[k] < 0) continue;
+        const double mA0 = kTwoPi / (exp10(params[(size_t)w0[k] * kNpars + 2]) * kDay);
+        const long off = tab[k].off;
+        for (int i = tid; i < (int)tab[k].n; i += blockDim.x) {
+          double sv, cv;
+          sincos((tcad[off + i] * kDay) * mA0, &sv, &cv);
+          ph[off + i] = make_double2(sv, cv);
+        }
+      }
+    }
+  }
   __syncthreads();
 #if HB_PREP_ABL == 4  // experiment builds only: data movement, no math
   {
@@ -154,7 +182,19 @@ __global__ __launch_bounds__(2 * kPrepWalkers) void hb_prep_kernel(const double*
       const double f1 = (r1 * kRsun) / peri;
       const double f2 = (r2 * kRsun) / peri;
       wc->roche = ((lobe_fraction(q12) < f1) || (lobe_fraction(1.0 / q12) < f2)) ? 1.0 : 0.0;
-      wc->pad[0] = wc->pad[1] = wc->pad[2] = 0.0;
+      // phase-table rotations (WalkerConst::tab); same Pc and mA as wave 0's orbit fields
+      double Pc0 = 0.0;
+      if (ph) Pc0 = exp10(params[(tab ? (size_t)w0[wt[base + j]] * kNpars : 0) + 2]) * kDay;
+      const bool use_tab = (ph != nullptr) && (Pc == Pc0);
+      wc->tab = use_tab ? 1.0 : 0.0;
+      double sv = 0.0, cv = 1.0;
+      if (use_tab) sincos((p[6] * kDay) * (kTwoPi / Pc), &sv, &cv);
+      wc->spsi = sv;
+      wc->cpsi = cv;
+      sincos(0.85 * e, &sv, &cv);
+      wc->sdel = sv;
+      wc->cdel = cv;
+      wc->pad[0] = wc->pad[1] = 0.0;
     }
   } else {
     // Gaia G term (loglikelihood :834-848) while wave 1 does the eclipse/Roche part
@@ -244,21 +284,31 @@ __device__ __forceinline__ double wave_sum(double v) {
 // per iteration (ILP for the fp64 Kepler chains), next iteration's times
 // prefetched; values go to vals[], min/max order keys returned per lane.
 template <int NT>
-__device__ __forceinline__ void model_pass(const double* __restrict__ t, int n, const WalkerConst& w,
-                                           double* vals, int tid, uint64_t& kmn_out, uint64_t& kmx_out) {
+__device__ __forceinline__ void model_pass(const double* __restrict__ t, const double2* __restrict__ ph, int n,
+                                           const WalkerConst& w, double* vals, int tid, uint64_t& kmn_out,
+                                           uint64_t& kmx_out) {
   constexpr int K = HB_K;
+  const bool tab = (ph != nullptr) && (w.tab != 0.0);  // walker-uniform
   // running min/max as doubles (v_min/v_max_f64); NaN lanes are tracked and
   // the order keys recomputed from vals[] in that (never observed) case
   double vmn = __builtin_inf(), vmx = -__builtin_inf();
   bool nan = false;
   const int last = n - 1;
   double tk[K];
+  double2 pk[K];
 #pragma unroll
-  for (int k = 0; k < K; ++k) tk[k] = t[min(k * NT + tid, last)];
+  for (int k = 0; k < K; ++k) {
+    tk[k] = t[min(k * NT + tid, last)];
+    pk[k] = tab ? ph[min(k * NT + tid, last)] : make_double2(0.0, 1.0);
+  }
   for (int base = 0; base < n; base += K * NT) {
     double tn[K];
+    double2 pn[K];
 #pragma unroll
-    for (int k = 0; k < K; ++k) tn[k] = t[min(base + (K + k) * NT + tid, last)];
+    for (int k = 0; k < K; ++k) {
+      tn[k] = t[min(base + (K + k) * NT + tid, last)];
+      pn[k] = tab ? ph[min(base + (K + k) * NT + tid, last)] : make_double2(0.0, 1.0);
+    }
     double v[K];
     bool bad;
 #if HB_ABLATE_MODEL  // experiment builds only: trivial model, same data flow
@@ -266,7 +316,7 @@ __device__ __forceinline__ void model_pass(const double* __restrict__ t, int n, 
     for (int k = 0; k < K; ++k) v[k] = tk[k] * w.kb + w.kr0;
     bad = false;
 #else
-    hb_cadence_flux_k<K>(tk, w, v, bad);
+    hb_cadence_flux_k<K>(tk, pk, tab, w, v, bad);
 #endif
     if (__any(bad)) {  // out-of-domain angles: reference-order ocml path
       if (bad) {
@@ -284,6 +334,7 @@ __device__ __forceinline__ void model_pass(const double* __restrict__ t, int n, 
         nan |= v[k] != v[k];
       }
       tk[k] = tn[k];
+      pk[k] = pn[k];
     }
   }
   // keys of the extremes; -0.0 / +0.0 compare equal but key apart: take the
@@ -407,7 +458,8 @@ __device__ __forceinline__ double block_sum(double v, SelShared* sh) {
 // ---------------------------------------------------------------------------
 template <int NW, bool LDS>
 __global__ __launch_bounds__(64 * NW) void hb_eval_kernel(
-    const double* __restrict__ t, const double* __restrict__ f, const double* __restrict__ isg,
+    const double* __restrict__ t, const double2* __restrict__ ph, const double* __restrict__ f,
+    const double* __restrict__ isg,
     long n, long kth, const WalkerConst* __restrict__ wcs, double* __restrict__ logl,
     double* __restrict__ tmpl_out, double* __restrict__ scratch, int mode) {
   constexpr int NT = 64 * NW;
@@ -427,7 +479,7 @@ __global__ __launch_bounds__(64 * NW) void hb_eval_kernel(
 
   // 1. model flux for every cadence
   uint64_t kmn, kmx;
-  model_pass<NT>(t, n, w, vals, tid, kmn, kmx);
+  model_pass<NT>(t, ph, (int)n, w, vals, tid, kmn, kmx);
   __syncthreads();
   block_minmax<NW>(kmn, kmx, sh);
 
@@ -766,6 +818,9 @@ __device__ __forceinline__ double wave_select2(const uint64_t (&key)[VPT], uint3
   return dval(readlane_u64(mine, who));
 }
 
+#ifndef HB_PHASE_TAB
+#define HB_PHASE_TAB 1  // 0: every walker evaluates sin/cos of the Kepler start directly
+#endif
 #ifndef HB_RUN_AGG
 #define HB_RUN_AGG 1  // block select: one LDS atomic per run of equal bins in a row of 16 lanes
 #endif
@@ -797,7 +852,8 @@ __device__ __forceinline__ int key_index(int v, int lane) {
 // its target's slice (tab[wt[walker]]); n and kth come from the descriptor.
 template <int VPT, bool MULTI>
 __global__ __launch_bounds__(64) HB_WPE_ATTR void hb_eval_wave_kernel(
-    const double* __restrict__ t, const double* __restrict__ f, const double* __restrict__ isg,
+    const double* __restrict__ t, const double2* __restrict__ ph, const double* __restrict__ f,
+    const double* __restrict__ isg,
     long n, long kth, const WalkerConst* __restrict__ wcs, double* __restrict__ logl,
     double* __restrict__ tmpl_out, int mode, int slab_bytes, const TargetDesc* __restrict__ tab,
     const int* __restrict__ wt, const int* __restrict__ list) {
@@ -808,6 +864,7 @@ __global__ __launch_bounds__(64) HB_WPE_ATTR void hb_eval_wave_kernel(
     wv = list[blockIdx.x];
     const TargetDesc& td = tab[wt[wv]];
     t += td.off;
+    if (ph) ph += td.off;
     f += td.off;
     isg += td.off;
     n = td.n;
@@ -823,7 +880,7 @@ __global__ __launch_bounds__(64) HB_WPE_ATTR void hb_eval_wave_kernel(
   }
 
   uint64_t kmn, kmx;
-  model_pass<64>(t, n, w, vals, lane, kmn, kmx);
+  model_pass<64>(t, ph, (int)n, w, vals, lane, kmn, kmx);
 #if HB_SEL_V == 1
   kmn = wave_min_u64(kmn);
   kmx = wave_max_u64(kmx);
@@ -995,7 +1052,8 @@ __device__ double block_select2(const uint64_t (&key)[VPT], uint32_t kth, uint64
 
 template <int NW, int VPT>
 __global__ __launch_bounds__(64 * NW) HB_WPE_ATTR void hb_eval_block_kernel(
-    const double* __restrict__ t, const double* __restrict__ f, const double* __restrict__ isg, long n,
+    const double* __restrict__ t, const double2* __restrict__ ph, const double* __restrict__ f,
+    const double* __restrict__ isg, long n,
     long kth, const WalkerConst* __restrict__ wcs, double* __restrict__ logl, double* __restrict__ tmpl_out,
     int mode) {
   constexpr int NT = 64 * NW;
@@ -1013,7 +1071,7 @@ __global__ __launch_bounds__(64 * NW) HB_WPE_ATTR void hb_eval_block_kernel(
   }
   const int nn = (int)n;
   uint64_t kmn, kmx;
-  model_pass<NT>(t, nn, w, vals, tid, kmn, kmx);
+  model_pass<NT>(t, ph, nn, w, vals, tid, kmn, kmx);
   kmn = wave_reduce_u64(kmn, OpMinU64());
   kmx = wave_reduce_u64(kmx, OpMaxU64());
   if (lane == 0) {
@@ -1199,15 +1257,18 @@ __global__ __launch_bounds__(1024) void hb_median_kernel(double* __restrict__ a,
 // host launchers
 // ---------------------------------------------------------------------------
 hipError_t launch_prep(const double* d_params, int nwalk, const MagArgs& ma, WalkerConst* d_wc,
-                       hipStream_t s, const TargetDesc* tab, const int* wt) {
+                       hipStream_t s, const TargetDesc* tab, const int* wt, const double* t, long n,
+                       double2* ph, const int* w0, int ntargets) {
   if (nwalk <= 0) return hipSuccess;
+  if (t == nullptr || (tab != nullptr && w0 == nullptr) || !HB_PHASE_TAB) ph = nullptr;
   hipLaunchKernelGGL(hb_prep_kernel, dim3((nwalk + kPrepWalkers - 1) / kPrepWalkers), dim3(2 * kPrepWalkers), 0, s,
-                     d_params, nwalk, ma, d_wc, tab, wt);
+                     d_params, nwalk, ma, d_wc, tab, wt, t, (int)n, ph, w0, ntargets);
   return hipGetLastError();
 }
 
 template <int NW, int VPT>
-static hipError_t launch_block_t(const EvalPlan& pl, const double* t, const double* f, const double* sg,
+static hipError_t launch_block_t(const EvalPlan& pl, const double* t, const double2* ph, const double* f,
+                                 const double* sg,
                                  const WalkerConst* wc, int nwalk, double* logl, double* tmpl, int mode,
                                  hipStream_t s) {
   auto kern = hb_eval_block_kernel<NW, VPT>;
@@ -1218,13 +1279,14 @@ static hipError_t launch_block_t(const EvalPlan& pl, const double* t, const doub
     if (e != hipSuccess) return e;
     attr_set = true;
   }
-  hipLaunchKernelGGL(kern, dim3(nwalk), dim3(64 * NW), pl.lds_bytes, s, t, f, sg, pl.n, pl.kth, wc, logl, tmpl,
-                     mode);
+  hipLaunchKernelGGL(kern, dim3(nwalk), dim3(64 * NW), pl.lds_bytes, s, t, ph, f, sg, pl.n, pl.kth, wc, logl,
+                     tmpl, mode);
   return hipGetLastError();
 }
 
 template <int NW, bool LDS>
-static hipError_t launch_eval_t(const EvalPlan& pl, const double* t, const double* f, const double* sg,
+static hipError_t launch_eval_t(const EvalPlan& pl, const double* t, const double2* ph, const double* f,
+                                const double* sg,
                                 const WalkerConst* wc, int nwalk, double* logl, double* tmpl,
                                 double* scratch, int mode, hipStream_t s) {
   auto kern = hb_eval_kernel<NW, LDS>;
@@ -1235,62 +1297,65 @@ static hipError_t launch_eval_t(const EvalPlan& pl, const double* t, const doubl
     if (e != hipSuccess) return e;
     attr_set = true;
   }
-  hipLaunchKernelGGL(kern, dim3(nwalk), dim3(64 * NW), pl.lds_bytes, s, t, f, sg, pl.n, pl.kth, wc,
+  hipLaunchKernelGGL(kern, dim3(nwalk), dim3(64 * NW), pl.lds_bytes, s, t, ph, f, sg, pl.n, pl.kth, wc,
                      logl, tmpl, scratch, mode);
   return hipGetLastError();
 }
 
 template <int VPT>
-static hipError_t launch_wave_t(const EvalPlan& pl, const double* t, const double* f, const double* sg,
+static hipError_t launch_wave_t(const EvalPlan& pl, const double* t, const double2* ph, const double* f,
+                                const double* sg,
                                 const WalkerConst* wc, int nwalk, double* logl, double* tmpl, int mode,
                                 hipStream_t s) {
-  hipLaunchKernelGGL((hb_eval_wave_kernel<VPT, false>), dim3(nwalk), dim3(64), pl.lds_bytes, s, t, f, sg, pl.n,
-                     pl.kth, wc, logl, tmpl, mode, (int)pl.slab_bytes, nullptr, nullptr, nullptr);
+  hipLaunchKernelGGL((hb_eval_wave_kernel<VPT, false>), dim3(nwalk), dim3(64), pl.lds_bytes, s, t, ph, f, sg,
+                     pl.n, pl.kth, wc, logl, tmpl, mode, (int)pl.slab_bytes, nullptr, nullptr, nullptr);
   return hipGetLastError();
 }
 
 template <int VPT>
-static hipError_t launch_multi_t(size_t slab, const double* t, const double* f, const double* sg,
+static hipError_t launch_multi_t(size_t slab, const double* t, const double2* ph, const double* f,
+                                 const double* sg,
                                  const TargetDesc* tab, const int* wt, const int* list, int count,
                                  const WalkerConst* wc, double* logl, hipStream_t s) {
   const size_t lds = slab + 8 * kCandMax;
-  hipLaunchKernelGGL((hb_eval_wave_kernel<VPT, true>), dim3(count), dim3(64), lds, s, t, f, sg, 0L, 0L, wc, logl,
-                     nullptr, 0, (int)slab, tab, wt, list);
+  hipLaunchKernelGGL((hb_eval_wave_kernel<VPT, true>), dim3(count), dim3(64), lds, s, t, ph, f, sg, 0L, 0L,
+                     wc, logl, nullptr, 0, (int)slab, tab, wt, list);
   return hipGetLastError();
 }
 
-hipError_t launch_eval_multi(int vpt, size_t slab, const double* t, const double* f, const double* sg,
+hipError_t launch_eval_multi(int vpt, size_t slab, const double* t, const double2* ph, const double* f,
+                             const double* sg,
                              const TargetDesc* tab, const int* wt, const int* list, int count,
                              const WalkerConst* wc, double* logl, hipStream_t s) {
   if (count <= 0) return hipSuccess;
   switch (vpt) {
-    case 1: return launch_multi_t<1>(slab, t, f, sg, tab, wt, list, count, wc, logl, s);
-    case 2: return launch_multi_t<2>(slab, t, f, sg, tab, wt, list, count, wc, logl, s);
-    case 4: return launch_multi_t<4>(slab, t, f, sg, tab, wt, list, count, wc, logl, s);
-    case 8: return launch_multi_t<8>(slab, t, f, sg, tab, wt, list, count, wc, logl, s);
-    case 16: return launch_multi_t<16>(slab, t, f, sg, tab, wt, list, count, wc, logl, s);
-    case 32: return launch_multi_t<32>(slab, t, f, sg, tab, wt, list, count, wc, logl, s);
+    case 1: return launch_multi_t<1>(slab, t, ph, f, sg, tab, wt, list, count, wc, logl, s);
+    case 2: return launch_multi_t<2>(slab, t, ph, f, sg, tab, wt, list, count, wc, logl, s);
+    case 4: return launch_multi_t<4>(slab, t, ph, f, sg, tab, wt, list, count, wc, logl, s);
+    case 8: return launch_multi_t<8>(slab, t, ph, f, sg, tab, wt, list, count, wc, logl, s);
+    case 16: return launch_multi_t<16>(slab, t, ph, f, sg, tab, wt, list, count, wc, logl, s);
+    case 32: return launch_multi_t<32>(slab, t, ph, f, sg, tab, wt, list, count, wc, logl, s);
     default: return hipErrorInvalidValue;
   }
 }
 
-hipError_t launch_eval(const EvalPlan& pl, const double* t, const double* f, const double* sg,
+hipError_t launch_eval(const EvalPlan& pl, const double* t, const double2* ph, const double* f, const double* sg,
                        const WalkerConst* wc, int nwalk, double* logl, double* tmpl, double* scratch,
                        int mode, hipStream_t s) {
   if (nwalk <= 0) return hipSuccess;
   switch (pl.vpt) {
     case 0: break;
-    case 1: return launch_wave_t<1>(pl, t, f, sg, wc, nwalk, logl, tmpl, mode, s);
-    case 2: return launch_wave_t<2>(pl, t, f, sg, wc, nwalk, logl, tmpl, mode, s);
-    case 4: return launch_wave_t<4>(pl, t, f, sg, wc, nwalk, logl, tmpl, mode, s);
-    case 8: return launch_wave_t<8>(pl, t, f, sg, wc, nwalk, logl, tmpl, mode, s);
-    case 16: return launch_wave_t<16>(pl, t, f, sg, wc, nwalk, logl, tmpl, mode, s);
-    case 32: return launch_wave_t<32>(pl, t, f, sg, wc, nwalk, logl, tmpl, mode, s);
+    case 1: return launch_wave_t<1>(pl, t, ph, f, sg, wc, nwalk, logl, tmpl, mode, s);
+    case 2: return launch_wave_t<2>(pl, t, ph, f, sg, wc, nwalk, logl, tmpl, mode, s);
+    case 4: return launch_wave_t<4>(pl, t, ph, f, sg, wc, nwalk, logl, tmpl, mode, s);
+    case 8: return launch_wave_t<8>(pl, t, ph, f, sg, wc, nwalk, logl, tmpl, mode, s);
+    case 16: return launch_wave_t<16>(pl, t, ph, f, sg, wc, nwalk, logl, tmpl, mode, s);
+    case 32: return launch_wave_t<32>(pl, t, ph, f, sg, wc, nwalk, logl, tmpl, mode, s);
     default: return hipErrorInvalidValue;
   }
   if (pl.bvpt > 0) {
 #define HB_BCASE(NWV, V)                                                                    \
-  if (pl.nw == NWV && pl.bvpt == V) return launch_block_t<NWV, V>(pl, t, f, sg, wc, nwalk, logl, tmpl, mode, s);
+  if (pl.nw == NWV && pl.bvpt == V) return launch_block_t<NWV, V>(pl, t, ph, f, sg, wc, nwalk, logl, tmpl, mode, s);
     HB_BCASE(4, 8) HB_BCASE(4, 16) HB_BCASE(4, 24) HB_BCASE(4, 32)
     HB_BCASE(8, 8) HB_BCASE(8, 16) HB_BCASE(8, 24) HB_BCASE(8, 32)
     HB_BCASE(16, 8) HB_BCASE(16, 16) HB_BCASE(16, 24) HB_BCASE(16, 32)
@@ -1299,8 +1364,8 @@ hipError_t launch_eval(const EvalPlan& pl, const double* t, const double* f, con
   }
 #define HB_CASE(NWV)                                                                              \
   case NWV:                                                                                       \
-    return pl.lds ? launch_eval_t<NWV, true>(pl, t, f, sg, wc, nwalk, logl, tmpl, scratch, mode, s) \
-                  : launch_eval_t<NWV, false>(pl, t, f, sg, wc, nwalk, logl, tmpl, scratch, mode, s);
+    return pl.lds ? launch_eval_t<NWV, true>(pl, t, ph, f, sg, wc, nwalk, logl, tmpl, scratch, mode, s) \
+                  : launch_eval_t<NWV, false>(pl, t, ph, f, sg, wc, nwalk, logl, tmpl, scratch, mode, s);
   switch (pl.nw) {
     HB_CASE(1)
     HB_CASE(2)
