@@ -61,6 +61,18 @@ namespace hbk {
 constexpr int kPrepWalkers = HB_PREP_W;  // walkers per prep block (2 lanes each)
 constexpr int kWcDoubles = (int)(sizeof(WalkerConst) / sizeof(double));
 
+// sin/cos of a phase-table angle: the branch-free reduction for |x| < 2^19,
+// ocml otherwise (never for folded light curves)
+__device__ __forceinline__ void sincos_table(double x, double& sv, double& cv) {
+  if (sincos_fast_ok(x)) {
+    sincos_fast(x, &sv, &cv);
+  } else {
+    const SinCos r = sincos_ocml(x);
+    sv = r.s;
+    cv = r.c;
+  }
+}
+
 __global__ __launch_bounds__(2 * kPrepWalkers) void hb_prep_kernel(const double* __restrict__ params,
                                                                     int nwalk, MagArgs ma,
                                                                     WalkerConst* __restrict__ out,
@@ -76,31 +88,6 @@ __global__ __launch_bounds__(2 * kPrepWalkers) void hb_prep_kernel(const double*
   const int base = blockIdx.x * kPrepWalkers;
   const int nb = min(kPrepWalkers, nwalk - base);
   for (int i = tid; i < nb * kNpars; i += 2 * kPrepWalkers) sp[i] = params[(size_t)base * kNpars + i];
-  // Shared-period phase table (WalkerConst::tab): per light curve, for the
-  // period of its first walker in this batch, ph[i] = (sin, cos)(t_i DAY 2pi/Pc0).
-  // Single context: walker 0, cadences [0, ncad).  Catalog: target k's first
-  // walker w0[k] (-1: no walkers), its slice of the concatenated arrays.
-  if (ph) {
-    if (tab == nullptr) {
-      const double mA0 = kTwoPi / (exp10(params[2]) * kDay);
-      for (int i = blockIdx.x * blockDim.x + tid; i < ncad; i += gridDim.x * blockDim.x) {
-        double sv, cv;
-        sincos((tcad[i] * kDay) * mA0, &sv, &cv);
-        ph[i] = make_double2(sv, cv);
-      }
-    } else {
-      for (int k = blockIdx.x; k < ntargets; k += gridDim.x) {
-        if (w0[k] < 0) continue;
-        const double mA0 = kTwoPi / (exp10(params[(size_t)w0[k] * kNpars + 2]) * kDay);
-        const long off = tab[k].off;
-        for (int i = tid; i < (int)tab[k].n; i += blockDim.x) {
-          double sv, cv;
-          sincos((tcad[off + i] * kDay) * mA0, &sv, &cv);
-          ph[off + i] = make_double2(sv, cv);
-        }
-      }
-    }
-  }
   __syncthreads();
 #if HB_PREP_ABL == 4  // experiment builds only: data movement, no math
   {
@@ -188,10 +175,10 @@ __global__ __launch_bounds__(2 * kPrepWalkers) void hb_prep_kernel(const double*
       const bool use_tab = (ph != nullptr) && (Pc == Pc0);
       wc->tab = use_tab ? 1.0 : 0.0;
       double sv = 0.0, cv = 1.0;
-      if (use_tab) sincos((p[6] * kDay) * (kTwoPi / Pc), &sv, &cv);
+      if (use_tab) sincos_table((p[6] * kDay) * (kTwoPi / Pc), sv, cv);
       wc->spsi = sv;
       wc->cpsi = cv;
-      sincos(0.85 * e, &sv, &cv);
+      sincos_table(0.85 * e, sv, cv);
       wc->sdel = sv;
       wc->cdel = cv;
       wc->pad[0] = wc->pad[1] = 0.0;
@@ -253,6 +240,32 @@ __global__ __launch_bounds__(2 * kPrepWalkers) void hb_prep_kernel(const double*
   __syncthreads();
   double* dst = reinterpret_cast<double*>(out) + (size_t)base * kWcDoubles;
   for (int i = tid; i < nb * kWcDoubles; i += 2 * kPrepWalkers) dst[i] = so[i];
+  // Shared-period phase table (WalkerConst::tab), written after the walker
+  // records so its latency overlaps their stores: per light curve, for the
+  // period of its first walker in this batch, ph[i] = (sin, cos)(t_i DAY 2pi/Pc0).
+  // Single context: walker 0, cadences [0, ncad).  Catalog: target k's first
+  // walker w0[k] (-1: no walkers), its slice of the concatenated arrays.
+  if (ph) {
+    if (tab == nullptr) {
+      const double mA0 = kTwoPi / (exp10(params[2]) * kDay);
+      for (int i = blockIdx.x * blockDim.x + tid; i < ncad; i += gridDim.x * blockDim.x) {
+        double sv, cv;
+        sincos_table((tcad[i] * kDay) * mA0, sv, cv);
+        ph[i] = make_double2(sv, cv);
+      }
+    } else {
+      for (int k = blockIdx.x; k < ntargets; k += gridDim.x) {
+        if (w0[k] < 0) continue;
+        const double mA0 = kTwoPi / (exp10(params[(size_t)w0[k] * kNpars + 2]) * kDay);
+        const long off = tab[k].off;
+        for (int i = tid; i < (int)tab[k].n; i += blockDim.x) {
+          double sv, cv;
+          sincos_table((tcad[off + i] * kDay) * mA0, sv, cv);
+          ph[off + i] = make_double2(sv, cv);
+        }
+      }
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------
