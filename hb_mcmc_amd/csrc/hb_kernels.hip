@@ -87,7 +87,20 @@ __global__ __launch_bounds__(2 * kPrepWalkers) void hb_prep_kernel(const double*
   const int tid = threadIdx.x;
   const int base = blockIdx.x * kPrepWalkers;
   const int nb = min(kPrepWalkers, nwalk - base);
-  for (int i = tid; i < nb * kNpars; i += 2 * kPrepWalkers) sp[i] = params[(size_t)base * kNpars + i];
+  {  // all loads in flight before the first LDS write (a rolled loop serialises on vmcnt(0))
+    constexpr int U = (kPrepWalkers * kNpars + 2 * kPrepWalkers - 1) / (2 * kPrepWalkers);
+    double v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = tid + u * 2 * kPrepWalkers;
+      v[u] = i < nb * kNpars ? params[(size_t)base * kNpars + i] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = tid + u * 2 * kPrepWalkers;
+      if (i < nb * kNpars) sp[i] = v[u];
+    }
+  }
   __syncthreads();
 #if HB_PREP_ABL == 4  // experiment builds only: data movement, no math
   {
@@ -238,8 +251,21 @@ __global__ __launch_bounds__(2 * kPrepWalkers) void hb_prep_kernel(const double*
     wc->chi2_extra = gr * gr;
   }
   __syncthreads();
-  double* dst = reinterpret_cast<double*>(out) + (size_t)base * kWcDoubles;
-  for (int i = tid; i < nb * kWcDoubles; i += 2 * kPrepWalkers) dst[i] = so[i];
+  {
+    double* dst = reinterpret_cast<double*>(out) + (size_t)base * kWcDoubles;
+    constexpr int U = (kPrepWalkers * kWcDoubles + 2 * kPrepWalkers - 1) / (2 * kPrepWalkers);
+    double v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = tid + u * 2 * kPrepWalkers;
+      v[u] = i < nb * kWcDoubles ? so[i] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = tid + u * 2 * kPrepWalkers;
+      if (i < nb * kWcDoubles) dst[i] = v[u];
+    }
+  }
   // Shared-period phase table (WalkerConst::tab), written after the walker
   // records so its latency overlaps their stores: per light curve, for the
   // period of its first walker in this batch, ph[i] = (sin, cos)(t_i DAY 2pi/Pc0).
