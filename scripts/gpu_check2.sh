@@ -12,3 +12,4 @@ step pytest_gpu 900 python -m pytest tests -q -m gpu -p no:cacheprovider
 step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 step bench_c2 600 python bench.py --steps 200 --warmup 20
 step bench_c3 600 python bench.py --ncad 20000 --steps 20 --warmup 3 --no-cpu-baseline
+step bench_c5 600 python bench.py --config C5 --steps 100 --warmup 10
