@@ -185,6 +185,34 @@ def test_block_kernel_sizes(hbmi, oracle, n):
     assert (np.abs(tm - ref) <= tol).all()
 
 
+@pytest.mark.parametrize("n", [1024, 6001])
+def test_phase_table_and_direct_paths(hbmi, oracle, n):
+    """Walkers on the batch's table period (walker 0's P) take the phase-table
+    Kepler start, the others the direct sincos; both against the oracle, and a
+    walker's logL agrees whichever path it takes.  T0 = 0 and T0 = t_k put
+    cadences exactly on x = 0 (the exact-fmod branch)."""
+    from hb_mcmc_amd import synth
+    from hb_mcmc_amd.likelihood import HBLikelihood
+
+    t, f, s = synth.dataset(n, oracle.light_curve)
+    P = synth.walkers(48, seed=11, roche_frac=0.0)
+    P[1::3, 2] += 1e-3 * np.random.default_rng(4).standard_normal(len(P[1::3]))  # off the table period
+    P[3, 6] = 0.0
+    P[6, 6] = t[5]
+    P[9, 3] = 0.6  # larger steps: direct sincos inside the Newton loop
+    Q = P.copy()
+    Q[0, 2] += 2e-3  # walker 0 moves: now every other walker is off the table period
+    with HBLikelihood(t, f, s) as L:
+        a = L.loglike(P)
+        b = L.loglike(Q)
+        tm = L.light_curve(P)
+    ref = oracle.loglike_batch(t, f, s, P, synth.MAG_DEFAULT, synth.MAGERR_DEFAULT, 8)
+    close_logl(a, ref)
+    close_logl(b[1:], ref[1:])
+    tol = lc_tol(P[:, 3])[:, None]
+    assert (np.abs(tm - oracle.light_curve_batch(t, P, 8)) <= tol).all()
+
+
 def test_real_1861_cadences(hbmi):
     from hb_mcmc_amd.likelihood import HBLikelihood
 
