@@ -35,6 +35,12 @@ using namespace hbdev;
 #else
 #define HB_WPE_ATTR
 #endif
+#ifndef HB_UNCOND_PH
+#define HB_UNCOND_PH 0  // 1: unpredicated table loads (measured slower: register pressure)
+#endif
+#ifndef HB_FULLTILE
+#define HB_FULLTILE 1  // full K*64 tiles store without per-cadence bounds tests
+#endif
 #ifndef HB_PREP_ABL
 #define HB_PREP_ABL 0  // experiment builds only: 1 no Gaia flux, 2 no star_coef, 3 no radius law
 #endif
@@ -333,20 +339,30 @@ __device__ __forceinline__ void model_pass(const double* __restrict__ t, const d
   double vmn = __builtin_inf(), vmx = -__builtin_inf();
   bool nan = false;
   const int last = n - 1;
+  // table entries load unconditionally: off the table, from t[0..1] (ignored)
+#if HB_UNCOND_PH
+  const double2* __restrict__ php = tab ? ph : reinterpret_cast<const double2*>(t);
+  const int pmask = tab ? ~0 : 0;
+#define HB_PH_LOAD(i) php[(i) & pmask]
+#else
+#define HB_PH_LOAD(i) (tab ? ph[i] : make_double2(0.0, 1.0))
+#endif
   double tk[K];
   double2 pk[K];
 #pragma unroll
   for (int k = 0; k < K; ++k) {
-    tk[k] = t[min(k * NT + tid, last)];
-    pk[k] = tab ? ph[min(k * NT + tid, last)] : make_double2(0.0, 1.0);
+    const int i = min(k * NT + tid, last);
+    tk[k] = t[i];
+    pk[k] = HB_PH_LOAD(i);
   }
   for (int base = 0; base < n; base += K * NT) {
     double tn[K];
     double2 pn[K];
 #pragma unroll
     for (int k = 0; k < K; ++k) {
-      tn[k] = t[min(base + (K + k) * NT + tid, last)];
-      pn[k] = tab ? ph[min(base + (K + k) * NT + tid, last)] : make_double2(0.0, 1.0);
+      const int i = min(base + (K + k) * NT + tid, last);
+      tn[k] = t[i];
+      pn[k] = HB_PH_LOAD(i);
     }
     double v[K];
     bool bad;
@@ -363,15 +379,28 @@ __device__ __forceinline__ void model_pass(const double* __restrict__ t, const d
         for (int k = 0; k < K; ++k) v[k] = hb_cadence_flux_slow(tk[k], &w);
       }
     }
+    if (HB_FULLTILE && base + K * NT <= n) {  // full tile: no per-cadence bounds test
 #pragma unroll
-    for (int k = 0; k < K; ++k) {
-      const int i = base + k * NT + tid;
-      if (i < n) {
-        vals[i] = v[k];
+      for (int k = 0; k < K; ++k) {
+        vals[base + k * NT + tid] = v[k];
         vmn = fmin(vmn, v[k]);
         vmx = fmax(vmx, v[k]);
         nan |= v[k] != v[k];
       }
+    } else {
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        const int i = base + k * NT + tid;
+        if (i < n) {
+          vals[i] = v[k];
+          vmn = fmin(vmn, v[k]);
+          vmx = fmax(vmx, v[k]);
+          nan |= v[k] != v[k];
+        }
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
       tk[k] = tn[k];
       pk[k] = pn[k];
     }
