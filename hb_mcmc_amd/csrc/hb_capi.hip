@@ -56,6 +56,8 @@ static int set_err_msg(const std::string& m, int code = -1) {
 }
 
 extern "C" const char* hb_last_error(void) { return g_err.c_str(); }
+// internal (hb_dsampler.hip): report through hb_last_error()
+extern "C" int hbx_set_error(const char* msg) { return set_err_msg(msg ? msg : "error"); }
 
 // ---------------------------------------------------------------------------
 // one-time runtime setup, transparent to the caller's glibc rand() sequence
@@ -164,6 +166,8 @@ struct hb_ctx {
   double* d_out = nullptr;       // hcap x n (templates) or hcap (logL)
   std::mutex mu;
 };
+
+extern "C" int hbx_ctx_device(const hb_ctx* c) { return c ? c->device : 0; }
 
 static int ctx_release_ws(hb_ctx* c) {
   if (c->d_wc) (void)hipFree(c->d_wc);

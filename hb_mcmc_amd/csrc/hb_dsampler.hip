@@ -1,0 +1,966 @@
+// hb_dsampler.hip -- the PT-MCMC step of mcmc_wrapper2.c (:378-650) resident
+// on the GPU: proposals, walls, priors, likelihood, Hastings test, history and
+// the tempering swaps all run as kernels on one stream, so an iteration never
+// waits for the host.  Results are bit-identical to the host sampler
+// (hb_sampler.cpp) and so to the reference's bookkeeping:
+//   * the integer L'Ecuyer/Bays-Durham streams (ran2_parallel :894-943) run
+//     per slot in 32-bit arithmetic (Schrage's products stay below 2^31), the
+//     shuffle table staged in LDS;
+//   * every libm call on the state path goes through hb_glibc_math.hpp, the
+//     bit-exact port of the host glibc's exp/log/pow; sqrt and division are
+//     IEEE (correctly rounded) on gfx950 as on x86;
+//   * the W sequential ptmcmc attempts (:768-817) consume glibc rand() in a
+//     fixed order that does not depend on the data, so the host draws them
+//     ahead (hbx_swap_draws) and sorts the attempts into dependency levels:
+//     attempt i touches slots b_i, b_i + 1 and must follow every earlier
+//     attempt that touches either; attempts within a level touch disjoint
+//     slots and commute.  One workgroup then replays the ~10 levels (W = 4096)
+//     with the exact exp() test, index[] and logL in LDS.
+// State is kept by chain id like the reference (x[chain], logL[chain],
+// index[slot] -> chain), so a swap moves one int, not a 23-double record.
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+#include <chrono>
+#include <string>
+#include <vector>
+
+#include "../../include/hb_sampler.h"
+#include "../../include/hbmi.h"
+#include "hb_glibc_math.hpp"
+#include "hb_sampler_view.hpp"
+
+extern "C" int hbx_set_error(const char* msg);
+extern "C" int hbx_ctx_device(const hb_ctx* c);
+
+namespace hbds {
+
+constexpr int kNp = 21;
+constexpr int NTAB = 32;
+constexpr int IM1 = 2147483563, IM2 = 2147483399, IMM1 = IM1 - 1;
+constexpr int IA1 = 40014, IA2 = 40692, IQ1 = 53668, IQ2 = 52774, IR1 = 12211, IR2 = 3791;
+constexpr int NDIV = 1 + IMM1 / NTAB;
+constexpr double AM = 1.0 / IM1;
+constexpr double RNMX = 1.0 - 1.2e-7;
+constexpr double kSqrt2Pi = 2.5066282746;  // mcmc_wrapper2.h:10
+constexpr int kBlk = 64;                   // slots per workgroup of the per-slot kernels
+constexpr int kSwapThreads = 1024;
+constexpr int kEvCap = 1024;               // big-jump records between drains (<= 6 per iteration)
+
+// run constants (kernel argument)
+struct Params {
+  int W, NPAST;
+  int log_on;
+  int pad;
+  double log_lc_period, LC_PERIOD;
+  double lim_lo[kNp], lim_hi[kNp];  // limits[i]
+  double fl_lo[kNp], fl_hi[kNp];    // limited[i] (1 reflecting, 2 periodic; doubles as in bounds)
+  double sigma_p[kNp];
+  int gpflag[kNp];
+};
+
+struct Counters {
+  long long acc, DEacc, DEtrial, atrial, cold_acc, nswap;
+  long long DEacc_tot, DEtrial_tot;  // sum over slots of DEacc_arr / DEtrial_arr
+  long long acc_it;                  // cold-chain acceptances of this iteration
+  long long snap[4];                 // {acc, DEacc, DEtrial, atrial} as printed at :577-579
+  double logLmap;
+  double xmap[kNp];
+  int nev;
+  int pad;
+};
+
+struct Event {  // LogSuspiciousJumps (:520-528) arguments
+  long long iter;
+  int chain, jtype, slot, pad;
+  double H, alpha, tmp, lx, ly, px, py;
+  double xo[kNp], xn[kNp];
+};
+
+struct SwapEnt {
+  int b;
+  int pad;
+  double beta;
+};
+
+// device state (pointers into one allocation set)
+struct Dev {
+  double* x;       // [W][21] by chain
+  double* logL;    // [W] by chain
+  double* logP;    // [W] by chain
+  int* logP_ok;    // [W] by chain
+  int* idx;        // [W] slot -> chain
+  double* temp;    // [W]
+  int* idum;       // [W] ran2 state by slot
+  int* idum2;
+  int* iy;
+  int* iset;
+  double* gset;
+  long long* cts;
+  int* iv;         // [32][W]
+  double* y;       // [W][21] proposals by slot
+  double* logPy;   // [W]
+  double* alpha2;  // [W]
+  double* logLy;   // [W]
+  int* jump;       // [W]
+  int* jtype;      // [W]
+  double* hist;    // [W][NPAST][21] by slot
+  int* DEacc_arr;  // [W]
+  int* DEtrial_arr;
+  Counters* ctr;
+  Event* ev;
+};
+
+// ---------------------------------------------------------------------------
+// ran2_parallel / gasdev2_parallel (:894-974), one slot per lane
+// ---------------------------------------------------------------------------
+struct Rng {
+  int idum, idum2, iy, iset;
+  double gset;
+  long long cts;
+  int* iv;  // LDS column, stride kBlk
+};
+
+__device__ double ran2(Rng& r) {
+  r.cts += 1;
+  if (r.idum <= 0) {
+    r.idum = (-(r.idum) < 1) ? 1 : -(r.idum);
+    r.idum2 = r.idum;
+    for (int j = NTAB + 7; j >= 0; --j) {
+      const int k = r.idum / IQ1;
+      r.idum = IA1 * (r.idum - k * IQ1) - k * IR1;
+      if (r.idum < 0) r.idum += IM1;
+      if (j < NTAB) r.iv[j * kBlk] = r.idum;
+    }
+    r.iy = r.iv[0];
+  }
+  int k = r.idum / IQ1;
+  r.idum = IA1 * (r.idum - k * IQ1) - k * IR1;
+  if (r.idum < 0) r.idum += IM1;
+  k = r.idum2 / IQ2;
+  r.idum2 = IA2 * (r.idum2 - k * IQ2) - k * IR2;
+  if (r.idum2 < 0) r.idum2 += IM2;
+  const int j = r.iy / NDIV;
+  r.iy = r.iv[j * kBlk] - r.idum2;
+  r.iv[j * kBlk] = r.idum;
+  if (r.iy < 1) r.iy += IMM1;
+  const double temp = AM * (double)r.iy;
+  return temp > RNMX ? RNMX : temp;
+}
+
+__device__ double gasdev(Rng& r) {
+  if (r.idum < 0) r.iset = 0;
+  if (r.iset == 0) {
+    double v1, v2, rsq;
+    do {
+      v1 = 2.0 * ran2(r) - 1.0;
+      v2 = 2.0 * ran2(r) - 1.0;
+      rsq = v1 * v1 + v2 * v2;
+    } while (rsq >= 1.0 || rsq == 0.0);
+    const double fac = sqrt(-2.0 * hbglibc::log(rsq) / rsq);
+    r.gset = v1 * fac;
+    r.iset = 1;
+    return v2 * fac;
+  }
+  r.iset = 0;
+  return r.gset;
+}
+
+// gaussian() (:1175-1178) and get_logP (:703-765)
+__device__ double gauss_pdf(double x, double mean, double sigma) {
+  return (1 / sigma / kSqrt2Pi) * hbglibc::exp(-hbglibc::pow((x - mean) / sigma, 2.) / 2.);
+}
+
+__device__ double log_prior(const double* x, const Params& P) {
+  double lp = 0.;
+#pragma unroll
+  for (int i = 0; i < kNp; ++i) {
+    double mean, sig;
+    if (i == 7 || i == 8) { mean = 0.; sig = 1.; }
+    else if (i == 9 || i == 11) { mean = 0.16; sig = 0.04; }
+    else if (i == 10 || i == 12) { mean = 0.34; sig = 0.04; }
+    else if (i == 13 || i == 14) { mean = 1.; sig = 0.2; }
+    else if (i == 15 || i == 16) { mean = 0.; sig = 0.1; }
+    else if (i == 17 || i == 18) { mean = 0.; sig = 1.; }
+    else { mean = 0.; sig = 1.e15; }
+    if (P.gpflag[i] == 1) lp += hbglibc::log(gauss_pdf(x[i], mean, sig));
+  }
+  return lp;
+}
+
+// gaussian_proposal_parallel (:1062-1088)
+__device__ void gaussian_step(const double* x, Rng& r, const Params& P, double scale, double temp, double* y) {
+  const double sqtemp = sqrt(temp);
+  double dx[kNp];
+  for (int n = 0; n < kNp; ++n) dx[n] = gasdev(r) * P.sigma_p[n] * sqtemp * scale;
+#pragma unroll
+  for (int n = 0; n < kNp; ++n) y[n] = x[n] + dx[n];
+}
+
+// differential_evolution_proposal_parallel (:1091-1140) as compiled (see
+// hb_sampler.cpp de_step: a == 0, the uninitialised c == 0)
+__device__ void de_step(const double* x, Rng& r, const double* hist, int npast, double* y) {
+  int a = (int)(ran2(r) * npast);
+  a = (int)ran2(r);
+  int b = a;
+  while (b == a) b = (int)(ran2(r) * npast);
+  const double g0 = gauss_pdf(0, 0, 1.e-4) - 0.5;
+  double dx[kNp], eps[kNp];
+#pragma unroll
+  for (int n = 0; n < kNp; ++n) {
+    dx[n] = hist[(size_t)b * kNp + n] - hist[(size_t)a * kNp + n];
+    eps[n] = dx[n] * g0;
+  }
+  if (ran2(r) < 0.9) {
+    const double gamma = 2.388 / sqrt(2. * kNp);  // GAMMA, mcmc_wrapper2.h:13
+    for (int n = 0; n < kNp; ++n) dx[n] *= gasdev(r) * gamma;
+  }
+#pragma unroll
+  for (int n = 0; n < kNp; ++n) {
+    dx[n] += eps[n];
+    y[n] = x[n] + dx[n];
+  }
+}
+
+// walls (:440-467), bounded like hb_sampler.cpp apply_walls
+__device__ void apply_walls(double* y, const Params& P) {
+#pragma unroll
+  for (int i = 0; i < kNp; ++i) {
+    const double lo = P.lim_lo[i], hi = P.lim_hi[i];
+    double v = y[i];
+    for (long guard = 0; guard < 100000000L; ++guard) {
+      const bool below = (P.fl_lo[i] == 1) && (v < lo);
+      const bool above = (P.fl_hi[i] == 1) && (v > hi);
+      if (!(below || above)) break;
+      v = (v < lo) ? 2.0 * lo - v : 2.0 * hi - v;
+    }
+    for (long guard = 0; (P.fl_lo[i] == 2) && (v < lo) && guard < 100000000L; ++guard) v = hi + (v - lo);
+    for (long guard = 0; (P.fl_hi[i] == 2) && (v > hi) && guard < 100000000L; ++guard) v = lo + (v - hi);
+    y[i] = v;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// kernels
+// ---------------------------------------------------------------------------
+// proposals (:386-485) for every slot; y, logPy, jump, alpha2 by slot
+__global__ __launch_bounds__(kBlk) void ds_propose(Params P, Dev D, long long iter) {
+  __shared__ int ivs[NTAB * kBlk];
+  const int lane = threadIdx.x;
+  const int j = blockIdx.x * kBlk + lane;
+  if (j >= P.W) return;
+  int* iv = &ivs[lane];
+  for (int t = 0; t < NTAB; ++t) iv[t * kBlk] = D.iv[(size_t)t * P.W + j];
+  Rng r{D.idum[j], D.idum2[j], D.iy[j], D.iset[j], D.gset[j], D.cts[j], iv};
+  const int chain = D.idx[j];
+  double xc[kNp], y[kNp];
+#pragma unroll
+  for (int i = 0; i < kNp; ++i) xc[i] = D.x[(size_t)chain * kNp + i];
+  const double a = ran2(r);
+  const double jscale = hbglibc::pow(10., -6. + 6. * a);
+  int jmp = 0, jt = 0;
+  if ((ran2(r) < 0.5) && (iter > P.NPAST)) jmp = 1;
+  if (jmp == 0) {
+    gaussian_step(xc, r, P, jscale, D.temp[j], y);
+    jt = 1;
+  }
+  if (jmp == 1) {
+    if (chain == 0) {
+      D.DEtrial_arr[j]++;
+      atomicAdd((unsigned long long*)&D.ctr->DEtrial_tot, 1ull);
+    }
+    de_step(xc, r, &D.hist[(size_t)j * P.NPAST * kNp], P.NPAST, y);
+    jt = 2;
+    double dx_mag = 0;
+    for (int i = 0; i < kNp; ++i) dx_mag += (xc[i] - y[i]) * (xc[i] - y[i]);
+    if (dx_mag < 1e-6) {
+      gaussian_step(xc, r, P, jscale, D.temp[j], y);
+      jt = 1;
+    }
+  }
+  apply_walls(y, P);
+  if (y[1] > y[0]) {  // "order the masses" (:470-475) as written: y[1] = y[0]
+    y[1] = y[0];
+  }
+  y[2] = P.log_lc_period;
+  y[6] = fmod(y[6], P.LC_PERIOD);
+  if (!D.logP_ok[chain]) {  // :444 recomputes it every step; it only changes with the state
+    D.logP[chain] = log_prior(xc, P);
+    D.logP_ok[chain] = 1;
+  }
+  D.logPy[j] = log_prior(y, P);
+  D.jump[j] = jmp;
+  D.jtype[j] = jt;
+  D.alpha2[j] = ran2(r);  // drawn after the likelihood calls in the reference; same stream order
+#pragma unroll
+  for (int i = 0; i < kNp; ++i) D.y[(size_t)j * kNp + i] = y[i];
+  D.idum[j] = r.idum;
+  D.idum2[j] = r.idum2;
+  D.iy[j] = r.iy;
+  D.iset[j] = r.iset;
+  D.gset[j] = r.gset;
+  D.cts[j] = r.cts;
+  for (int t = 0; t < NTAB; ++t) D.iv[(size_t)t * P.W + j] = iv[t * kBlk];
+}
+
+// Hastings test and history (:492-546)
+__global__ __launch_bounds__(kBlk) void ds_accept(Params P, Dev D, long long iter) {
+  const int j = blockIdx.x * kBlk + threadIdx.x;
+  if (j >= P.W) return;
+  const int k = (int)(iter - (iter / P.NPAST) * P.NPAST);
+  const int chain = D.idx[j];
+  const double ly = D.logLy[j], lx = D.logL[chain];
+  double* xc = &D.x[(size_t)chain * kNp];
+  const double* yj = &D.y[(size_t)j * kNp];
+  const double H = hbglibc::exp((ly - lx) / D.temp[j] + (D.logPy[j] - D.logP[chain]));
+  if (D.alpha2[j] <= H) {
+    if ((lx / ly <= 0.5) && (iter > 10000) && (j <= 5) && P.log_on) {
+      const int e = atomicAdd(&D.ctr->nev, 1);
+      if (e < kEvCap) {
+        Event& ev = D.ev[e];
+        ev.iter = iter;
+        ev.chain = chain;
+        ev.jtype = D.jtype[j];
+        ev.slot = j;
+        ev.H = H;
+        ev.alpha = D.alpha2[j];
+        ev.tmp = D.temp[j];
+        ev.lx = lx;
+        ev.ly = ly;
+        ev.px = D.logP[chain];
+        ev.py = D.logPy[j];
+        for (int i = 0; i < kNp; ++i) {
+          ev.xo[i] = xc[i];
+          ev.xn[i] = yj[i];
+        }
+      }
+    }
+    if (chain == 0) atomicAdd((unsigned long long*)&D.ctr->acc_it, 1ull);
+#pragma unroll
+    for (int i = 0; i < kNp; ++i) xc[i] = yj[i];
+    D.logL[chain] = ly;
+    D.logP[chain] = D.logPy[j];
+    if ((D.jump[j] == 1) && (chain == 0)) {
+      D.DEacc_arr[j]++;
+      atomicAdd((unsigned long long*)&D.ctr->DEacc_tot, 1ull);
+    }
+  }
+  double* h = &D.hist[((size_t)j * P.NPAST + k) * kNp];
+#pragma unroll
+  for (int i = 0; i < kNp; ++i) h[i] = xc[i];
+}
+
+// index[] accessors: LDS (small W) or device-coherent global (large W)
+template <bool LDS>
+struct IdxRef {
+  int* p;
+  __device__ int ld(int i) const {
+    if (LDS) return p[i];
+    return __hip_atomic_load(p + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __device__ void st(int i, int v) const {
+    if (LDS) p[i] = v;
+    else __hip_atomic_store(p + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+};
+
+// the W tempering attempts (ptmcmc :768-817) in dependency levels, then the
+// per-iteration bookkeeping of :551-572 / :590 / :639-641
+template <bool LDS>
+__global__ __launch_bounds__(kSwapThreads) void ds_swap(Params P, Dev D, const SwapEnt* sched, const int* off,
+                                                         int nlv, long long iter) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  __shared__ int nacc_s;
+  const int W = P.W, tid = threadIdx.x;
+  double* Ls = reinterpret_cast<double*>(smem);
+  IdxRef<LDS> idx{LDS ? reinterpret_cast<int*>(smem + sizeof(double) * (size_t)W) : D.idx};
+  const double* L = LDS ? Ls : D.logL;
+  if (tid == 0) nacc_s = 0;
+  if (LDS) {
+    for (int c = tid; c < W; c += kSwapThreads) {
+      Ls[c] = D.logL[c];
+      idx.st(c, D.idx[c]);
+    }
+  }
+  __syncthreads();
+  int nacc = 0;
+  for (int lv = 0; lv < nlv; ++lv) {
+    const int e1 = off[lv + 1];
+    for (int s = off[lv] + tid; s < e1; s += kSwapThreads) {
+      const int b = sched[s].b, a = b + 1;
+      const double be = sched[s].beta;
+      const int olda = idx.ld(a), oldb = idx.ld(b);
+      const double heat1 = D.temp[a], heat2 = D.temp[b];
+      const double dlogL = L[oldb] - L[olda];
+      const double Hs = (heat2 - heat1) / (heat2 * heat1);
+      const double al = hbglibc::exp(dlogL * Hs);
+      if (al >= be) {
+        idx.st(a, oldb);
+        idx.st(b, olda);
+        ++nacc;
+      }
+    }
+    __syncthreads();
+  }
+  if (nacc) atomicAdd(&nacc_s, nacc);
+  if (LDS)
+    for (int c = tid; c < W; c += kSwapThreads) D.idx[c] = idx.ld(c);
+  __syncthreads();
+  Counters* C = D.ctr;
+  const bool reset = (iter % 100 == 0);
+  if (tid == 0) {
+    C->acc += C->acc_it;  // hb_sampler_accept's sums over the slots
+    C->cold_acc += C->acc_it;
+    C->DEacc += C->DEacc_tot;
+    C->DEtrial += C->DEtrial_tot;
+    C->acc_it = 0;
+    C->nswap += nacc_s;
+    C->snap[0] = C->acc;
+    C->snap[1] = C->DEacc;
+    C->snap[2] = C->DEtrial;
+    C->snap[3] = C->atrial;
+    const int c0 = idx.ld(0);  // :565-572
+    if (D.logL[c0] > C->logLmap) {
+      for (int i = 0; i < kNp; ++i) C->xmap[i] = D.x[(size_t)c0 * kNp + i];
+      C->logLmap = D.logL[c0];
+    }
+    C->atrial++;  // :590 and the 100-step reset of :622-629
+    if (reset) {
+      C->acc = C->atrial = 0;
+      C->DEacc_tot = C->DEtrial_tot = 0;
+    }
+  }
+  if (reset)
+    for (int c = tid; c < W; c += kSwapThreads) D.DEacc_arr[c] = D.DEtrial_arr[c] = 0;
+}
+
+// states and logL by slot (writer / verbose / download)
+__global__ __launch_bounds__(kBlk) void ds_gather(int W, Dev D, double* xs, double* ls, double* ps, int* oks) {
+  const int j = blockIdx.x * kBlk + threadIdx.x;
+  if (j >= W) return;
+  const int c = D.idx[j];
+  for (int i = 0; i < kNp; ++i) xs[(size_t)j * kNp + i] = D.x[(size_t)c * kNp + i];
+  ls[j] = D.logL[c];
+  if (ps) ps[j] = D.logP[c];
+  if (oks) oks[j] = D.logP_ok[c];
+}
+
+// glibc-exact math on the device, for tests (fn 0 exp, 1 log, 2 pow, 3 sqrt, 4 div)
+__global__ void ds_math_probe(int fn, const double* x, const double* y, long n, double* out) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const double a = x[i], b = y[i];
+  out[i] = fn == 0 ? hbglibc::exp(a) : fn == 1 ? hbglibc::log(a) : fn == 2 ? hbglibc::pow(a, b)
+         : fn == 3 ? sqrt(a) : a / b;
+}
+
+}  // namespace hbds
+
+using namespace hbds;
+
+#define DS_TRY(expr, what)                                   \
+  do {                                                       \
+    hipError_t _e = (expr);                                  \
+    if (_e != hipSuccess) {                                  \
+      std::string m = std::string(what) + ": " + hipGetErrorString(_e); \
+      return hbx_set_error(m.c_str());                       \
+    }                                                        \
+  } while (0)
+
+static double now_s() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+struct hb_dsampler {
+  hb_sampler* s = nullptr;
+  hb_ctx* ctx = nullptr;
+  hipStream_t st = nullptr;
+  HbSamplerView v{};
+  Params P{};
+  Dev D{};
+  int W = 0, NPAST = 0, device = 0;
+  bool lds_swap = true;
+  size_t swap_lds = 0;
+  std::vector<void*> allocs;
+  // swap schedules: pinned ring -> one device buffer (stream-ordered)
+  static constexpr int R = 4;
+  unsigned char* pin[R] = {};
+  hipEvent_t ev[R] = {};
+  bool ev_used[R] = {};
+  int ring = 0;
+  unsigned char* d_sched = nullptr;
+  size_t sched_bytes = 0;
+  std::vector<int> b, last, lvl, cnt;
+  std::vector<double> beta;
+  // staging for gathers / counters / events
+  double* d_xs = nullptr;
+  double* d_ls = nullptr;
+  double* d_ps = nullptr;
+  int* d_ok = nullptr;
+  Counters* h_ctr = nullptr;
+  Event* h_ev = nullptr;
+  ~hb_dsampler() {
+    if (st) (void)hipStreamSynchronize(st);
+    for (void* p : allocs) (void)hipFree(p);
+    for (int r = 0; r < R; ++r) {
+      if (pin[r]) (void)hipHostFree(pin[r]);
+      if (ev[r]) (void)hipEventDestroy(ev[r]);
+    }
+    if (h_ctr) (void)hipHostFree(h_ctr);
+    if (h_ev) (void)hipHostFree(h_ev);
+    if (st) (void)hipStreamDestroy(st);
+  }
+  template <class T>
+  hipError_t alloc(T** p, size_t n) {
+    hipError_t e = hipMalloc((void**)p, sizeof(T) * (n ? n : 1));
+    if (e == hipSuccess) allocs.push_back((void*)*p);
+    return e;
+  }
+};
+
+static int ds_upload(hb_dsampler* d);
+
+extern "C" hb_dsampler* hb_dsampler_create(hb_sampler* s, hb_ctx* ctx) {
+  if (!s || !ctx) {
+    hbx_set_error("hb_dsampler_create: null sampler or context");
+    return nullptr;
+  }
+  hb_dsampler* d = new hb_dsampler();
+  d->s = s;
+  d->ctx = ctx;
+  hbx_sampler_view(s, &d->v);
+  const HbSamplerView& v = d->v;
+  if (v.lo != 0 || v.hi != v.W) {
+    hbx_set_error("hb_dsampler_create: the sampler must own every slot (one GPU)");
+    delete d;
+    return nullptr;
+  }
+  d->W = v.W;
+  d->NPAST = v.NPAST;
+  d->device = hbx_ctx_device(ctx);
+  if (hb_reserve(ctx, v.W)) {  // the likelihood workspace, before anything is enqueued
+    delete d;
+    return nullptr;
+  }
+  auto fail = [&](const char* what, hipError_t e) -> hb_dsampler* {
+    std::string m = std::string("hb_dsampler_create: ") + what + ": " + hipGetErrorString(e);
+    hbx_set_error(m.c_str());
+    delete d;
+    return nullptr;
+  };
+  hipError_t e = hipSetDevice(d->device);
+  if (e != hipSuccess) return fail("hipSetDevice", e);
+  if ((e = hipStreamCreateWithFlags(&d->st, hipStreamNonBlocking)) != hipSuccess) return fail("stream", e);
+  const int W = d->W;
+  const size_t Wz = (size_t)W;
+  Dev& D = d->D;
+  if ((e = d->alloc(&D.x, Wz * kNp)) || (e = d->alloc(&D.logL, Wz)) || (e = d->alloc(&D.logP, Wz)) ||
+      (e = d->alloc(&D.logP_ok, Wz)) || (e = d->alloc(&D.idx, Wz)) || (e = d->alloc(&D.temp, Wz)) ||
+      (e = d->alloc(&D.idum, Wz)) || (e = d->alloc(&D.idum2, Wz)) || (e = d->alloc(&D.iy, Wz)) ||
+      (e = d->alloc(&D.iset, Wz)) || (e = d->alloc(&D.gset, Wz)) || (e = d->alloc(&D.cts, Wz)) ||
+      (e = d->alloc(&D.iv, Wz * NTAB)) || (e = d->alloc(&D.y, Wz * kNp)) || (e = d->alloc(&D.logPy, Wz)) ||
+      (e = d->alloc(&D.alpha2, Wz)) || (e = d->alloc(&D.logLy, Wz)) || (e = d->alloc(&D.jump, Wz)) ||
+      (e = d->alloc(&D.jtype, Wz)) || (e = d->alloc(&D.hist, Wz * (size_t)d->NPAST * kNp)) ||
+      (e = d->alloc(&D.DEacc_arr, Wz)) || (e = d->alloc(&D.DEtrial_arr, Wz)) || (e = d->alloc(&D.ctr, 1)) ||
+      (e = d->alloc(&D.ev, (size_t)kEvCap)) || (e = d->alloc(&d->d_xs, Wz * kNp)) ||
+      (e = d->alloc(&d->d_ls, Wz)) || (e = d->alloc(&d->d_ps, Wz)) || (e = d->alloc(&d->d_ok, Wz)))
+    return fail("hipMalloc", e);
+  d->sched_bytes = sizeof(SwapEnt) * Wz + sizeof(int) * (Wz + 2);
+  if ((e = d->alloc(&d->d_sched, d->sched_bytes))) return fail("hipMalloc", e);
+  for (int r = 0; r < hb_dsampler::R; ++r) {
+    if ((e = hipHostMalloc((void**)&d->pin[r], d->sched_bytes, hipHostMallocDefault))) return fail("pinned", e);
+    if ((e = hipEventCreateWithFlags(&d->ev[r], hipEventDisableTiming))) return fail("event", e);
+  }
+  if ((e = hipHostMalloc((void**)&d->h_ctr, sizeof(Counters), hipHostMallocDefault))) return fail("pinned", e);
+  if ((e = hipHostMalloc((void**)&d->h_ev, sizeof(Event) * kEvCap, hipHostMallocDefault))) return fail("pinned", e);
+  d->b.resize(W);
+  d->beta.resize(W);
+  d->last.resize(W + 1);
+  d->lvl.resize(W);
+  d->cnt.resize(W + 2);
+  // index[] + logL by chain in LDS when they fit (160 KB per CU on gfx950)
+  d->swap_lds = (sizeof(double) + sizeof(int)) * Wz;
+  d->lds_swap = d->swap_lds <= 150 * 1024;
+  if (d->lds_swap) {
+    e = hipFuncSetAttribute((const void*)ds_swap<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)d->swap_lds);
+    if (e != hipSuccess) return fail("LDS attribute", e);
+  }
+  Params& P = d->P;
+  P.W = W;
+  P.NPAST = d->NPAST;
+  P.log_on = v.log != nullptr;
+  P.log_lc_period = v.log_lc_period;
+  P.LC_PERIOD = v.LC_PERIOD;
+  for (int i = 0; i < kNp; ++i) {
+    P.lim_lo[i] = v.limits[i].lo;
+    P.lim_hi[i] = v.limits[i].hi;
+    P.fl_lo[i] = v.limited[i].lo;
+    P.fl_hi[i] = v.limited[i].hi;
+    P.sigma_p[i] = v.sigma_p[i];
+    P.gpflag[i] = v.gp[i].flag;
+  }
+  if (ds_upload(d)) {
+    delete d;
+    return nullptr;
+  }
+  return d;
+}
+
+extern "C" void hb_dsampler_destroy(hb_dsampler* d) { delete d; }
+
+// host sampler (by slot) -> device (by chain)
+static int ds_upload(hb_dsampler* d) {
+  const HbSamplerView& v = d->v;
+  const int W = d->W;
+  const size_t Wz = (size_t)W;
+  Dev& D = d->D;
+  std::vector<double> x(Wz * kNp), L(Wz), Pp(Wz), gset(Wz);
+  std::vector<int> ok(Wz), idx(Wz), idum(Wz), idum2(Wz), iy(Wz), iset(Wz), iv(Wz * NTAB);
+  std::vector<long long> cts(Wz);
+  for (int j = 0; j < W; ++j) {
+    const int c = v.cid[j];
+    idx[j] = c;
+    memcpy(&x[(size_t)c * kNp], &v.x[(size_t)j * kNp], sizeof(double) * kNp);
+    L[c] = v.logL[j];
+    Pp[c] = v.logP[j];
+    ok[c] = v.logP_ok[j] ? 1 : 0;
+    const RNG_Vars& r = v.states[j];
+    if (v.seeds[j] > 2147483647L || v.seeds[j] < -2147483647L) return hbx_set_error("hb_dsampler: seed out of range");
+    idum[j] = (int)v.seeds[j];
+    idum2[j] = (int)r.idum2;
+    iy[j] = (int)r.iy;
+    iset[j] = r.iset;
+    gset[j] = r.gset;
+    cts[j] = r.cts;
+    for (int t = 0; t < NTAB; ++t) iv[(size_t)t * W + j] = (int)r.iv[t];
+  }
+  Counters c{};
+  c.acc = *v.acc;
+  c.DEacc = *v.DEacc;
+  c.DEtrial = *v.DEtrial;
+  c.atrial = *v.atrial;
+  c.cold_acc = *v.cold_acc;
+  c.nswap = *v.nswap;
+  for (int j = 0; j < W; ++j) {
+    c.DEacc_tot += v.DEacc_arr[j];
+    c.DEtrial_tot += v.DEtrial_arr[j];
+    c.acc_it += v.acc_arr[j];
+  }
+  c.logLmap = -1.0 / 0.0;
+  hipStream_t s = d->st;
+  DS_TRY(hipSetDevice(d->device), "hipSetDevice");
+  DS_TRY(hipMemcpyAsync(D.x, x.data(), sizeof(double) * x.size(), hipMemcpyHostToDevice, s), "upload");
+  DS_TRY(hipMemcpyAsync(D.logL, L.data(), sizeof(double) * Wz, hipMemcpyHostToDevice, s), "upload");
+  DS_TRY(hipMemcpyAsync(D.logP, Pp.data(), sizeof(double) * Wz, hipMemcpyHostToDevice, s), "upload");
+  DS_TRY(hipMemcpyAsync(D.logP_ok, ok.data(), sizeof(int) * Wz, hipMemcpyHostToDevice, s), "upload");
+  DS_TRY(hipMemcpyAsync(D.idx, idx.data(), sizeof(int) * Wz, hipMemcpyHostToDevice, s), "upload");
+  DS_TRY(hipMemcpyAsync(D.temp, v.temp, sizeof(double) * Wz, hipMemcpyHostToDevice, s), "upload");
+  DS_TRY(hipMemcpyAsync(D.idum, idum.data(), sizeof(int) * Wz, hipMemcpyHostToDevice, s), "upload");
+  DS_TRY(hipMemcpyAsync(D.idum2, idum2.data(), sizeof(int) * Wz, hipMemcpyHostToDevice, s), "upload");
+  DS_TRY(hipMemcpyAsync(D.iy, iy.data(), sizeof(int) * Wz, hipMemcpyHostToDevice, s), "upload");
+  DS_TRY(hipMemcpyAsync(D.iset, iset.data(), sizeof(int) * Wz, hipMemcpyHostToDevice, s), "upload");
+  DS_TRY(hipMemcpyAsync(D.gset, gset.data(), sizeof(double) * Wz, hipMemcpyHostToDevice, s), "upload");
+  DS_TRY(hipMemcpyAsync(D.cts, cts.data(), sizeof(long long) * Wz, hipMemcpyHostToDevice, s), "upload");
+  DS_TRY(hipMemcpyAsync(D.iv, iv.data(), sizeof(int) * iv.size(), hipMemcpyHostToDevice, s), "upload");
+  DS_TRY(hipMemcpyAsync(D.hist, v.hist, sizeof(double) * Wz * d->NPAST * kNp, hipMemcpyHostToDevice, s),
+         "upload");
+  DS_TRY(hipMemcpyAsync(D.DEacc_arr, v.DEacc_arr, sizeof(int) * Wz, hipMemcpyHostToDevice, s), "upload");
+  DS_TRY(hipMemcpyAsync(D.DEtrial_arr, v.DEtrial_arr, sizeof(int) * Wz, hipMemcpyHostToDevice, s), "upload");
+  DS_TRY(hipMemcpyAsync(D.ctr, &c, sizeof c, hipMemcpyHostToDevice, s), "upload");
+  DS_TRY(hipStreamSynchronize(s), "upload sync");
+  return 0;
+}
+
+// device -> host sampler (by slot); also drains the big-jump records
+static int ds_drain_events(hb_dsampler* d);
+
+extern "C" int hb_dsampler_download(hb_dsampler* d) {
+  if (!d) return hbx_set_error("hb_dsampler_download: null");
+  const HbSamplerView& v = d->v;
+  const int W = d->W;
+  const size_t Wz = (size_t)W;
+  Dev& D = d->D;
+  hipStream_t s = d->st;
+  DS_TRY(hipSetDevice(d->device), "hipSetDevice");
+  ds_gather<<<(W + kBlk - 1) / kBlk, kBlk, 0, s>>>(W, D, d->d_xs, d->d_ls, d->d_ps, d->d_ok);
+  DS_TRY(hipGetLastError(), "gather");
+  std::vector<int> idx(Wz), ok(Wz), idum(Wz), idum2(Wz), iy(Wz), iset(Wz), iv(Wz * NTAB);
+  std::vector<double> gset(Wz);
+  std::vector<long long> cts(Wz);
+  DS_TRY(hipMemcpyAsync(v.x, d->d_xs, sizeof(double) * Wz * kNp, hipMemcpyDeviceToHost, s), "download");
+  DS_TRY(hipMemcpyAsync(v.logL, d->d_ls, sizeof(double) * Wz, hipMemcpyDeviceToHost, s), "download");
+  DS_TRY(hipMemcpyAsync(v.logP, d->d_ps, sizeof(double) * Wz, hipMemcpyDeviceToHost, s), "download");
+  DS_TRY(hipMemcpyAsync(ok.data(), d->d_ok, sizeof(int) * Wz, hipMemcpyDeviceToHost, s), "download");
+  DS_TRY(hipMemcpyAsync(idx.data(), D.idx, sizeof(int) * Wz, hipMemcpyDeviceToHost, s), "download");
+  DS_TRY(hipMemcpyAsync(idum.data(), D.idum, sizeof(int) * Wz, hipMemcpyDeviceToHost, s), "download");
+  DS_TRY(hipMemcpyAsync(idum2.data(), D.idum2, sizeof(int) * Wz, hipMemcpyDeviceToHost, s), "download");
+  DS_TRY(hipMemcpyAsync(iy.data(), D.iy, sizeof(int) * Wz, hipMemcpyDeviceToHost, s), "download");
+  DS_TRY(hipMemcpyAsync(iset.data(), D.iset, sizeof(int) * Wz, hipMemcpyDeviceToHost, s), "download");
+  DS_TRY(hipMemcpyAsync(gset.data(), D.gset, sizeof(double) * Wz, hipMemcpyDeviceToHost, s), "download");
+  DS_TRY(hipMemcpyAsync(cts.data(), D.cts, sizeof(long long) * Wz, hipMemcpyDeviceToHost, s), "download");
+  DS_TRY(hipMemcpyAsync(iv.data(), D.iv, sizeof(int) * iv.size(), hipMemcpyDeviceToHost, s), "download");
+  DS_TRY(hipMemcpyAsync(v.hist, D.hist, sizeof(double) * Wz * d->NPAST * kNp, hipMemcpyDeviceToHost, s),
+         "download");
+  DS_TRY(hipMemcpyAsync(v.DEacc_arr, D.DEacc_arr, sizeof(int) * Wz, hipMemcpyDeviceToHost, s), "download");
+  DS_TRY(hipMemcpyAsync(v.DEtrial_arr, D.DEtrial_arr, sizeof(int) * Wz, hipMemcpyDeviceToHost, s), "download");
+  DS_TRY(hipMemcpyAsync(d->h_ctr, D.ctr, sizeof(Counters), hipMemcpyDeviceToHost, s), "download");
+  DS_TRY(hipStreamSynchronize(s), "download sync");
+  for (int j = 0; j < W; ++j) {
+    v.cid[j] = idx[j];
+    v.logP_ok[j] = (char)ok[j];
+    v.seeds[j] = idum[j];
+    RNG_Vars& r = v.states[j];
+    r.idum2 = idum2[j];
+    r.iy = iy[j];
+    r.iset = iset[j];
+    r.gset = gset[j];
+    r.cts = cts[j];
+    for (int t = 0; t < NTAB; ++t) r.iv[t] = iv[(size_t)t * W + j];
+    v.acc_arr[j] = 0;  // cleared by every accept step (hb_sampler_accept)
+  }
+  const Counters& c = *d->h_ctr;
+  *v.acc = c.acc;
+  *v.DEacc = c.DEacc;
+  *v.DEtrial = c.DEtrial;
+  *v.atrial = c.atrial;
+  *v.cold_acc = c.cold_acc;
+  *v.nswap = c.nswap;
+  return ds_drain_events(d);
+}
+
+static int ds_drain_events(hb_dsampler* d) {
+  DS_TRY(hipMemcpyAsync(d->h_ctr, d->D.ctr, sizeof(Counters), hipMemcpyDeviceToHost, d->st), "events");
+  DS_TRY(hipStreamSynchronize(d->st), "events");
+  const int n = std::min(d->h_ctr->nev, kEvCap);
+  if (d->h_ctr->nev > kEvCap) return hbx_set_error("hb_dsampler: big-jump record buffer overflowed");
+  if (n == 0) return 0;
+  DS_TRY(hipMemcpyAsync(d->h_ev, d->D.ev, sizeof(Event) * n, hipMemcpyDeviceToHost, d->st), "events");
+  const int zero = 0;
+  DS_TRY(hipMemcpyAsync(&d->D.ctr->nev, &zero, sizeof(int), hipMemcpyHostToDevice, d->st), "events");
+  DS_TRY(hipStreamSynchronize(d->st), "events");
+  std::vector<Event> evs(d->h_ev, d->h_ev + n);
+  // the host sampler logs in slot order within an iteration (slots 0..5)
+  std::stable_sort(evs.begin(), evs.end(), [](const Event& a, const Event& b) {
+    return a.iter != b.iter ? a.iter < b.iter : a.slot < b.slot;
+  });
+  for (const Event& e : evs)
+    hbx_log_big_jump(d->v.log, (long)e.iter, e.chain, e.H, e.alpha, e.tmp, e.lx, e.ly, e.px, e.py, e.xo, e.xn,
+                     e.jtype);
+  return 0;
+}
+
+// iteration-0 recompute (:488): logL of every current state, and the MAP
+// tracker seeded with chain 0's state (:342)
+extern "C" int hb_dsampler_init_logl(hb_dsampler* d) {
+  if (!d) return hbx_set_error("hb_dsampler_init_logl: null");
+  DS_TRY(hipSetDevice(d->device), "hipSetDevice");
+  const int rc = hb_loglik_batch_dev(d->ctx, d->D.x, d->W, d->D.logL, (void*)d->st);
+  if (rc) return rc;
+  // logLmap = logL(x of chain 0), xmap = x of chain 0
+  DS_TRY(hipMemcpyAsync(&d->D.ctr->logLmap, d->D.logL, sizeof(double), hipMemcpyDeviceToDevice, d->st), "map");
+  DS_TRY(hipMemcpyAsync(d->D.ctr->xmap, d->D.x, sizeof(double) * kNp, hipMemcpyDeviceToDevice, d->st), "map");
+  return 0;
+}
+
+// one iteration, enqueued on the sampler's stream (no host wait)
+extern "C" int hb_dsampler_step(hb_dsampler* d, long iter) {
+  if (!d) return hbx_set_error("hb_dsampler_step: null");
+  const int W = d->W;
+  const Params& P = d->P;
+  const Dev& D = d->D;
+  hipStream_t s = d->st;
+  DS_TRY(hipSetDevice(d->device), "hipSetDevice");
+  // swap schedule of this iteration (draws in the reference's order)
+  hbx_swap_draws(d->s, d->b.data(), d->beta.data());
+  std::fill(d->last.begin(), d->last.end(), 0);
+  int nlv = 0;
+  for (int i = 0; i < W; ++i) {
+    const int b = d->b[i];
+    if (b < 0 || b + 1 >= W) {  // rand() == RAND_MAX: the reference reads index[NCHAINS]; no swap here
+      d->lvl[i] = -1;
+      continue;
+    }
+    const int l = std::max(d->last[b], d->last[b + 1]) + 1;
+    d->lvl[i] = l;
+    d->last[b] = d->last[b + 1] = l;
+    nlv = std::max(nlv, l);
+  }
+  const int r = d->ring;
+  d->ring = (d->ring + 1) % hb_dsampler::R;
+  if (d->ev_used[r]) DS_TRY(hipEventSynchronize(d->ev[r]), "schedule ring");
+  SwapEnt* ent = reinterpret_cast<SwapEnt*>(d->pin[r]);
+  int* off = reinterpret_cast<int*>(d->pin[r] + sizeof(SwapEnt) * (size_t)W);
+  std::fill(d->cnt.begin(), d->cnt.begin() + nlv + 2, 0);
+  for (int i = 0; i < W; ++i)
+    if (d->lvl[i] > 0) d->cnt[d->lvl[i]]++;
+  off[0] = 0;
+  for (int l = 1; l <= nlv; ++l) off[l] = off[l - 1] + d->cnt[l];
+  for (int l = 0; l <= nlv; ++l) d->cnt[l] = off[l];  // next free entry of level l+1 at cnt[l]
+  for (int i = 0; i < W; ++i) {
+    const int l = d->lvl[i];
+    if (l <= 0) continue;
+    SwapEnt& e = ent[d->cnt[l - 1]++];
+    e.b = d->b[i];
+    e.pad = 0;
+    e.beta = d->beta[i];
+  }
+  DS_TRY(hipMemcpyAsync(d->d_sched, d->pin[r], d->sched_bytes, hipMemcpyHostToDevice, s), "schedule upload");
+  DS_TRY(hipEventRecord(d->ev[r], s), "schedule ring");
+  d->ev_used[r] = true;
+  const SwapEnt* d_ent = reinterpret_cast<const SwapEnt*>(d->d_sched);
+  const int* d_off = reinterpret_cast<const int*>(d->d_sched + sizeof(SwapEnt) * (size_t)W);
+
+  const int nb = (W + kBlk - 1) / kBlk;
+  ds_propose<<<nb, kBlk, 0, s>>>(P, D, (long long)iter);
+  DS_TRY(hipGetLastError(), "ds_propose");
+  const int rc = hb_loglik_batch_dev(d->ctx, D.y, W, D.logLy, (void*)s);
+  if (rc) return rc;
+  ds_accept<<<nb, kBlk, 0, s>>>(P, D, (long long)iter);
+  DS_TRY(hipGetLastError(), "ds_accept");
+  if (d->lds_swap)
+    ds_swap<true><<<1, kSwapThreads, d->swap_lds, s>>>(P, D, d_ent, d_off, nlv, (long long)iter);
+  else
+    ds_swap<false><<<1, kSwapThreads, 0, s>>>(P, D, d_ent, d_off, nlv, (long long)iter);
+  DS_TRY(hipGetLastError(), "ds_swap");
+  if (P.log_on && iter > 10000 && iter % 100 == 0) return ds_drain_events(d);
+  return 0;
+}
+
+// states / logL by slot after the last step, the MAP tracker and the
+// counters as :577-579 print them; synchronises
+extern "C" int hb_dsampler_gather(hb_dsampler* d, double* x_slots, double* logl_slots, double* xmap,
+                                  double* logLmap, long* stats4) {
+  if (!d) return hbx_set_error("hb_dsampler_gather: null");
+  const int W = d->W;
+  hipStream_t s = d->st;
+  DS_TRY(hipSetDevice(d->device), "hipSetDevice");
+  ds_gather<<<(W + kBlk - 1) / kBlk, kBlk, 0, s>>>(W, d->D, d->d_xs, d->d_ls, nullptr, nullptr);
+  DS_TRY(hipGetLastError(), "gather");
+  if (x_slots)
+    DS_TRY(hipMemcpyAsync(x_slots, d->d_xs, sizeof(double) * W * kNp, hipMemcpyDeviceToHost, s), "gather");
+  if (logl_slots)
+    DS_TRY(hipMemcpyAsync(logl_slots, d->d_ls, sizeof(double) * W, hipMemcpyDeviceToHost, s), "gather");
+  DS_TRY(hipMemcpyAsync(d->h_ctr, d->D.ctr, sizeof(Counters), hipMemcpyDeviceToHost, s), "gather");
+  DS_TRY(hipStreamSynchronize(s), "gather");
+  if (xmap) memcpy(xmap, d->h_ctr->xmap, sizeof(double) * kNp);
+  if (logLmap) *logLmap = d->h_ctr->logLmap;
+  if (stats4)
+    for (int i = 0; i < 4; ++i) stats4[i] = (long)d->h_ctr->snap[i];
+  return 0;
+}
+
+extern "C" int hb_dsampler_sync(hb_dsampler* d) {
+  if (!d) return hbx_set_error("hb_dsampler_sync: null");
+  DS_TRY(hipStreamSynchronize(d->st), "sync");
+  return 0;
+}
+
+// glibc-exact device math, for tests
+extern "C" int hb_glibc_eval(int fn, const double* x, const double* y, long n, double* out) {
+  if (n <= 0) return 0;
+  double *dx = nullptr, *dy = nullptr, *dout = nullptr;
+  const size_t bytes = sizeof(double) * (size_t)n;
+  DS_TRY(hipMalloc((void**)&dx, bytes), "hipMalloc");
+  DS_TRY(hipMalloc((void**)&dy, bytes), "hipMalloc");
+  DS_TRY(hipMalloc((void**)&dout, bytes), "hipMalloc");
+  hipError_t e = hipMemcpy(dx, x, bytes, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(dy, y, bytes, hipMemcpyHostToDevice);
+  if (e == hipSuccess) {
+    ds_math_probe<<<(unsigned)((n + 255) / 256), 256>>>(fn, dx, dy, n, dout);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) e = hipMemcpy(out, dout, bytes, hipMemcpyDeviceToHost);
+  (void)hipFree(dx);
+  (void)hipFree(dy);
+  (void)hipFree(dout);
+  DS_TRY(e, "hb_glibc_eval");
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
+// hb_mcmc_run on the device: the mcmc_wrapper2.c loop with every iteration
+// enqueued without a host round trip; the host joins every 100 iterations
+// for the reference's file writes (:593-649) and progress lines (:575-589).
+// ---------------------------------------------------------------------------
+extern "C" int hb_mcmc_run_device(const hb_mcmc_cfg* cfg, hb_ctx* ctx, const double* t, const double* flux,
+                                  long n, hb_mcmc_result* res) {
+  if (!cfg || !ctx || cfg->nchains < 2 || cfg->npast < 2) return hbx_set_error("hb_mcmc_run_device: bad config");
+  if (cfg->ladder == 0 && cfg->nchains > 2000) return hbx_set_error("hb_mcmc_run_device: ladder 0 needs W <= 2000");
+  const int W = cfg->nchains;
+  const long NITER = cfg->niter;
+  hb_sampler* s = hb_sampler_create(cfg, 0, W);
+  if (!s) return hbx_set_error("hb_mcmc_run_device: sampler");
+  hb_writer* wr = nullptr;
+  if (cfg->out_root && cfg->out_root[0]) {
+    wr = hb_writer_open(cfg->out_root, cfg->run_id, cfg->run, W);
+    if (!wr) {
+      hb_sampler_destroy(s);
+      return hbx_set_error("hb_mcmc_run_device: cannot open output files");
+    }
+    hb_sampler_attach_log(s, wr);
+  }
+  hb_dsampler* d = hb_dsampler_create(s, ctx);
+  int rc = d ? 0 : -1;
+  std::vector<double> xs((size_t)W * kNp), ls(W), model(n > 0 ? n : 1), xmap(kNp);
+  double logLmap = 0;
+  long st4[4];
+  const double t_start = now_s();
+  if (!rc) rc = hb_dsampler_init_logl(d);
+  if (!rc && cfg->verbose) {
+    rc = hb_dsampler_gather(d, nullptr, nullptr, xmap.data(), &logLmap, nullptr);
+    if (!rc) printf("initial chi2 and likelihood %lf \t %lf\n", -2 * logLmap, logLmap);
+  }
+  for (long iter = 0; iter < NITER && !rc; ++iter) {
+    rc = hb_dsampler_step(d, iter);
+    if (rc) break;
+    const bool show = cfg->verbose && iter % 1000 == 0;
+    const bool write = wr && iter % 100 == 0;
+    if (!(show || write)) continue;
+    rc = hb_dsampler_gather(d, xs.data(), ls.data(), xmap.data(), &logLmap, st4);
+    if (rc) break;
+    if (show) {  // :575-589
+      printf("%ld/%ld logL=%.10g acc=%.3g DEacc=%.3g", iter, NITER, ls[0], (double)st4[0] / ((double)st4[3]),
+             (double)st4[1] / (double)st4[2]);
+      printf("\n");
+      printf("Parameter values: \n");
+      for (int i = 0; i < 5; ++i) printf("%lf\t", xs[(size_t)(W > 10 ? 10 : W - 1) * kNp + i]);
+      printf("\n");
+    }
+    if (write) {  // :593-649
+      hb_writer_step(wr, iter, ls.data(), xs.data());
+      if (n > 0 && t && flux) {
+        rc = hb_light_curve_batch(ctx, xmap.data(), 1, model.data(), nullptr);
+        if (rc) break;
+        hb_writer_lc(wr, t, flux, model.data(), n);
+      }
+      hb_writer_pars(wr, 0, xs.data());
+    }
+  }
+  if (!rc) rc = hb_dsampler_gather(d, xs.data(), ls.data(), xmap.data(), &logLmap, nullptr);
+  if (!rc) rc = hb_dsampler_download(d);
+  if (!rc && wr) {  // :655-681
+    if (n > 0 && t && flux) {
+      rc = hb_light_curve_batch(ctx, xmap.data(), 1, model.data(), nullptr);
+      if (!rc) hb_writer_lc(wr, t, flux, model.data(), n);
+    }
+    hb_writer_pars(wr, 1, xs.data());
+  }
+  if (!rc && res) {
+    long st6[6];
+    hb_sampler_stats(s, st6);
+    memcpy(res->xmap, xmap.data(), sizeof(double) * kNp);
+    res->logLmap = logLmap;
+    res->accepted = st6[4];
+    res->swaps = st6[5];
+    res->seconds_total = now_s() - t_start;
+    res->seconds_loglik = -1.0;  // not separable: the likelihood runs inside the device loop
+    res->loglik_evals = (long)W * (NITER + 1);
+  }
+  hb_dsampler_destroy(d);
+  if (wr) hb_writer_close(wr);
+  hb_sampler_destroy(s);
+  return rc;
+}

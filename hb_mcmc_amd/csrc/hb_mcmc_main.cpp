@@ -8,6 +8,7 @@
 //   data/{chains,logL,log,pars,subpars}, data/lightcurves/mcmc_lightcurves,
 //   debug/temp_<j>_log.txt                              (outputs)
 // Extra options: --chains W --npast K --ladder 0|1 --threads T --device D --quiet
+//   --device-sampler: the whole iteration on the GPU (hb_mcmc_run_device)
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -47,6 +48,7 @@ int main(int argc, char** argv) {
   cfg.npast = 500;    // NPAST, mcmc_wrapper2.h:12
   cfg.verbose = 1;
   int device = 0;
+  bool device_sampler = false;
   const char* envroot = getenv("HB_MCMC_ROOT");
   std::string root = envroot ? envroot : ".";
   for (int i = 5; i < argc; ++i) {
@@ -59,11 +61,14 @@ int main(int argc, char** argv) {
     else if (a == "--threads") cfg.nthreads = atoi(next());
     else if (a == "--device") device = atoi(next());
     else if (a == "--quiet") cfg.verbose = 0;
+    else if (a == "--device-sampler") device_sampler = true;
     else { fprintf(stderr, "unknown option %s\n", a.c_str()); return 2; }
   }
   cfg.out_root = root.c_str();
   cfg.run_id = run_id.c_str();
-  if (cfg.verbose) printf("Using libhbmi (GPU batched likelihood, %d chains)\n", cfg.nchains);
+  if (cfg.verbose)
+    printf("Using libhbmi (GPU batched likelihood, %s, %d chains)\n",
+           device_sampler ? "device-resident sampler" : "host sampler", cfg.nchains);
 
   const std::string dfname = root + "/data/lightcurves/folded_lightcurves/" + run_id + "_new.txt";
   const std::string magname = root + "/data/magnitudes/" + run_id + ".txt";
@@ -97,7 +102,8 @@ int main(int argc, char** argv) {
   if (!c.ctx) { fprintf(stderr, "hb_create: %s\n", hb_last_error()); return 1; }
   hb_reserve(c.ctx, cfg.nchains);
   hb_mcmc_result res;
-  const int rc = hb_mcmc_run(&cfg, t.data(), f.data(), e.data(), nt, cb_loglik, cb_model, &c, &res);
+  const int rc = device_sampler ? hb_mcmc_run_device(&cfg, c.ctx, t.data(), f.data(), nt, &res)
+                                : hb_mcmc_run(&cfg, t.data(), f.data(), e.data(), nt, cb_loglik, cb_model, &c, &res);
   hb_destroy(c.ctx);
   if (rc != 0) { fprintf(stderr, "hb_mcmc_run failed (%d): %s\n", rc, hb_last_error()); return 1; }
   if (cfg.verbose)

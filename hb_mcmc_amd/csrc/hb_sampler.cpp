@@ -31,6 +31,7 @@
 
 #include "../../include/hb_sampler.h"
 #include "../../include/hbmi.h"
+#include "hb_sampler_view.hpp"
 
 namespace {
 
@@ -671,11 +672,14 @@ extern "C" int hb_sampler_swap(hb_sampler* s, const double* logl_all, int* perm_
   for (int i = 0; i < W; ++i) {
     const int b = (int)(((double)s->rng.rand() / (RAND_MAX)) * ((double)(W - 1)));
     const int a = b + 1;
+    const double be = ((double)s->rng.rand() / (RAND_MAX));
+    // rand() == RAND_MAX gives b = W-1: the reference then reads index[NCHAINS]
+    // out of bounds (:791-797); here that attempt is void (draws consumed)
+    if (a >= W) continue;
     const double heat1 = s->temp[a], heat2 = s->temp[b];
     const double dlogL = L[b] - L[a];
     const double Hs = (heat2 - heat1) / (heat2 * heat1);
     const double al = exp(dlogL * Hs);
-    const double be = ((double)s->rng.rand() / (RAND_MAX));
     if (al >= be) {
       std::swap(p[a], p[b]);
       std::swap(L[a], L[b]);
@@ -739,6 +743,14 @@ extern "C" int hb_sampler_stats(const hb_sampler* s, long* out6) {
   return 0;
 }
 
+extern "C" int hb_sampler_export(const hb_sampler* s, long* seeds, void* states, double* hist) {
+  if (!s) return -1;
+  if (seeds) memcpy(seeds, s->seeds.data(), sizeof(long) * s->nl);
+  if (states) memcpy(states, s->states.data(), sizeof(RNG_Vars) * s->nl);
+  if (hist) memcpy(hist, s->hist.data(), sizeof(double) * s->hist.size());
+  return 0;
+}
+
 extern "C" int hb_sampler_end_iter(hb_sampler* s, long iter) {
   if (!s) return -1;
   s->atrial++;
@@ -747,6 +759,63 @@ extern "C" int hb_sampler_end_iter(hb_sampler* s, long iter) {
     for (int jl = 0; jl < s->nl; ++jl) s->DEtrial_arr[jl] = s->DEacc_arr[jl] = s->acc_arr[jl] = 0;
   }
   return 0;
+}
+
+// ---------------------------------------------------------------------------
+// Internal bridge for the device-resident sampler (hb_dsampler.hip).
+// ---------------------------------------------------------------------------
+extern "C" int hbx_sampler_view(hb_sampler* s, HbSamplerView* v) {
+  if (!s || !v) return -1;
+  v->W = s->W;
+  v->NPAST = s->NPAST;
+  v->lo = s->lo;
+  v->hi = s->hi;
+  v->nl = s->nl;
+  v->NITER = s->NITER;
+  v->log_lc_period = s->log_lc_period;
+  v->LC_PERIOD = s->LC_PERIOD;
+  v->limited = s->pr.limited;
+  v->limits = s->pr.limits;
+  v->gp = s->pr.gp;
+  v->sigma_p = s->sigma_p;
+  v->temp = s->temp.data();
+  v->seeds = s->seeds.data();
+  v->states = s->states.data();
+  v->x = s->x.data();
+  v->logL = s->logL.data();
+  v->logP = s->logP.data();
+  v->logP_ok = s->logP_ok.data();
+  v->cid = s->cid.data();
+  v->hist = s->hist.data();
+  v->acc_arr = s->acc_arr.data();
+  v->DEacc_arr = s->DEacc_arr.data();
+  v->DEtrial_arr = s->DEtrial_arr.data();
+  v->acc = &s->acc;
+  v->DEacc = &s->DEacc;
+  v->DEtrial = &s->DEtrial;
+  v->atrial = &s->atrial;
+  v->cold_acc = &s->cold_acc;
+  v->nswap = &s->nswap;
+  v->log = s->log;
+  return 0;
+}
+
+extern "C" int hbx_swap_draws(hb_sampler* s, int* b, double* beta) {
+  if (!s) return -1;
+  const int W = s->W;
+  for (int i = 0; i < W; ++i) {  // same expressions as hb_sampler_swap / ptmcmc :791, :810
+    b[i] = (int)(((double)s->rng.rand() / (RAND_MAX)) * ((double)(W - 1)));
+    beta[i] = ((double)s->rng.rand() / (RAND_MAX));
+  }
+  return 0;
+}
+
+extern "C" void hbx_log_big_jump(hb_writer* w, long iter, int chain_id, double H, double alpha, double tmp,
+                                 double lx, double ly, double px, double py, const double* xo, const double* xn,
+                                 int jump_type) {
+  if (!w) return;
+  std::lock_guard<std::mutex> lk(w->mu);
+  log_big_jump(w->files.log, iter, chain_id, H, alpha, tmp, lx, ly, px, py, xo, xn, jump_type);
 }
 
 // ---------------------------------------------------------------------------

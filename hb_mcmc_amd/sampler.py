@@ -59,6 +59,16 @@ def _declare(lib):
             ("hb_sampler_apply_perm", C.c_int, [vp, pi, pd]),
             ("hb_sampler_stats", C.c_int, [vp, C.POINTER(C.c_long)]),
             ("hb_sampler_end_iter", C.c_int, [vp, C.c_long]),
+            ("hb_sampler_export", C.c_int, [vp, C.POINTER(C.c_long), vp, pd]),
+            ("hb_dsampler_create", vp, [vp, vp]),
+            ("hb_dsampler_destroy", None, [vp]),
+            ("hb_dsampler_init_logl", C.c_int, [vp]),
+            ("hb_dsampler_step", C.c_int, [vp, C.c_long]),
+            ("hb_dsampler_gather", C.c_int, [vp, pd, pd, pd, pd, C.POINTER(C.c_long)]),
+            ("hb_dsampler_sync", C.c_int, [vp]),
+            ("hb_dsampler_download", C.c_int, [vp]),
+            ("hb_mcmc_run_device", C.c_int, [C.POINTER(MCMCConfig), vp, pd, pd, C.c_long, C.POINTER(MCMCResult)]),
+            ("hb_glibc_eval", C.c_int, [C.c_int, pd, pd, C.c_long, pd]),
             ("hb_writer_open", vp, [C.c_char_p, C.c_char_p, C.c_int, C.c_int]),
             ("hb_writer_step", C.c_int, [vp, C.c_long, pd, pd]),
             ("hb_writer_lc", C.c_int, [vp, pd, pd, pd, C.c_long]),
@@ -71,6 +81,7 @@ def _declare(lib):
 
 
 REC = 23  # HB_SAMPLER_REC: x[21], logL, chain id
+RNG_VARS_BYTES = 8 * 34 + 8 + 8 + 8  # struct RNG_Vars: idum2, iy, iv[32], iset (+pad), gset, cts
 
 
 def _pd(a):
@@ -150,6 +161,15 @@ class SlotSampler:
 
     def end_iter(self, it):
         _ok(self.lib.hb_sampler_end_iter(self._h, int(it)), "hb_sampler_end_iter")
+
+    def state_arrays(self):
+        """RNG streams (seeds, raw RNG_Vars records) and history of the owned slots."""
+        seeds = np.empty(self.nl, dtype=np.int64)
+        states = np.empty((self.nl, RNG_VARS_BYTES), dtype=np.uint8)
+        hist = np.empty((self.nl, self.cfg.npast, 21))
+        _ok(self.lib.hb_sampler_export(self._h, seeds.ctypes.data_as(C.POINTER(C.c_long)),
+                                       states.ctypes.data_as(C.c_void_p), _pd(hist)), "hb_sampler_export")
+        return {"seeds": seeds, "rng_states": states, "history": hist}
 
 
 class Writer:

@@ -92,6 +92,40 @@ int hb_writer_lc(hb_writer *w, const double *t, const double *flux, const double
 int hb_writer_pars(hb_writer *w, int final_par, const double *x);
 void hb_writer_close(hb_writer *w);
 
+/* RNG streams and history of the owned slots, for state comparisons:
+ * seeds[nl] (ran2 idum), states[nl] (struct RNG_Vars), hist[nl x npast x 21];
+ * NULL skips. */
+int hb_sampler_export(const hb_sampler *s, long *seeds, void *states, double *hist);
+
+/* ---- Device-resident sampler (hb_dsampler.hip): the same iteration with
+ * proposals, walls, priors, the batched likelihood, the Hastings test, the
+ * history and the tempering swaps as kernels on one stream of the context's
+ * GPU, bit-identical to the host loop (glibc-exact exp/log/pow on the device,
+ * the rand()-driven swap attempts drawn by the host ahead of time and
+ * replayed in dependency levels).  Starts from, and hands back to, a host
+ * sampler that owns every slot (slot_lo = 0, slot_hi = nchains). */
+struct hb_ctx;
+typedef struct hb_dsampler hb_dsampler;
+hb_dsampler *hb_dsampler_create(hb_sampler *s, struct hb_ctx *ctx);
+void hb_dsampler_destroy(hb_dsampler *d);
+/* iteration-0 recompute (mcmc_wrapper2.c:488): logL of every current state */
+int hb_dsampler_init_logl(hb_dsampler *d);
+/* one iteration, enqueued without waiting for the GPU */
+int hb_dsampler_step(hb_dsampler *d, long iter);
+/* states/logL by slot, MAP tracker and {acc, DEacc, DEtrial, atrial} as of
+ * the last step; synchronises.  NULL skips. */
+int hb_dsampler_gather(hb_dsampler *d, double *x_slots, double *logl_slots, double *xmap, double *logLmap,
+                       long *stats4);
+int hb_dsampler_sync(hb_dsampler *d);
+/* copies the whole device state back into the host sampler */
+int hb_dsampler_download(hb_dsampler *d);
+/* hb_mcmc_run with the device-resident loop; the light curve and magnitude
+ * data come from ctx (t, flux: host copies for the .out file) */
+int hb_mcmc_run_device(const hb_mcmc_cfg *cfg, struct hb_ctx *ctx, const double *t, const double *flux, long n,
+                       hb_mcmc_result *result);
+/* test hook: fn 0 exp, 1 log, 2 pow(x, y), 3 sqrt, 4 x / y evaluated on the GPU */
+int hb_glibc_eval(int fn, const double *x, const double *y, long n, double *out);
+
 /* The reference's random streams, exposed for tests (mcmc_wrapper2.c:894-974). */
 double hb_ran2_parallel(long *idum, void *rng_state /* struct RNG_Vars */);
 double hb_gasdev2_parallel(long *idum, void *rng_state);

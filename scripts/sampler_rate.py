@@ -25,6 +25,7 @@ ap.add_argument("--walkers", type=int, default=4096)
 ap.add_argument("--ncad", type=int, default=1024)
 ap.add_argument("--iters", type=int, default=200)
 ap.add_argument("--threads", type=int, default=16)
+ap.add_argument("--device", action="store_true", help="device-resident sampler (hb_dsampler_*)")
 a = ap.parse_args()
 
 n, W = a.ncad, a.walkers
@@ -36,6 +37,27 @@ f = truth + s * synth.noise(n)
 L = HBLikelihood(t, f, s)
 L.reserve(W)
 S = SlotSampler(a.iters, W, synth.THETA_STAR[2], 0, W, run=0, npast=500, ladder=1, nthreads=a.threads)
+if a.device:  # device-resident loop (hb_dsampler_*): host only draws the swap schedule
+    from hb_mcmc_amd.dsampler import DeviceSampler
+
+    with DeviceSampler(S, L) as D:
+        D.init_logl()
+        for it in range(min(20, a.iters)):  # warm-up (code objects, first launches)
+            D.step(it)
+        D.sync()
+        t0 = time.perf_counter()
+        for it in range(20, a.iters):
+            D.step(it)
+        D.sync()
+        wall = time.perf_counter() - t0
+        _, _, _, lmap, st = D.gather()
+        D.download()
+    k = a.iters - 20
+    print(json.dumps({"mode": "device", "walkers": W, "ncad": n, "iters": k, "ms_per_iter": wall / k * 1e3,
+                      "evals_per_s": W * k / wall, "logLmap": lmap, "stats": S.stats()}))
+    S.close()
+    L.close()
+    sys.exit(0)
 x, _, _ = S.get()
 S.set_logl(L.loglike(x))
 ph = dict(propose=0.0, loglik=0.0, accept=0.0, swap=0.0, perm=0.0, end=0.0)

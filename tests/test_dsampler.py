@@ -1,0 +1,162 @@
+"""The device-resident sampler (hb_mcmc_amd/csrc/hb_dsampler.hip): the same
+PT-MCMC loop as the host sampler with proposals, walls, priors, Hastings,
+history and tempering swaps on the GPU.
+
+CPU: the level-parallel replay of the W sequential tempering attempts equals
+the sequential ptmcmc loop (mcmc_wrapper2.c:768-817) on random inputs -- the
+schedule logic of hb_dsampler_step restated in numpy.
+
+GPU: (1) the device run reproduces the REFERENCE sampler's own trace
+(`HB_MCMC 1200 127079833 0.5021 0`, tests/golden) like the host loop does:
+states and bookkeeping exact, logL within 1e-10; (2) after K iterations the
+device sampler's whole state (states, logL, chain ids, RNG streams, history,
+counters) equals the host sampler's after the same K iterations with the same
+GPU likelihood, bit for bit -- at W = 50 (trace config) and W = 4096 with the
+large-W ladder, past NPAST so differential-evolution jumps are exercised.
+"""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import ROOT
+
+
+def levels(b, W):
+    """Dependency level of each attempt (hb_dsampler_step); -1 = void (b = W-1)."""
+    last = np.zeros(W + 1, dtype=np.int64)
+    lv = np.full(len(b), -1)
+    for i, x in enumerate(b):
+        if x + 1 >= W:
+            continue
+        lv[i] = max(last[x], last[x + 1]) + 1
+        last[x] = last[x + 1] = lv[i]
+    return lv
+
+
+def swap_sequential(idx, L, temp, b, beta):
+    idx = idx.copy()
+    for x, be in zip(b, beta):
+        a = x + 1
+        if a >= len(idx):
+            continue
+        olda, oldb = idx[a], idx[x]
+        hs = (temp[x] - temp[a]) / (temp[x] * temp[a])
+        if np.exp((L[oldb] - L[olda]) * hs) >= be:
+            idx[a], idx[x] = oldb, olda
+    return idx
+
+
+def swap_levels(idx, L, temp, b, beta):
+    idx = idx.copy()
+    lv = levels(b, len(idx))
+    for level in range(1, lv.max() + 1):
+        sel = np.nonzero(lv == level)[0]
+        xs = b[sel]
+        assert len(np.unique(np.concatenate([xs, xs + 1]))) == 2 * len(xs), "attempts of a level overlap"
+        a = xs + 1
+        olda, oldb = idx[a], idx[xs]
+        hs = (temp[xs] - temp[a]) / (temp[xs] * temp[a])
+        acc = np.exp((L[oldb] - L[olda]) * hs) >= beta[sel]
+        idx[a[acc]], idx[xs[acc]] = oldb[acc], olda[acc]
+    return idx
+
+
+@pytest.mark.parametrize("W", [2, 3, 50, 1000, 4096])
+def test_level_schedule_equals_sequential_swaps(W):
+    rng = np.random.default_rng(W)
+    temp = np.array([1.4 ** (i % 50) for i in range(W)])
+    for rep in range(3):
+        L = -np.abs(rng.normal(0, 50, W))
+        idx = rng.permutation(W)
+        b = rng.integers(0, W, W)  # includes the void b = W-1 attempts
+        beta = rng.uniform(0, 1, W)
+        assert np.array_equal(swap_levels(idx, L, temp, b, beta), swap_sequential(idx, L, temp, b, beta))
+
+
+def test_level_count_is_small():
+    """~10 levels at W = 4096: the swap kernel's sequential depth."""
+    rng = np.random.default_rng(7)
+    lv = levels(rng.integers(0, 4095, 4096), 4096)
+    assert lv.max() <= 20
+
+
+def test_device_sampler_symbols_exported():
+    from hb_mcmc_amd import _lib, sampler
+
+    lib = sampler._declare(_lib.lib())
+    for name in ("hb_dsampler_create", "hb_dsampler_step", "hb_dsampler_download", "hb_mcmc_run_device",
+                 "hb_sampler_export", "hb_glibc_eval"):
+        assert hasattr(lib, name)
+
+
+# ---------------------------------------------------------------------------
+# GPU
+# ---------------------------------------------------------------------------
+@pytest.mark.gpu
+def test_device_sampler_reproduces_reference_trace(tmp_path):
+    from test_sampler import assert_gpu_run_matches_reference, stage_input
+
+    g = stage_input(str(tmp_path))
+    exe = os.path.join(ROOT, "hb_mcmc_amd", "lib", "hb_mcmc")
+    r = subprocess.run([exe, "1200", "127079833", "0.5021", "0", "--root", str(tmp_path), "--device-sampler"],
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr
+    assert "device-resident sampler" in r.stdout
+    assert_gpu_run_matches_reference(tmp_path, g)
+
+
+def _host_vs_device(W, niter, ladder, seed_run=0):
+    from hb_mcmc_amd import synth
+    from hb_mcmc_amd.dsampler import DeviceSampler
+    from hb_mcmc_amd.likelihood import HBLikelihood
+    from hb_mcmc_amd.sampler import SlotSampler
+
+    n = 256
+    t = synth.cadences(n)
+    with HBLikelihood(t, np.ones(n), np.ones(n)) as tmp:
+        truth = tmp.light_curve(synth.THETA_STAR[None, :])[0]
+    s = np.full(n, 1e-3)
+    f = truth + s * synth.noise(n)
+    L = HBLikelihood(t, f, s)
+    L.reserve(W)
+    npast = 20
+    logp = synth.THETA_STAR[2]
+    # host loop with the GPU likelihood
+    H = SlotSampler(niter, W, logp, 0, W, run=seed_run, npast=npast, ladder=ladder, nthreads=8)
+    x, _, _ = H.get()
+    H.set_logl(L.loglike(x))
+    for it in range(niter):
+        y = H.propose(it)
+        H.accept(it, L.loglike(y))
+        _, ll, _ = H.get()
+        perm, _ = H.swap(ll)
+        H.apply_perm(perm)
+        H.end_iter(it)
+    # device loop from a fresh sampler with the same configuration
+    D0 = SlotSampler(niter, W, logp, 0, W, run=seed_run, npast=npast, ladder=ladder, nthreads=8)
+    with DeviceSampler(D0, L) as D:
+        D.init_logl()
+        for it in range(niter):
+            D.step(it)
+        D.download()
+    out = []
+    for S in (H, D0):
+        xs, ls, cid = S.get()
+        out.append((xs, ls, cid, S.stats(), S.state_arrays()))
+    L.close()
+    return out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("W,niter,ladder", [(50, 60, 0), (4096, 30, 1)])
+def test_device_sampler_state_equals_host_sampler(W, niter, ladder):
+    (hx, hl, hc, hs, ha), (dx, dl, dc, ds, da) = _host_vs_device(W, niter, ladder)
+    assert np.array_equal(hc, dc), "chain ids by slot"
+    assert np.array_equal(hx, dx), "states"
+    assert np.array_equal(hl, dl), "logL"
+    assert hs == ds, (hs, ds)
+    for k in ha:
+        assert np.array_equal(ha[k], da[k]), k
+    assert hs["cold_acc"] > 0 and hs["nswap"] > 0
