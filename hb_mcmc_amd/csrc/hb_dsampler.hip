@@ -31,6 +31,7 @@
 #include "../../include/hbmi.h"
 #include "hb_glibc_math.hpp"
 #include "hb_sampler_view.hpp"
+#include "hb_walls.hpp"
 
 extern "C" int hbx_set_error(const char* msg);
 extern "C" int hbx_ctx_device(const hb_ctx* c);
@@ -45,8 +46,10 @@ constexpr int NDIV = 1 + IMM1 / NTAB;
 constexpr double AM = 1.0 / IM1;
 constexpr double RNMX = 1.0 - 1.2e-7;
 constexpr double kSqrt2Pi = 2.5066282746;  // mcmc_wrapper2.h:10
-constexpr int kBlk = 64;                   // slots per workgroup of the per-slot kernels
+constexpr int kBlk = 64;                   // slots per workgroup of the gather kernel
+constexpr int kPW = 16;                    // slots per propose wave (lanes 0..15 draw, 64 share the priors)
 constexpr int kSwapThreads = 1024;
+constexpr int kMaxLevels = 255;            // swap levels staged in LDS (W = 4096 needs ~10)
 constexpr int kEvCap = 1024;               // big-jump records between drains (<= 6 per iteration)
 
 // run constants (kernel argument)
@@ -87,6 +90,8 @@ struct SwapEnt {
 
 // device state (pointers into one allocation set)
 struct Dev {
+  const Params* P; // run constants (device copy)
+  double* hs;      // [W] tempering factor of the pair (b, b+1): (T_b - T_b+1) / (T_b T_b+1)
   double* x;       // [W][21] by chain
   double* logL;    // [W] by chain
   double* logP;    // [W] by chain
@@ -120,7 +125,7 @@ struct Rng {
   int idum, idum2, iy, iset;
   double gset;
   long long cts;
-  int* iv;  // LDS column, stride kBlk
+  int* iv;  // LDS column, stride kPW (ds_propose)
 };
 
 __device__ double ran2(Rng& r) {
@@ -132,7 +137,7 @@ __device__ double ran2(Rng& r) {
       const int k = r.idum / IQ1;
       r.idum = IA1 * (r.idum - k * IQ1) - k * IR1;
       if (r.idum < 0) r.idum += IM1;
-      if (j < NTAB) r.iv[j * kBlk] = r.idum;
+      if (j < NTAB) r.iv[j * kPW] = r.idum;
     }
     r.iy = r.iv[0];
   }
@@ -143,8 +148,8 @@ __device__ double ran2(Rng& r) {
   r.idum2 = IA2 * (r.idum2 - k * IQ2) - k * IR2;
   if (r.idum2 < 0) r.idum2 += IM2;
   const int j = r.iy / NDIV;
-  r.iy = r.iv[j * kBlk] - r.idum2;
-  r.iv[j * kBlk] = r.idum;
+  r.iy = r.iv[j * kPW] - r.idum2;
+  r.iv[j * kPW] = r.idum;
   if (r.iy < 1) r.iy += IMM1;
   const double temp = AM * (double)r.iy;
   return temp > RNMX ? RNMX : temp;
@@ -173,183 +178,235 @@ __device__ double gauss_pdf(double x, double mean, double sigma) {
   return (1 / sigma / kSqrt2Pi) * hbglibc::exp(-hbglibc::pow((x - mean) / sigma, 2.) / 2.);
 }
 
-__device__ double log_prior(const double* x, const Params& P) {
-  double lp = 0.;
-#pragma unroll
-  for (int i = 0; i < kNp; ++i) {
-    double mean, sig;
-    if (i == 7 || i == 8) { mean = 0.; sig = 1.; }
-    else if (i == 9 || i == 11) { mean = 0.16; sig = 0.04; }
-    else if (i == 10 || i == 12) { mean = 0.34; sig = 0.04; }
-    else if (i == 13 || i == 14) { mean = 1.; sig = 0.2; }
-    else if (i == 15 || i == 16) { mean = 0.; sig = 0.1; }
-    else if (i == 17 || i == 18) { mean = 0.; sig = 1.; }
-    else { mean = 0.; sig = 1.e15; }
-    if (P.gpflag[i] == 1) lp += hbglibc::log(gauss_pdf(x[i], mean, sig));
-  }
-  return lp;
+// one term of get_logP (:703-765): log(gaussian(x_i, mean_i, sigma_i))
+__device__ double prior_term(int i, double xi) {
+  double mean, sig;
+  if (i == 7 || i == 8) { mean = 0.; sig = 1.; }
+  else if (i == 9 || i == 11) { mean = 0.16; sig = 0.04; }
+  else if (i == 10 || i == 12) { mean = 0.34; sig = 0.04; }
+  else if (i == 13 || i == 14) { mean = 1.; sig = 0.2; }
+  else if (i == 15 || i == 16) { mean = 0.; sig = 0.1; }
+  else if (i == 17 || i == 18) { mean = 0.; sig = 1.; }
+  else { mean = 0.; sig = 1.e15; }
+  return hbglibc::log(gauss_pdf(xi, mean, sig));
 }
 
-// gaussian_proposal_parallel (:1062-1088)
-__device__ void gaussian_step(const double* x, Rng& r, const Params& P, double scale, double temp, double* y) {
+// Per-lane parameter vectors live in LDS columns: v[n * kPW] is slot n.
+// gaussian_proposal_parallel (:1062-1088); dx is drawn and added in one pass
+// (the draws come in n order either way)
+__device__ void gaussian_step(const double* x, double* y, Rng& r, const Params* P, double scale, double temp) {
   const double sqtemp = sqrt(temp);
-  double dx[kNp];
-  for (int n = 0; n < kNp; ++n) dx[n] = gasdev(r) * P.sigma_p[n] * sqtemp * scale;
-#pragma unroll
-  for (int n = 0; n < kNp; ++n) y[n] = x[n] + dx[n];
+  for (int n = 0; n < kNp; ++n) y[n * kPW] = x[n * kPW] + gasdev(r) * P->sigma_p[n] * sqtemp * scale;
 }
 
 // differential_evolution_proposal_parallel (:1091-1140) as compiled (see
-// hb_sampler.cpp de_step: a == 0, the uninitialised c == 0)
-__device__ void de_step(const double* x, Rng& r, const double* hist, int npast, double* y) {
+// hb_sampler.cpp de_step: a == 0, the uninitialised c == 0).  The 0.9 draw
+// precedes the per-parameter Gaussians, as in the reference.
+__device__ void de_step(const double* x, double* y, Rng& r, const double* hist, int npast) {
   int a = (int)(ran2(r) * npast);
   a = (int)ran2(r);
   int b = a;
   while (b == a) b = (int)(ran2(r) * npast);
   const double g0 = gauss_pdf(0, 0, 1.e-4) - 0.5;
-  double dx[kNp], eps[kNp];
-#pragma unroll
+  const bool scaled = ran2(r) < 0.9;
+  const double gamma = 2.388 / sqrt(2. * kNp);  // GAMMA, mcmc_wrapper2.h:13
+  const double* hb = hist + (size_t)b * kNp;
+  const double* ha = hist + (size_t)a * kNp;
   for (int n = 0; n < kNp; ++n) {
-    dx[n] = hist[(size_t)b * kNp + n] - hist[(size_t)a * kNp + n];
-    eps[n] = dx[n] * g0;
-  }
-  if (ran2(r) < 0.9) {
-    const double gamma = 2.388 / sqrt(2. * kNp);  // GAMMA, mcmc_wrapper2.h:13
-    for (int n = 0; n < kNp; ++n) dx[n] *= gasdev(r) * gamma;
-  }
-#pragma unroll
-  for (int n = 0; n < kNp; ++n) {
-    dx[n] += eps[n];
-    y[n] = x[n] + dx[n];
+    double dx = hb[n] - ha[n];
+    const double eps = dx * g0;
+    if (scaled) dx *= gasdev(r) * gamma;
+    dx += eps;
+    y[n * kPW] = x[n * kPW] + dx;
   }
 }
 
-// walls (:440-467), bounded like hb_sampler.cpp apply_walls
-__device__ void apply_walls(double* y, const Params& P) {
-#pragma unroll
-  for (int i = 0; i < kNp; ++i) {
-    const double lo = P.lim_lo[i], hi = P.lim_hi[i];
-    double v = y[i];
-    for (long guard = 0; guard < 100000000L; ++guard) {
-      const bool below = (P.fl_lo[i] == 1) && (v < lo);
-      const bool above = (P.fl_hi[i] == 1) && (v > hi);
-      if (!(below || above)) break;
-      v = (v < lo) ? 2.0 * lo - v : 2.0 * hi - v;
-    }
-    for (long guard = 0; (P.fl_lo[i] == 2) && (v < lo) && guard < 100000000L; ++guard) v = hi + (v - lo);
-    for (long guard = 0; (P.fl_hi[i] == 2) && (v > hi) && guard < 100000000L; ++guard) v = lo + (v - hi);
-    y[i] = v;
-  }
-}
 
 // ---------------------------------------------------------------------------
 // kernels
 // ---------------------------------------------------------------------------
-// proposals (:386-485) for every slot; y, logPy, jump, alpha2 by slot
-__global__ __launch_bounds__(kBlk) void ds_propose(Params P, Dev D, long long iter) {
-  __shared__ int ivs[NTAB * kBlk];
+// proposals (:386-485) for kPW slots per wave: lanes 0..kPW-1 run the slots'
+// random streams (inherently sequential per slot), then all 64 lanes share
+// the prior terms (4 lanes per slot), summed per slot in the reference's
+// order.  Vectors and shuffle tables are staged in LDS; y leaves coalesced.
+__global__ __launch_bounds__(64) void ds_propose(Dev D, int W, int NPAST, long long iter) {
+  __shared__ int ivs[NTAB * kPW];
+  __shared__ double xs[kNp * kPW], ys[kNp * kPW];
+  __shared__ double terms[2][kNp][kPW];
+  __shared__ int chain_s[kPW], needx_s[kPW];
+  const Params* P = D.P;
   const int lane = threadIdx.x;
-  const int j = blockIdx.x * kBlk + lane;
-  if (j >= P.W) return;
-  int* iv = &ivs[lane];
-  for (int t = 0; t < NTAB; ++t) iv[t * kBlk] = D.iv[(size_t)t * P.W + j];
-  Rng r{D.idum[j], D.idum2[j], D.iy[j], D.iset[j], D.gset[j], D.cts[j], iv};
-  const int chain = D.idx[j];
-  double xc[kNp], y[kNp];
-#pragma unroll
-  for (int i = 0; i < kNp; ++i) xc[i] = D.x[(size_t)chain * kNp + i];
-  const double a = ran2(r);
-  const double jscale = hbglibc::pow(10., -6. + 6. * a);
-  int jmp = 0, jt = 0;
-  if ((ran2(r) < 0.5) && (iter > P.NPAST)) jmp = 1;
-  if (jmp == 0) {
-    gaussian_step(xc, r, P, jscale, D.temp[j], y);
-    jt = 1;
+  const int j0 = blockIdx.x * kPW;
+  const int nw = min(kPW, W - j0);
+  if (lane < kPW) {
+    const int c = lane < nw ? D.idx[j0 + lane] : 0;
+    chain_s[lane] = c;
+    needx_s[lane] = lane < nw ? !D.logP_ok[c] : 0;
   }
-  if (jmp == 1) {
-    if (chain == 0) {
-      D.DEtrial_arr[j]++;
-      atomicAdd((unsigned long long*)&D.ctr->DEtrial_tot, 1ull);
-    }
-    de_step(xc, r, &D.hist[(size_t)j * P.NPAST * kNp], P.NPAST, y);
-    jt = 2;
-    double dx_mag = 0;
-    for (int i = 0; i < kNp; ++i) dx_mag += (xc[i] - y[i]) * (xc[i] - y[i]);
-    if (dx_mag < 1e-6) {
-      gaussian_step(xc, r, P, jscale, D.temp[j], y);
+  for (int q = lane; q < NTAB * kPW; q += 64) {
+    const int t = q / kPW, w = q % kPW;
+    ivs[q] = w < nw ? D.iv[(size_t)t * W + j0 + w] : 0;
+  }
+  __syncthreads();
+  for (int q = lane; q < kNp * kPW; q += 64) {
+    const int w = q / kNp, n = q % kNp;
+    xs[n * kPW + w] = w < nw ? D.x[(size_t)chain_s[w] * kNp + n] : 0.0;
+  }
+  __syncthreads();
+  if (lane < nw) {
+    const int j = j0 + lane;
+    const int chain = chain_s[lane];
+    Rng r{D.idum[j], D.idum2[j], D.iy[j], D.iset[j], D.gset[j], D.cts[j], &ivs[lane]};
+    const double* x = &xs[lane];
+    double* y = &ys[lane];
+    const double temp = D.temp[j];
+    const double a = ran2(r);
+    const double jscale = hbglibc::pow(10., -6. + 6. * a);
+    int jmp = 0, jt = 0;
+    if ((ran2(r) < 0.5) && (iter > NPAST)) jmp = 1;
+    if (jmp == 0) {
+      gaussian_step(x, y, r, P, jscale, temp);
       jt = 1;
     }
-  }
-  apply_walls(y, P);
-  if (y[1] > y[0]) {  // "order the masses" (:470-475) as written: y[1] = y[0]
-    y[1] = y[0];
-  }
-  y[2] = P.log_lc_period;
-  y[6] = fmod(y[6], P.LC_PERIOD);
-  if (!D.logP_ok[chain]) {  // :444 recomputes it every step; it only changes with the state
-    D.logP[chain] = log_prior(xc, P);
-    D.logP_ok[chain] = 1;
-  }
-  D.logPy[j] = log_prior(y, P);
-  D.jump[j] = jmp;
-  D.jtype[j] = jt;
-  D.alpha2[j] = ran2(r);  // drawn after the likelihood calls in the reference; same stream order
-#pragma unroll
-  for (int i = 0; i < kNp; ++i) D.y[(size_t)j * kNp + i] = y[i];
-  D.idum[j] = r.idum;
-  D.idum2[j] = r.idum2;
-  D.iy[j] = r.iy;
-  D.iset[j] = r.iset;
-  D.gset[j] = r.gset;
-  D.cts[j] = r.cts;
-  for (int t = 0; t < NTAB; ++t) D.iv[(size_t)t * P.W + j] = iv[t * kBlk];
-}
-
-// Hastings test and history (:492-546)
-__global__ __launch_bounds__(kBlk) void ds_accept(Params P, Dev D, long long iter) {
-  const int j = blockIdx.x * kBlk + threadIdx.x;
-  if (j >= P.W) return;
-  const int k = (int)(iter - (iter / P.NPAST) * P.NPAST);
-  const int chain = D.idx[j];
-  const double ly = D.logLy[j], lx = D.logL[chain];
-  double* xc = &D.x[(size_t)chain * kNp];
-  const double* yj = &D.y[(size_t)j * kNp];
-  const double H = hbglibc::exp((ly - lx) / D.temp[j] + (D.logPy[j] - D.logP[chain]));
-  if (D.alpha2[j] <= H) {
-    if ((lx / ly <= 0.5) && (iter > 10000) && (j <= 5) && P.log_on) {
-      const int e = atomicAdd(&D.ctr->nev, 1);
-      if (e < kEvCap) {
-        Event& ev = D.ev[e];
-        ev.iter = iter;
-        ev.chain = chain;
-        ev.jtype = D.jtype[j];
-        ev.slot = j;
-        ev.H = H;
-        ev.alpha = D.alpha2[j];
-        ev.tmp = D.temp[j];
-        ev.lx = lx;
-        ev.ly = ly;
-        ev.px = D.logP[chain];
-        ev.py = D.logPy[j];
-        for (int i = 0; i < kNp; ++i) {
-          ev.xo[i] = xc[i];
-          ev.xn[i] = yj[i];
-        }
+    if (jmp == 1) {
+      if (chain == 0) {
+        D.DEtrial_arr[j]++;
+        atomicAdd((unsigned long long*)&D.ctr->DEtrial_tot, 1ull);
+      }
+      de_step(x, y, r, &D.hist[(size_t)j * NPAST * kNp], NPAST);
+      jt = 2;
+      double dx_mag = 0;
+      for (int i = 0; i < kNp; ++i) dx_mag += (x[i * kPW] - y[i * kPW]) * (x[i * kPW] - y[i * kPW]);
+      if (dx_mag < 1e-6) {
+        gaussian_step(x, y, r, P, jscale, temp);
+        jt = 1;
       }
     }
-    if (chain == 0) atomicAdd((unsigned long long*)&D.ctr->acc_it, 1ull);
-#pragma unroll
-    for (int i = 0; i < kNp; ++i) xc[i] = yj[i];
-    D.logL[chain] = ly;
-    D.logP[chain] = D.logPy[j];
-    if ((D.jump[j] == 1) && (chain == 0)) {
-      D.DEacc_arr[j]++;
-      atomicAdd((unsigned long long*)&D.ctr->DEacc_tot, 1ull);
+    D.jump[j] = jmp;
+    D.jtype[j] = jt;
+    D.alpha2[j] = ran2(r);  // drawn after the likelihood calls in the reference; same stream order
+    D.idum[j] = r.idum;
+    D.idum2[j] = r.idum2;
+    D.iy[j] = r.iy;
+    D.iset[j] = r.iset;
+    D.gset[j] = r.gset;
+    D.cts[j] = r.cts;
+  }
+  __syncthreads();
+  // walls (:440-467): the kPW x 21 coordinates spread over all 64 lanes
+  for (int q = lane; q < kNp * kPW; q += 64) {
+    const int i = q / kPW, w = q % kPW;
+    if (w < nw) ys[q] = hbwall::apply_wall(ys[q], P->lim_lo[i], P->lim_hi[i], P->fl_lo[i], P->fl_hi[i]);
+  }
+  __syncthreads();
+  if (lane < nw) {
+    double* y = &ys[lane];
+    if (y[kPW] > y[0]) y[kPW] = y[0];  // "order the masses" (:470-475) as written: y[1] = y[0]
+    y[2 * kPW] = P->log_lc_period;
+    y[6 * kPW] = fmod(y[6 * kPW], P->LC_PERIOD);
+  }
+  __syncthreads();
+  // prior terms: lane group g = lane / kPW takes slots i = g, g + 4, ... of walker lane % kPW
+  {
+    const int w = lane % kPW;
+    for (int i = lane / kPW; i < kNp; i += 64 / kPW) {
+      if (P->gpflag[i] != 1 || w >= nw) continue;
+#ifdef HB_DS_ABL_NOPRIOR  // experiment builds only (timing ablation)
+      terms[0][i][w] = 0.0; terms[1][i][w] = 0.0; continue;
+#endif
+      terms[0][i][w] = prior_term(i, ys[i * kPW + w]);
+      if (needx_s[w]) terms[1][i][w] = prior_term(i, xs[i * kPW + w]);  // :444, first use of a state
     }
   }
-  double* h = &D.hist[((size_t)j * P.NPAST + k) * kNp];
-#pragma unroll
-  for (int i = 0; i < kNp; ++i) h[i] = xc[i];
+  __syncthreads();
+  if (lane < nw) {
+    const int j = j0 + lane;
+    double lpy = 0., lpx = 0.;
+    for (int i = 0; i < kNp; ++i) {
+      if (P->gpflag[i] != 1) continue;
+      lpy += terms[0][i][lane];
+      lpx += terms[1][i][lane];
+    }
+    D.logPy[j] = lpy;
+    if (needx_s[lane]) {
+      D.logP[chain_s[lane]] = lpx;
+      D.logP_ok[chain_s[lane]] = 1;
+    }
+  }
+  for (int q = lane; q < kNp * nw; q += 64) {
+    const int w = q / kNp, n = q % kNp;
+    D.y[(size_t)j0 * kNp + q] = ys[n * kPW + w];
+  }
+  for (int q = lane; q < NTAB * kPW; q += 64) {
+    const int t = q / kPW, w = q % kPW;
+    if (w < nw) D.iv[(size_t)t * W + j0 + w] = ivs[q];
+  }
+}
+
+// Hastings test and history (:492-546); 64 slots per block, the state and
+// history rows copied cooperatively
+__global__ __launch_bounds__(64) void ds_accept(Dev D, int W, int NPAST, long long iter) {
+  __shared__ int chain_s[64], acc_s[64];
+  const int lane = threadIdx.x;
+  const int j0 = blockIdx.x * 64;
+  const int nw = min(64, W - j0);
+  const int k = (int)(iter - (iter / NPAST) * NPAST);
+  if (lane < nw) {
+    const int j = j0 + lane;
+    const int chain = D.idx[j];
+    const double ly = D.logLy[j], lx = D.logL[chain];
+    const double* xc = &D.x[(size_t)chain * kNp];
+    const double* yj = &D.y[(size_t)j * kNp];
+    const double H = hbglibc::exp((ly - lx) / D.temp[j] + (D.logPy[j] - D.logP[chain]));
+    const bool acc = D.alpha2[j] <= H;
+    chain_s[lane] = chain;
+    acc_s[lane] = acc;
+    if (acc) {
+      if ((lx / ly <= 0.5) && (iter > 10000) && (j <= 5) && D.P->log_on) {
+        const int e = atomicAdd(&D.ctr->nev, 1);
+        if (e < kEvCap) {
+          Event& ev = D.ev[e];
+          ev.iter = iter;
+          ev.chain = chain;
+          ev.jtype = D.jtype[j];
+          ev.slot = j;
+          ev.H = H;
+          ev.alpha = D.alpha2[j];
+          ev.tmp = D.temp[j];
+          ev.lx = lx;
+          ev.ly = ly;
+          ev.px = D.logP[chain];
+          ev.py = D.logPy[j];
+          for (int i = 0; i < kNp; ++i) {
+            ev.xo[i] = xc[i];
+            ev.xn[i] = yj[i];
+          }
+        }
+      }
+      if (chain == 0) atomicAdd((unsigned long long*)&D.ctr->acc_it, 1ull);
+      D.logL[chain] = ly;
+      D.logP[chain] = D.logPy[j];
+      if ((D.jump[j] == 1) && (chain == 0)) {
+        D.DEacc_arr[j]++;
+        atomicAdd((unsigned long long*)&D.ctr->DEacc_tot, 1ull);
+      }
+    }
+  }
+  __syncthreads();
+  // x[chain] = y (accepted), history row k = x[chain] (:533-546)
+  for (int q = lane; q < kNp * nw; q += 64) {
+    const int w = q / kNp, n = q % kNp;
+    const int j = j0 + w;
+    double* xc = &D.x[(size_t)chain_s[w] * kNp];
+    double v;
+    if (acc_s[w]) {
+      v = D.y[(size_t)j * kNp + n];
+      xc[n] = v;
+    } else {
+      v = xc[n];
+    }
+    D.hist[((size_t)j * NPAST + k) * kNp + n] = v;
+  }
 }
 
 // index[] accessors: LDS (small W) or device-coherent global (large W)
@@ -368,33 +425,51 @@ struct IdxRef {
 
 // the W tempering attempts (ptmcmc :768-817) in dependency levels, then the
 // per-iteration bookkeeping of :551-572 / :590 / :639-641
+// LDS mode stages the schedule, logL by chain, the pair factors and index[]
+// (36 W bytes) so that a level costs LDS latency only.
 template <bool LDS>
-__global__ __launch_bounds__(kSwapThreads) void ds_swap(Params P, Dev D, const SwapEnt* sched, const int* off,
-                                                         int nlv, long long iter) {
+__global__ __launch_bounds__(kSwapThreads) void ds_swap(Dev D, int W, const SwapEnt* __restrict__ sched,
+                                                         const int* __restrict__ off, int nlv, long long iter) {
   extern __shared__ __align__(16) unsigned char smem[];
   __shared__ int nacc_s;
-  const int W = P.W, tid = threadIdx.x;
-  double* Ls = reinterpret_cast<double*>(smem);
-  IdxRef<LDS> idx{LDS ? reinterpret_cast<int*>(smem + sizeof(double) * (size_t)W) : D.idx};
-  const double* L = LDS ? Ls : D.logL;
-  if (tid == 0) nacc_s = 0;
+  __shared__ int off_s[kMaxLevels + 1];
+  const int tid = threadIdx.x;
+  const bool off_lds = nlv <= kMaxLevels;
+  const SwapEnt* S = sched;
+  const double* L = D.logL;
+  const double* hs = D.hs;
+  IdxRef<LDS> idx{D.idx};
+  if (off_lds)
+    for (int l = tid; l <= nlv; l += kSwapThreads) off_s[l] = off[l];
   if (LDS) {
+    SwapEnt* s_l = reinterpret_cast<SwapEnt*>(smem);
+    double* L_l = reinterpret_cast<double*>(smem + sizeof(SwapEnt) * (size_t)W);
+    double* h_l = L_l + W;
+    int* i_l = reinterpret_cast<int*>(h_l + W);
+    const int nent = off[nlv];
     for (int c = tid; c < W; c += kSwapThreads) {
-      Ls[c] = D.logL[c];
-      idx.st(c, D.idx[c]);
+      L_l[c] = D.logL[c];
+      h_l[c] = D.hs[c];
+      i_l[c] = D.idx[c];
     }
+    for (int q = tid; q < nent; q += kSwapThreads) s_l[q] = sched[q];
+    S = s_l;
+    L = L_l;
+    hs = h_l;
+    idx.p = i_l;
   }
+  if (tid == 0) nacc_s = 0;
   __syncthreads();
   int nacc = 0;
   for (int lv = 0; lv < nlv; ++lv) {
-    const int e1 = off[lv + 1];
-    for (int s = off[lv] + tid; s < e1; s += kSwapThreads) {
-      const int b = sched[s].b, a = b + 1;
-      const double be = sched[s].beta;
+    const int e0 = off_lds ? off_s[lv] : off[lv];
+    const int e1 = off_lds ? off_s[lv + 1] : off[lv + 1];
+    for (int s = e0 + tid; s < e1; s += kSwapThreads) {
+      const int b = S[s].b, a = b + 1;
+      const double be = S[s].beta;
       const int olda = idx.ld(a), oldb = idx.ld(b);
-      const double heat1 = D.temp[a], heat2 = D.temp[b];
       const double dlogL = L[oldb] - L[olda];
-      const double Hs = (heat2 - heat1) / (heat2 * heat1);
+      const double Hs = hs[b];  // (temp[b] - temp[a]) / (temp[b] temp[a]), fixed ladder (:803)
       const double al = hbglibc::exp(dlogL * Hs);
       if (al >= be) {
         idx.st(a, oldb);
@@ -405,8 +480,10 @@ __global__ __launch_bounds__(kSwapThreads) void ds_swap(Params P, Dev D, const S
     __syncthreads();
   }
   if (nacc) atomicAdd(&nacc_s, nacc);
-  if (LDS)
+  if (LDS) {
     for (int c = tid; c < W; c += kSwapThreads) D.idx[c] = idx.ld(c);
+    idx.p = D.idx;
+  }
   __syncthreads();
   Counters* C = D.ctr;
   const bool reset = (iter % 100 == 0);
@@ -479,18 +556,23 @@ struct hb_dsampler {
   hipStream_t st = nullptr;
   HbSamplerView v{};
   Params P{};
+  Params* d_params = nullptr;
   Dev D{};
   int W = 0, NPAST = 0, device = 0;
   bool lds_swap = true;
   size_t swap_lds = 0;
   std::vector<void*> allocs;
-  // swap schedules: pinned ring -> one device buffer (stream-ordered)
+  // swap schedules: pinned ring -> device ring, copied on their own stream
+  // (they do not depend on GPU results) so the copy overlaps the iteration's
+  // kernels; the swap launch waits on the copy's event
   static constexpr int R = 4;
+  hipStream_t cst = nullptr;
   unsigned char* pin[R] = {};
-  hipEvent_t ev[R] = {};
-  bool ev_used[R] = {};
+  unsigned char* d_sched[R] = {};
+  hipEvent_t ev_copy[R] = {};   // copy r done
+  hipEvent_t ev_used[R] = {};   // swap that read ring entry r done
+  bool used[R] = {};
   int ring = 0;
-  unsigned char* d_sched = nullptr;
   size_t sched_bytes = 0;
   std::vector<int> b, last, lvl, cnt;
   std::vector<double> beta;
@@ -503,14 +585,17 @@ struct hb_dsampler {
   Event* h_ev = nullptr;
   ~hb_dsampler() {
     if (st) (void)hipStreamSynchronize(st);
+    if (cst) (void)hipStreamSynchronize(cst);
     for (void* p : allocs) (void)hipFree(p);
     for (int r = 0; r < R; ++r) {
       if (pin[r]) (void)hipHostFree(pin[r]);
-      if (ev[r]) (void)hipEventDestroy(ev[r]);
+      if (ev_copy[r]) (void)hipEventDestroy(ev_copy[r]);
+      if (ev_used[r]) (void)hipEventDestroy(ev_used[r]);
     }
     if (h_ctr) (void)hipHostFree(h_ctr);
     if (h_ev) (void)hipHostFree(h_ev);
     if (st) (void)hipStreamDestroy(st);
+    if (cst) (void)hipStreamDestroy(cst);
   }
   template <class T>
   hipError_t alloc(T** p, size_t n) {
@@ -565,13 +650,17 @@ extern "C" hb_dsampler* hb_dsampler_create(hb_sampler* s, hb_ctx* ctx) {
       (e = d->alloc(&D.jtype, Wz)) || (e = d->alloc(&D.hist, Wz * (size_t)d->NPAST * kNp)) ||
       (e = d->alloc(&D.DEacc_arr, Wz)) || (e = d->alloc(&D.DEtrial_arr, Wz)) || (e = d->alloc(&D.ctr, 1)) ||
       (e = d->alloc(&D.ev, (size_t)kEvCap)) || (e = d->alloc(&d->d_xs, Wz * kNp)) ||
-      (e = d->alloc(&d->d_ls, Wz)) || (e = d->alloc(&d->d_ps, Wz)) || (e = d->alloc(&d->d_ok, Wz)))
+      (e = d->alloc(&d->d_ls, Wz)) || (e = d->alloc(&d->d_ps, Wz)) || (e = d->alloc(&d->d_ok, Wz)) ||
+      (e = d->alloc(&D.hs, Wz)) || (e = d->alloc(&d->d_params, 1)))
     return fail("hipMalloc", e);
+  D.P = d->d_params;
+  if ((e = hipStreamCreateWithFlags(&d->cst, hipStreamNonBlocking)) != hipSuccess) return fail("stream", e);
   d->sched_bytes = sizeof(SwapEnt) * Wz + sizeof(int) * (Wz + 2);
-  if ((e = d->alloc(&d->d_sched, d->sched_bytes))) return fail("hipMalloc", e);
   for (int r = 0; r < hb_dsampler::R; ++r) {
+    if ((e = d->alloc(&d->d_sched[r], d->sched_bytes))) return fail("hipMalloc", e);
     if ((e = hipHostMalloc((void**)&d->pin[r], d->sched_bytes, hipHostMallocDefault))) return fail("pinned", e);
-    if ((e = hipEventCreateWithFlags(&d->ev[r], hipEventDisableTiming))) return fail("event", e);
+    if ((e = hipEventCreateWithFlags(&d->ev_copy[r], hipEventDisableTiming))) return fail("event", e);
+    if ((e = hipEventCreateWithFlags(&d->ev_used[r], hipEventDisableTiming))) return fail("event", e);
   }
   if ((e = hipHostMalloc((void**)&d->h_ctr, sizeof(Counters), hipHostMallocDefault))) return fail("pinned", e);
   if ((e = hipHostMalloc((void**)&d->h_ev, sizeof(Event) * kEvCap, hipHostMallocDefault))) return fail("pinned", e);
@@ -580,9 +669,9 @@ extern "C" hb_dsampler* hb_dsampler_create(hb_sampler* s, hb_ctx* ctx) {
   d->last.resize(W + 1);
   d->lvl.resize(W);
   d->cnt.resize(W + 2);
-  // index[] + logL by chain in LDS when they fit (160 KB per CU on gfx950)
-  d->swap_lds = (sizeof(double) + sizeof(int)) * Wz;
-  d->lds_swap = d->swap_lds <= 150 * 1024;
+  // schedule, logL, pair factors and index[] in LDS when they fit (160 KB per CU on gfx950)
+  d->swap_lds = (sizeof(SwapEnt) + 2 * sizeof(double) + sizeof(int)) * Wz;
+  d->lds_swap = d->swap_lds <= 158 * 1024;
   if (d->lds_swap) {
     e = hipFuncSetAttribute((const void*)ds_swap<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)d->swap_lds);
@@ -658,6 +747,13 @@ static int ds_upload(hb_dsampler* d) {
   DS_TRY(hipMemcpyAsync(D.logP_ok, ok.data(), sizeof(int) * Wz, hipMemcpyHostToDevice, s), "upload");
   DS_TRY(hipMemcpyAsync(D.idx, idx.data(), sizeof(int) * Wz, hipMemcpyHostToDevice, s), "upload");
   DS_TRY(hipMemcpyAsync(D.temp, v.temp, sizeof(double) * Wz, hipMemcpyHostToDevice, s), "upload");
+  std::vector<double> hs(Wz, 0.0);
+  for (int b = 0; b + 1 < W; ++b) {  // ptmcmc's H (:803) for the pair (a, b) = (b+1, b): same IEEE ops
+    const double heat1 = v.temp[b + 1], heat2 = v.temp[b];
+    hs[b] = (heat2 - heat1) / (heat2 * heat1);
+  }
+  DS_TRY(hipMemcpyAsync(D.hs, hs.data(), sizeof(double) * Wz, hipMemcpyHostToDevice, s), "upload");
+  DS_TRY(hipMemcpyAsync(d->d_params, &d->P, sizeof(Params), hipMemcpyHostToDevice, s), "upload");
   DS_TRY(hipMemcpyAsync(D.idum, idum.data(), sizeof(int) * Wz, hipMemcpyHostToDevice, s), "upload");
   DS_TRY(hipMemcpyAsync(D.idum2, idum2.data(), sizeof(int) * Wz, hipMemcpyHostToDevice, s), "upload");
   DS_TRY(hipMemcpyAsync(D.iy, iy.data(), sizeof(int) * Wz, hipMemcpyHostToDevice, s), "upload");
@@ -790,7 +886,7 @@ extern "C" int hb_dsampler_step(hb_dsampler* d, long iter) {
   }
   const int r = d->ring;
   d->ring = (d->ring + 1) % hb_dsampler::R;
-  if (d->ev_used[r]) DS_TRY(hipEventSynchronize(d->ev[r]), "schedule ring");
+  if (d->used[r]) DS_TRY(hipEventSynchronize(d->ev_used[r]), "schedule ring");  // entry r free again
   SwapEnt* ent = reinterpret_cast<SwapEnt*>(d->pin[r]);
   int* off = reinterpret_cast<int*>(d->pin[r] + sizeof(SwapEnt) * (size_t)W);
   std::fill(d->cnt.begin(), d->cnt.begin() + nlv + 2, 0);
@@ -807,24 +903,27 @@ extern "C" int hb_dsampler_step(hb_dsampler* d, long iter) {
     e.pad = 0;
     e.beta = d->beta[i];
   }
-  DS_TRY(hipMemcpyAsync(d->d_sched, d->pin[r], d->sched_bytes, hipMemcpyHostToDevice, s), "schedule upload");
-  DS_TRY(hipEventRecord(d->ev[r], s), "schedule ring");
-  d->ev_used[r] = true;
-  const SwapEnt* d_ent = reinterpret_cast<const SwapEnt*>(d->d_sched);
-  const int* d_off = reinterpret_cast<const int*>(d->d_sched + sizeof(SwapEnt) * (size_t)W);
+  const size_t used_bytes = sizeof(SwapEnt) * (size_t)W + sizeof(int) * (size_t)(nlv + 1);
+  DS_TRY(hipMemcpyAsync(d->d_sched[r], d->pin[r], used_bytes, hipMemcpyHostToDevice, d->cst), "schedule upload");
+  DS_TRY(hipEventRecord(d->ev_copy[r], d->cst), "schedule ring");
+  const SwapEnt* d_ent = reinterpret_cast<const SwapEnt*>(d->d_sched[r]);
+  const int* d_off = reinterpret_cast<const int*>(d->d_sched[r] + sizeof(SwapEnt) * (size_t)W);
 
-  const int nb = (W + kBlk - 1) / kBlk;
-  ds_propose<<<nb, kBlk, 0, s>>>(P, D, (long long)iter);
+  const int NPAST = d->NPAST;
+  ds_propose<<<(W + kPW - 1) / kPW, 64, 0, s>>>(D, W, NPAST, (long long)iter);
   DS_TRY(hipGetLastError(), "ds_propose");
   const int rc = hb_loglik_batch_dev(d->ctx, D.y, W, D.logLy, (void*)s);
   if (rc) return rc;
-  ds_accept<<<nb, kBlk, 0, s>>>(P, D, (long long)iter);
+  ds_accept<<<(W + 63) / 64, 64, 0, s>>>(D, W, NPAST, (long long)iter);
   DS_TRY(hipGetLastError(), "ds_accept");
+  DS_TRY(hipStreamWaitEvent(s, d->ev_copy[r], 0), "schedule wait");
   if (d->lds_swap)
-    ds_swap<true><<<1, kSwapThreads, d->swap_lds, s>>>(P, D, d_ent, d_off, nlv, (long long)iter);
+    ds_swap<true><<<1, kSwapThreads, d->swap_lds, s>>>(D, W, d_ent, d_off, nlv, (long long)iter);
   else
-    ds_swap<false><<<1, kSwapThreads, 0, s>>>(P, D, d_ent, d_off, nlv, (long long)iter);
+    ds_swap<false><<<1, kSwapThreads, 0, s>>>(D, W, d_ent, d_off, nlv, (long long)iter);
   DS_TRY(hipGetLastError(), "ds_swap");
+  DS_TRY(hipEventRecord(d->ev_used[r], s), "schedule ring");
+  d->used[r] = true;
   if (P.log_on && iter > 10000 && iter % 100 == 0) return ds_drain_events(d);
   return 0;
 }

@@ -34,3 +34,15 @@ long hbg_check(int fn, const double* x, const double* y, long n, long* first_bad
   return bad;
 }
 }
+
+// ---- walls (hb_walls.hpp): fast-forwarded folds vs the plain loop ----
+#include "hb_walls.hpp"
+
+extern "C" {
+void hbw_eval(int plain, const double* v, const double* lo, const double* hi, const double* fl, const double* fh,
+              long n, double* out) {
+  for (long i = 0; i < n; ++i)
+    out[i] = plain ? hbwall::apply_wall_plain(v[i], lo[i], hi[i], fl[i], fh[i])
+                   : hbwall::apply_wall(v[i], lo[i], hi[i], fl[i], fh[i]);
+}
+}

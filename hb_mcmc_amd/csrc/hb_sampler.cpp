@@ -32,6 +32,7 @@
 #include "../../include/hb_sampler.h"
 #include "../../include/hbmi.h"
 #include "hb_sampler_view.hpp"
+#include "hb_walls.hpp"
 
 namespace {
 
@@ -126,20 +127,10 @@ double log_prior(const double* x, const Prior& pr) {
 // reflecting (flag 1) and periodic (flag 2) walls (:440-467).  The reference
 // loops forever on a non-finite coordinate; here such a coordinate is left
 // alone after a bounded number of folds (it yields NaN logL -> rejection).
+// Long reflection runs (hot chains) are fast-forwarded exactly (hb_walls.hpp).
 void apply_walls(double* y, const Prior& pr) {
-  for (int i = 0; i < kNp; ++i) {
-    const double lo = pr.limits[i].lo, hi = pr.limits[i].hi;
-    for (long guard = 0; guard < 100000000L; ++guard) {
-      const bool below = (pr.limited[i].lo == 1) && (y[i] < lo);
-      const bool above = (pr.limited[i].hi == 1) && (y[i] > hi);
-      if (!(below || above)) break;
-      y[i] = (y[i] < lo) ? 2.0 * lo - y[i] : 2.0 * hi - y[i];
-    }
-    for (long guard = 0; (pr.limited[i].lo == 2) && (y[i] < lo) && guard < 100000000L; ++guard)
-      y[i] = hi + (y[i] - lo);
-    for (long guard = 0; (pr.limited[i].hi == 2) && (y[i] > hi) && guard < 100000000L; ++guard)
-      y[i] = lo + (y[i] - hi);
-  }
+  for (int i = 0; i < kNp; ++i)
+    y[i] = hbwall::apply_wall(y[i], pr.limits[i].lo, pr.limits[i].hi, pr.limited[i].lo, pr.limited[i].hi);
 }
 
 void gaussian_step(const double* x, long* seed, const double* sigma, double scale, double temp, double* y,

@@ -1,0 +1,132 @@
+// hb_walls.hpp -- the reflecting / periodic walls of mcmc_wrapper2.c:440-467,
+// bit for bit, with an exact fast-forward of long reflection runs.
+//
+// Hot chains (temperatures up to 1.4^49 on the 50-rung ladder) propose steps
+// thousands of ranges wide, and the reference then folds the coordinate back
+// one reflection at a time: v <- 2 lo - v below the range, v <- 2 hi - v above
+// (each a rounded subtraction).  On a GPU lane every fold is a dependent
+// step; 10^4 folds of one hot chain stall its whole wave.
+//
+// Fast-forward (both walls reflecting, v far outside): while |v| stays in one
+// binade [2^e, 2^(e+1)) every double there is a multiple of g = 2^(e-52), and
+// the exact result c - v of a fold lands in the same binade, so
+//     fl(c - v) = round_g(c) - v        (translation by a grid multiple)
+// unless c/g is a rounding tie (then round-half-even would depend on v: no
+// fast-forward).  Two folds (2 lo then 2 hi, or the reverse) therefore move
+// K = v/g by the exact integer D = round(2hi/g) - round(2lo/g); m double
+// folds are K + m D.  m is capped so that every intermediate value keeps a
+// margin inside the binade (and outside [lo, hi]), and so that the fold
+// counter never passes the 10^8 guard of the host loop; the remaining folds
+// run one by one.  tests/test_walls.py checks it against the plain loop.
+#pragma once
+#include <math.h>
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#include <hip/hip_runtime.h>
+#define HBW_FN __host__ __device__ inline
+#else
+#define HBW_FN static inline
+#endif
+
+namespace hbwall {
+
+constexpr int kGuard = 100000000;  // fold bound of the host loop (hb_sampler.cpp, before hb_walls)
+
+// floor(num / den) for exact integers 0 <= num, 1 <= den below 2^53: an
+// approximate quotient corrected with exact products
+HBW_FN double floor_div(double num, double den) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  double y = __builtin_amdgcn_rcp(den);
+  y = __builtin_fma(__builtin_fma(-den, y, 1.0), y, y);
+  double q = floor(num * y);
+#else
+  double q = floor(num / den);
+#endif
+  if (q * den > num) q -= 1.0;
+  if ((q + 1.0) * den <= num) q += 1.0;
+  return q;
+}
+
+// Fast-forward within v's binade: returns v after 2m folds, m >= 0 (m = 0:
+// not applicable, v unchanged); folds_left caps 2m.
+//
+// In units of g (K = |v| / g in [2^52, 2^53)): a pair of folds starting
+// below the range (v < 0) takes the magnitude K -> K + rlo (first fold, the
+// chain is now above hi) -> K + rlo - rhi = K - D; starting above (v > 0),
+// K -> K - rhi -> K - D.  Both exact results must stay in the binade:
+// K_j + c1 >= 2^52 + 1 (c1 = rlo or -rhi), K_j - D >= 2^52 + 1, and at the
+// top K_0 + c1 <= 2^53 - 2.  Every magnitude of the binade exceeds
+// 2 max(|lo|, |hi|), so each value lies outside [lo, hi] on its sign's side.
+HBW_FN double ff_double_folds(double v, double lo, double hi, int folds_left, int& m_out) {
+  m_out = 0;
+  const double av = fabs(v);
+  if (!(av < 0x1p1000) || !(av > 0.0)) return v;
+  int e;
+  frexp(av, &e);                       // av = f 2^e, f in [0.5, 1): binade [2^(e-1), 2^e)
+  const int eb = e - 1;                // av in [2^eb, 2^(eb+1))
+  const double lim = fabs(lo) > fabs(hi) ? fabs(lo) : fabs(hi);
+  if (!(ldexp(1.0, eb) > 2.0 * lim)) return v;
+  const double scale = ldexp(1.0, 52 - eb);  // 1/g
+  const double clo = 2.0 * lo * scale, chi = 2.0 * hi * scale;  // exact (power-of-2 scaling), |.| < 2^52
+  if (clo - floor(clo) == 0.5 || chi - floor(chi) == 0.5) return v;  // rounding ties: no translation
+  const double rlo = rint(clo), rhi = rint(chi);
+  const double D = rhi - rlo;                  // exact integer
+  if (!(D > 0.0)) return v;
+  const double K = av * scale;                 // exact integer in [2^52, 2^53)
+  const double c1 = v < 0.0 ? rlo : -rhi;
+  if (!(K + (c1 > 0.0 ? c1 : 0.0) <= 0x1p53 - 2.0)) return v;
+  // m pairs: K - (m-1) D + c1 >= 2^52 + 1 and K - m D >= 2^52 + 1
+  const double n1 = K - 0x1p52 - 1.0, n2 = K + c1 - 0x1p52 - 1.0;
+  if (!(n1 >= D) || !(n2 >= 0.0)) return v;
+  double m = floor_div(n1, D);
+  const double m2 = floor_div(n2, D) + 1.0;
+  if (m2 < m) m = m2;
+  const double cap = (double)(folds_left / 2);
+  if (m > cap) m = cap;
+  if (!(m >= 1.0)) return v;
+  m_out = (int)m;
+  return copysign((K - m * D) / scale, v);  // exact: integers below 2^53, power-of-2 scaling
+}
+
+// v after the walls of one coordinate (flags: 1 reflecting, 2 periodic).
+// Each pass: one fast-forward through the current binade, then up to four
+// single folds (a binade crossing, a rounding-tie binade, the last approach);
+// the fold count and stopping rule are those of the plain loop.
+HBW_FN double apply_wall(double v, double lo, double hi, double fl, double fh) {
+  int guard = 0;
+  if (fl == 1 && fh == 1) {
+    while (guard < kGuard && (v < lo || v > hi)) {
+      int m;
+      v = ff_double_folds(v, lo, hi, kGuard - guard, m);
+      guard += 2 * m;
+      for (int s = 0; s < 4 && guard < kGuard && (v < lo || v > hi); ++s, ++guard)
+        v = (v < lo) ? 2.0 * lo - v : 2.0 * hi - v;
+    }
+  } else {
+    for (; guard < kGuard; ++guard) {
+      const bool below = (fl == 1) && (v < lo);
+      const bool above = (fh == 1) && (v > hi);
+      if (!(below || above)) break;
+      v = (v < lo) ? 2.0 * lo - v : 2.0 * hi - v;
+    }
+  }
+  for (int g = 0; (fl == 2) && (v < lo) && g < kGuard; ++g) v = hi + (v - lo);
+  for (int g = 0; (fh == 2) && (v > hi) && g < kGuard; ++g) v = lo + (v - hi);
+  return v;
+}
+
+// the plain loop (reference order), for tests
+HBW_FN double apply_wall_plain(double v, double lo, double hi, double fl, double fh) {
+  for (int guard = 0; guard < kGuard; ++guard) {
+    const bool below = (fl == 1) && (v < lo);
+    const bool above = (fh == 1) && (v > hi);
+    if (!(below || above)) break;
+    v = (v < lo) ? 2.0 * lo - v : 2.0 * hi - v;
+  }
+  for (int g = 0; (fl == 2) && (v < lo) && g < kGuard; ++g) v = hi + (v - lo);
+  for (int g = 0; (fh == 2) && (v > hi) && g < kGuard; ++g) v = lo + (v - hi);
+  return v;
+}
+
+}  // namespace hbwall

@@ -150,7 +150,7 @@ def _host_vs_device(W, niter, ladder, seed_run=0):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("W,niter,ladder", [(50, 60, 0), (4096, 30, 1)])
+@pytest.mark.parametrize("W,niter,ladder", [(50, 60, 0), (4096, 30, 1), (6000, 24, 1)])
 def test_device_sampler_state_equals_host_sampler(W, niter, ladder):
     (hx, hl, hc, hs, ha), (dx, dl, dc, ds, da) = _host_vs_device(W, niter, ladder)
     assert np.array_equal(hc, dc), "chain ids by slot"
