@@ -47,7 +47,7 @@ constexpr double AM = 1.0 / IM1;
 constexpr double RNMX = 1.0 - 1.2e-7;
 constexpr double kSqrt2Pi = 2.5066282746;  // mcmc_wrapper2.h:10
 constexpr int kBlk = 64;                   // slots per workgroup of the gather kernel
-constexpr int kPW = 16;                    // slots per propose wave (lanes 0..15 draw, 64 share the priors)
+constexpr int kPW = 4;                     // slots per propose wave (lanes 0..3 draw, 64 share walls and priors)
 constexpr int kSwapThreads = 1024;
 constexpr int kMaxLevels = 255;            // swap levels staged in LDS (W = 4096 needs ~10)
 constexpr int kEvCap = 1024;               // big-jump records between drains (<= 6 per iteration)
@@ -236,16 +236,27 @@ __global__ __launch_bounds__(64) void ds_propose(Dev D, int W, int NPAST, long l
   __shared__ int chain_s[kPW], needx_s[kPW];
   const Params* P = D.P;
   const int lane = threadIdx.x;
-  const int j0 = blockIdx.x * kPW;
-  const int nw = min(kPW, W - j0);
+  // slots blockIdx.x + w gridDim.x (w < kPW): each wave mixes ladder rungs, so
+  // the hot chains' long wall runs spread over the waves instead of piling up
+  // in the blocks of the hottest rungs
+  const int G = gridDim.x;
+  auto slot = [&](int w) { return (int)blockIdx.x + w * G; };
+  const int nw = (W - (int)blockIdx.x + G - 1) / G;  // valid w are 0 .. nw-1 (nw <= kPW)
+#ifdef HB_DS_TIMING  // experiment builds only: per-phase shader clocks of a few blocks
+  long long tclk[8];
+#define DS_T(k) tclk[k] = clock64()
+#else
+#define DS_T(k)
+#endif
+  DS_T(0);
   if (lane < kPW) {
-    const int c = lane < nw ? D.idx[j0 + lane] : 0;
+    const int c = lane < nw ? D.idx[slot(lane)] : 0;
     chain_s[lane] = c;
     needx_s[lane] = lane < nw ? !D.logP_ok[c] : 0;
   }
   for (int q = lane; q < NTAB * kPW; q += 64) {
     const int t = q / kPW, w = q % kPW;
-    ivs[q] = w < nw ? D.iv[(size_t)t * W + j0 + w] : 0;
+    ivs[q] = w < nw ? D.iv[(size_t)t * W + slot(w)] : 0;
   }
   __syncthreads();
   for (int q = lane; q < kNp * kPW; q += 64) {
@@ -253,8 +264,9 @@ __global__ __launch_bounds__(64) void ds_propose(Dev D, int W, int NPAST, long l
     xs[n * kPW + w] = w < nw ? D.x[(size_t)chain_s[w] * kNp + n] : 0.0;
   }
   __syncthreads();
+  DS_T(1);
   if (lane < nw) {
-    const int j = j0 + lane;
+    const int j = slot(lane);
     const int chain = chain_s[lane];
     Rng r{D.idum[j], D.idum2[j], D.iy[j], D.iset[j], D.gset[j], D.cts[j], &ivs[lane]};
     const double* x = &xs[lane];
@@ -293,12 +305,14 @@ __global__ __launch_bounds__(64) void ds_propose(Dev D, int W, int NPAST, long l
     D.cts[j] = r.cts;
   }
   __syncthreads();
+  DS_T(2);
   // walls (:440-467): the kPW x 21 coordinates spread over all 64 lanes
   for (int q = lane; q < kNp * kPW; q += 64) {
     const int i = q / kPW, w = q % kPW;
     if (w < nw) ys[q] = hbwall::apply_wall(ys[q], P->lim_lo[i], P->lim_hi[i], P->fl_lo[i], P->fl_hi[i]);
   }
   __syncthreads();
+  DS_T(3);
   if (lane < nw) {
     double* y = &ys[lane];
     if (y[kPW] > y[0]) y[kPW] = y[0];  // "order the masses" (:470-475) as written: y[1] = y[0]
@@ -306,6 +320,7 @@ __global__ __launch_bounds__(64) void ds_propose(Dev D, int W, int NPAST, long l
     y[6 * kPW] = fmod(y[6 * kPW], P->LC_PERIOD);
   }
   __syncthreads();
+  DS_T(4);
   // prior terms: lane group g = lane / kPW takes slots i = g, g + 4, ... of walker lane % kPW
   {
     const int w = lane % kPW;
@@ -319,8 +334,9 @@ __global__ __launch_bounds__(64) void ds_propose(Dev D, int W, int NPAST, long l
     }
   }
   __syncthreads();
+  DS_T(5);
   if (lane < nw) {
-    const int j = j0 + lane;
+    const int j = slot(lane);
     double lpy = 0., lpx = 0.;
     for (int i = 0; i < kNp; ++i) {
       if (P->gpflag[i] != 1) continue;
@@ -335,12 +351,19 @@ __global__ __launch_bounds__(64) void ds_propose(Dev D, int W, int NPAST, long l
   }
   for (int q = lane; q < kNp * nw; q += 64) {
     const int w = q / kNp, n = q % kNp;
-    D.y[(size_t)j0 * kNp + q] = ys[n * kPW + w];
+    D.y[(size_t)slot(w) * kNp + n] = ys[n * kPW + w];
   }
   for (int q = lane; q < NTAB * kPW; q += 64) {
     const int t = q / kPW, w = q % kPW;
-    if (w < nw) D.iv[(size_t)t * W + j0 + w] = ivs[q];
+    if (w < nw) D.iv[(size_t)t * W + slot(w)] = ivs[q];
   }
+#ifdef HB_DS_TIMING
+  DS_T(6);
+  if (lane == 0 && iter == 100 && blockIdx.x % 32 == 0)
+    printf("propose blk %d: load %lld draws %lld walls %lld quirks %lld priors %lld store %lld\n", blockIdx.x,
+           tclk[1] - tclk[0], tclk[2] - tclk[1], tclk[3] - tclk[2], tclk[4] - tclk[3], tclk[5] - tclk[4],
+           tclk[6] - tclk[5]);
+#endif
 }
 
 // Hastings test and history (:492-546); 64 slots per block, the state and
