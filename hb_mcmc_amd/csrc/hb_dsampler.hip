@@ -104,7 +104,7 @@ struct Dev {
   int* iset;
   double* gset;
   long long* cts;
-  int* iv;         // [32][W]
+  int* iv;         // [W][32] (shuffle table row per slot)
   double* y;       // [W][21] proposals by slot
   double* logPy;   // [W]
   double* alpha2;  // [W]
@@ -155,7 +155,7 @@ __device__ double ran2(Rng& r) {
   return temp > RNMX ? RNMX : temp;
 }
 
-__device__ double gasdev(Rng& r) {
+__device__ double gasdev(Rng& r, const hbglibc::Tabs& T) {
   if (r.idum < 0) r.iset = 0;
   if (r.iset == 0) {
     double v1, v2, rsq;
@@ -164,7 +164,7 @@ __device__ double gasdev(Rng& r) {
       v2 = 2.0 * ran2(r) - 1.0;
       rsq = v1 * v1 + v2 * v2;
     } while (rsq >= 1.0 || rsq == 0.0);
-    const double fac = sqrt(-2.0 * hbglibc::log(rsq) / rsq);
+    const double fac = sqrt(-2.0 * hbglibc::log(rsq, T) / rsq);
     r.gset = v1 * fac;
     r.iset = 1;
     return v2 * fac;
@@ -174,12 +174,12 @@ __device__ double gasdev(Rng& r) {
 }
 
 // gaussian() (:1175-1178) and get_logP (:703-765)
-__device__ double gauss_pdf(double x, double mean, double sigma) {
-  return (1 / sigma / kSqrt2Pi) * hbglibc::exp(-hbglibc::pow((x - mean) / sigma, 2.) / 2.);
+__device__ double gauss_pdf(double x, double mean, double sigma, const hbglibc::Tabs& T) {
+  return (1 / sigma / kSqrt2Pi) * hbglibc::exp(-hbglibc::pow((x - mean) / sigma, 2., T) / 2., T);
 }
 
 // one term of get_logP (:703-765): log(gaussian(x_i, mean_i, sigma_i))
-__device__ double prior_term(int i, double xi) {
+__device__ double prior_term(int i, double xi, const hbglibc::Tabs& T) {
   double mean, sig;
   if (i == 7 || i == 8) { mean = 0.; sig = 1.; }
   else if (i == 9 || i == 11) { mean = 0.16; sig = 0.04; }
@@ -188,26 +188,27 @@ __device__ double prior_term(int i, double xi) {
   else if (i == 15 || i == 16) { mean = 0.; sig = 0.1; }
   else if (i == 17 || i == 18) { mean = 0.; sig = 1.; }
   else { mean = 0.; sig = 1.e15; }
-  return hbglibc::log(gauss_pdf(xi, mean, sig));
+  return hbglibc::log(gauss_pdf(xi, mean, sig, T), T);
 }
 
 // Per-lane parameter vectors live in LDS columns: v[n * kPW] is slot n.
 // gaussian_proposal_parallel (:1062-1088); dx is drawn and added in one pass
 // (the draws come in n order either way)
-__device__ void gaussian_step(const double* x, double* y, Rng& r, const Params* P, double scale, double temp) {
+__device__ void gaussian_step(const double* x, double* y, Rng& r, const Params* P, double scale, double temp,
+                              const hbglibc::Tabs& T) {
   const double sqtemp = sqrt(temp);
-  for (int n = 0; n < kNp; ++n) y[n * kPW] = x[n * kPW] + gasdev(r) * P->sigma_p[n] * sqtemp * scale;
+  for (int n = 0; n < kNp; ++n) y[n * kPW] = x[n * kPW] + gasdev(r, T) * P->sigma_p[n] * sqtemp * scale;
 }
 
 // differential_evolution_proposal_parallel (:1091-1140) as compiled (see
 // hb_sampler.cpp de_step: a == 0, the uninitialised c == 0).  The 0.9 draw
 // precedes the per-parameter Gaussians, as in the reference.
-__device__ void de_step(const double* x, double* y, Rng& r, const double* hist, int npast) {
+__device__ void de_step(const double* x, double* y, Rng& r, const double* hist, int npast, const hbglibc::Tabs& T) {
   int a = (int)(ran2(r) * npast);
   a = (int)ran2(r);
   int b = a;
   while (b == a) b = (int)(ran2(r) * npast);
-  const double g0 = gauss_pdf(0, 0, 1.e-4) - 0.5;
+  const double g0 = gauss_pdf(0, 0, 1.e-4, T) - 0.5;
   const bool scaled = ran2(r) < 0.9;
   const double gamma = 2.388 / sqrt(2. * kNp);  // GAMMA, mcmc_wrapper2.h:13
   const double* hb = hist + (size_t)b * kNp;
@@ -215,7 +216,7 @@ __device__ void de_step(const double* x, double* y, Rng& r, const double* hist, 
   for (int n = 0; n < kNp; ++n) {
     double dx = hb[n] - ha[n];
     const double eps = dx * g0;
-    if (scaled) dx *= gasdev(r) * gamma;
+    if (scaled) dx *= gasdev(r, T) * gamma;
     dx += eps;
     y[n * kPW] = x[n * kPW] + dx;
   }
@@ -234,7 +235,9 @@ __global__ __launch_bounds__(64) void ds_propose(Dev D, int W, int NPAST, long l
   __shared__ double xs[kNp * kPW], ys[kNp * kPW];
   __shared__ double terms[2][kNp][kPW];
   __shared__ int chain_s[kPW], needx_s[kPW];
+  __shared__ uint64_t tab_s[hbglibc::kTabWords];  // exp / log / pow tables (divergent lookups)
   const Params* P = D.P;
+  const hbglibc::Tabs T{tab_s, tab_s + 256, tab_s + 512};
   const int lane = threadIdx.x;
   // slots blockIdx.x + w gridDim.x (w < kPW): each wave mixes ladder rungs, so
   // the hot chains' long wall runs spread over the waves instead of piling up
@@ -254,9 +257,18 @@ __global__ __launch_bounds__(64) void ds_propose(Dev D, int W, int NPAST, long l
     chain_s[lane] = c;
     needx_s[lane] = lane < nw ? !D.logP_ok[c] : 0;
   }
-  for (int q = lane; q < NTAB * kPW; q += 64) {
-    const int t = q / kPW, w = q % kPW;
-    ivs[q] = w < nw ? D.iv[(size_t)t * W + slot(w)] : 0;
+  {
+    const hbglibc::Tabs C = hbglibc::const_tabs();
+    for (int q = lane; q < 256; q += 64) {
+      tab_s[q] = C.exp[q];
+      tab_s[256 + q] = C.log[q];
+      tab_s[512 + q] = C.pow[q];
+      tab_s[768 + q] = C.pow[256 + q];
+    }
+  }
+  for (int q = lane; q < NTAB * kPW; q += 64) {  // one 128-B row per slot
+    const int w = q / NTAB, t = q % NTAB;
+    ivs[t * kPW + w] = w < nw ? D.iv[(size_t)slot(w) * NTAB + t] : 0;
   }
   __syncthreads();
   for (int q = lane; q < kNp * kPW; q += 64) {
@@ -273,11 +285,11 @@ __global__ __launch_bounds__(64) void ds_propose(Dev D, int W, int NPAST, long l
     double* y = &ys[lane];
     const double temp = D.temp[j];
     const double a = ran2(r);
-    const double jscale = hbglibc::pow(10., -6. + 6. * a);
+    const double jscale = hbglibc::pow(10., -6. + 6. * a, T);
     int jmp = 0, jt = 0;
     if ((ran2(r) < 0.5) && (iter > NPAST)) jmp = 1;
     if (jmp == 0) {
-      gaussian_step(x, y, r, P, jscale, temp);
+      gaussian_step(x, y, r, P, jscale, temp, T);
       jt = 1;
     }
     if (jmp == 1) {
@@ -285,12 +297,12 @@ __global__ __launch_bounds__(64) void ds_propose(Dev D, int W, int NPAST, long l
         D.DEtrial_arr[j]++;
         atomicAdd((unsigned long long*)&D.ctr->DEtrial_tot, 1ull);
       }
-      de_step(x, y, r, &D.hist[(size_t)j * NPAST * kNp], NPAST);
+      de_step(x, y, r, &D.hist[(size_t)j * NPAST * kNp], NPAST, T);
       jt = 2;
       double dx_mag = 0;
       for (int i = 0; i < kNp; ++i) dx_mag += (x[i * kPW] - y[i * kPW]) * (x[i * kPW] - y[i * kPW]);
       if (dx_mag < 1e-6) {
-        gaussian_step(x, y, r, P, jscale, temp);
+        gaussian_step(x, y, r, P, jscale, temp, T);
         jt = 1;
       }
     }
@@ -329,8 +341,8 @@ __global__ __launch_bounds__(64) void ds_propose(Dev D, int W, int NPAST, long l
 #ifdef HB_DS_ABL_NOPRIOR  // experiment builds only (timing ablation)
       terms[0][i][w] = 0.0; terms[1][i][w] = 0.0; continue;
 #endif
-      terms[0][i][w] = prior_term(i, ys[i * kPW + w]);
-      if (needx_s[w]) terms[1][i][w] = prior_term(i, xs[i * kPW + w]);  // :444, first use of a state
+      terms[0][i][w] = prior_term(i, ys[i * kPW + w], T);
+      if (needx_s[w]) terms[1][i][w] = prior_term(i, xs[i * kPW + w], T);  // :444, first use of a state
     }
   }
   __syncthreads();
@@ -354,8 +366,8 @@ __global__ __launch_bounds__(64) void ds_propose(Dev D, int W, int NPAST, long l
     D.y[(size_t)slot(w) * kNp + n] = ys[n * kPW + w];
   }
   for (int q = lane; q < NTAB * kPW; q += 64) {
-    const int t = q / kPW, w = q % kPW;
-    if (w < nw) D.iv[(size_t)t * W + slot(w)] = ivs[q];
+    const int w = q / NTAB, t = q % NTAB;
+    if (w < nw) D.iv[(size_t)slot(w) * NTAB + t] = ivs[t * kPW + w];
   }
 #ifdef HB_DS_TIMING
   DS_T(6);
@@ -456,7 +468,10 @@ __global__ __launch_bounds__(kSwapThreads) void ds_swap(Dev D, int W, const Swap
   extern __shared__ __align__(16) unsigned char smem[];
   __shared__ int nacc_s;
   __shared__ int off_s[kMaxLevels + 1];
+  __shared__ uint64_t exp_s[256];  // exp table for the divergent lookups of the level loop
   const int tid = threadIdx.x;
+  for (int q = tid; q < 256; q += kSwapThreads) exp_s[q] = hbglibc::kExpTab[q];
+  const hbglibc::Tabs T{exp_s, hbglibc::kLogTab, hbglibc::kPowTab};
   const bool off_lds = nlv <= kMaxLevels;
   const SwapEnt* S = sched;
   const double* L = D.logL;
@@ -493,7 +508,7 @@ __global__ __launch_bounds__(kSwapThreads) void ds_swap(Dev D, int W, const Swap
       const int olda = idx.ld(a), oldb = idx.ld(b);
       const double dlogL = L[oldb] - L[olda];
       const double Hs = hs[b];  // (temp[b] - temp[a]) / (temp[b] temp[a]), fixed ladder (:803)
-      const double al = hbglibc::exp(dlogL * Hs);
+      const double al = hbglibc::exp(dlogL * Hs, T);
       if (al >= be) {
         idx.st(a, oldb);
         idx.st(b, olda);
@@ -694,7 +709,7 @@ extern "C" hb_dsampler* hb_dsampler_create(hb_sampler* s, hb_ctx* ctx) {
   d->cnt.resize(W + 2);
   // schedule, logL, pair factors and index[] in LDS when they fit (160 KB per CU on gfx950)
   d->swap_lds = (sizeof(SwapEnt) + 2 * sizeof(double) + sizeof(int)) * Wz;
-  d->lds_swap = d->swap_lds <= 158 * 1024;
+  d->lds_swap = d->swap_lds <= 150 * 1024;  // + ~3 KB of static LDS
   if (d->lds_swap) {
     e = hipFuncSetAttribute((const void*)ds_swap<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)d->swap_lds);
@@ -747,7 +762,7 @@ static int ds_upload(hb_dsampler* d) {
     iset[j] = r.iset;
     gset[j] = r.gset;
     cts[j] = r.cts;
-    for (int t = 0; t < NTAB; ++t) iv[(size_t)t * W + j] = (int)r.iv[t];
+    for (int t = 0; t < NTAB; ++t) iv[(size_t)j * NTAB + t] = (int)r.iv[t];
   }
   Counters c{};
   c.acc = *v.acc;
@@ -837,7 +852,7 @@ extern "C" int hb_dsampler_download(hb_dsampler* d) {
     r.iset = iset[j];
     r.gset = gset[j];
     r.cts = cts[j];
-    for (int t = 0; t < NTAB; ++t) r.iv[t] = iv[(size_t)t * W + j];
+    for (int t = 0; t < NTAB; ++t) r.iv[t] = iv[(size_t)j * NTAB + t];
     v.acc_arr[j] = 0;  // cleared by every accept step (hb_sampler_accept)
   }
   const Counters& c = *d->h_ctr;

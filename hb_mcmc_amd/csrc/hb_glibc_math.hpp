@@ -42,6 +42,16 @@ HBG_TABLE uint64_t kLogTab[256] = HBG_LOG_TAB;
 HBG_TABLE uint64_t kPowHead[9] = HBG_POW_HEAD;
 HBG_TABLE uint64_t kPowTab[512] = HBG_POW_TAB;
 
+// the three data tables, by pointer: the defaults live in constant memory;
+// a kernel that calls these functions on every lane may stage them in LDS
+// (8 KiB) to take the divergent table loads off the L2 round trip
+struct Tabs {
+  const uint64_t* exp;  // 256
+  const uint64_t* log;  // 256
+  const uint64_t* pow;  // 512
+};
+constexpr int kTabWords = 256 + 256 + 512;
+
 HBG_FN double asdouble(uint64_t u) { return __builtin_bit_cast(double, u); }
 HBG_FN uint64_t asuint64(double d) { return __builtin_bit_cast(uint64_t, d); }
 HBG_FN double ld(const uint64_t* t, int i) { return asdouble(t[i]); }
@@ -83,7 +93,7 @@ HBG_FN double exp_special(double tmp, uint64_t sbits, uint64_t ki) {
   return 0x1p-1022 * y;
 }
 
-HBG_FN double exp(double x) {
+HBG_FN double exp(double x, const Tabs& T) {
   const uint64_t ix = asuint64(x);
   uint32_t abstop = (uint32_t)(ix >> 52) & 0x7ff;
   if (abstop - 0x3c9u >= 0x3fu) {  // |x| < 2^-54, |x| >= 512, inf, nan
@@ -102,8 +112,8 @@ HBG_FN double exp(double x) {
   r = __builtin_fma(kd, HBG_NEGLN2LON, r);
   const int idx = 2 * (int)(ki % 128);
   const uint64_t top = ki << 45;
-  const double tail = asdouble(kExpTab[idx]);
-  const uint64_t sbits = kExpTab[idx + 1] + top;
+  const double tail = asdouble(T.exp[idx]);
+  const uint64_t sbits = T.exp[idx + 1] + top;
   const double r2 = r * r;
   const double p23 = __builtin_fma(r, HBG_C3, HBG_C2);
   const double p45 = __builtin_fma(r, HBG_C5, HBG_C4);
@@ -116,7 +126,7 @@ HBG_FN double exp(double x) {
 // ---------------------------------------------------------------------------
 // log (e_log.c): log(x) = k ln2 + log(c) + log1p(z/c - 1)
 // ---------------------------------------------------------------------------
-HBG_FN double log(double x) {
+HBG_FN double log(double x, const Tabs& T) {
   uint64_t ix = asuint64(x);
   const uint32_t top = (uint32_t)(ix >> 48);
   if (ix - 0x3fee000000000000ull < 0x3090000000000ull) {  // x in [1 - 2^-4, 1 + 0x1.09p-4)
@@ -157,7 +167,7 @@ HBG_FN double log(double x) {
   const int i = (int)((tmp >> 45) % 128);
   const int k = (int)((int64_t)tmp >> 52);
   const uint64_t iz = ix - (tmp & (0xfffull << 52));
-  const double invc = ld(kLogTab, 2 * i), logc = ld(kLogTab, 2 * i + 1);
+  const double invc = ld(T.log, 2 * i), logc = ld(T.log, 2 * i + 1);
   const double z = asdouble(iz);
   const double kd = (double)k;
   const double Ln2hi = ld(kLogHead, 0), Ln2lo = ld(kLogHead, 1);
@@ -180,14 +190,14 @@ HBG_FN double log(double x) {
 // ---------------------------------------------------------------------------
 // pow (e_pow.c): exp(y log x) with a double-double log
 // ---------------------------------------------------------------------------
-HBG_FN double pow_log_inline(uint64_t ix, double* tail) {
+HBG_FN double pow_log_inline(uint64_t ix, double* tail, const Tabs& T) {
   const uint64_t tmp = ix - 0x3fe6955500000000ull;
   const int i = (int)((tmp >> 45) % 128);
   const int k = (int)((int64_t)tmp >> 52);
   const uint64_t iz = ix - (tmp & (0xfffull << 52));
   const double z = asdouble(iz);
   const double kd = (double)k;
-  const double invc = ld(kPowTab, 4 * i), logc = ld(kPowTab, 4 * i + 2), logctail = ld(kPowTab, 4 * i + 3);
+  const double invc = ld(T.pow, 4 * i), logc = ld(T.pow, 4 * i + 2), logctail = ld(T.pow, 4 * i + 3);
   const double Ln2hi = ld(kPowHead, 0), Ln2lo = ld(kPowHead, 1);
   const double A0 = ld(kPowHead, 2), A1 = ld(kPowHead, 3), A2 = ld(kPowHead, 4), A3 = ld(kPowHead, 5),
                A4 = ld(kPowHead, 6), A5 = ld(kPowHead, 7), A6 = ld(kPowHead, 8);
@@ -233,7 +243,7 @@ HBG_FN double pow_exp_special(double tmp, uint64_t sbits, uint64_t ki) {
   return 0x1p-1022 * y;
 }
 
-HBG_FN double pow_exp_inline(double x, double xtail, uint32_t sign_bias) {
+HBG_FN double pow_exp_inline(double x, double xtail, uint32_t sign_bias, const Tabs& T) {
   const uint64_t ix = asuint64(x);
   uint32_t abstop = (uint32_t)(ix >> 52) & 0x7ff;
   if (abstop - 0x3c9u >= 0x3fu) {
@@ -252,8 +262,8 @@ HBG_FN double pow_exp_inline(double x, double xtail, uint32_t sign_bias) {
   r = xtail + r;
   const int idx = 2 * (int)(ki % 128);
   const uint64_t top = (ki + sign_bias) << 45;
-  const double tail = asdouble(kExpTab[idx]);
-  const uint64_t sbits = kExpTab[idx + 1] + top;
+  const double tail = asdouble(T.exp[idx]);
+  const uint64_t sbits = T.exp[idx + 1] + top;
   const double r2 = r * r;
   const double p23 = __builtin_fma(r, HBG_C3, HBG_C2);
   const double p45 = __builtin_fma(r, HBG_C5, HBG_C4);
@@ -275,7 +285,7 @@ HBG_FN int checkint(uint64_t iy) {
 
 HBG_FN bool zeroinfnan(uint64_t i) { return 2 * i - 1 >= 2 * 0x7ff0000000000000ull - 1; }
 
-HBG_FN double pow(double x, double y) {
+HBG_FN double pow(double x, double y, const Tabs& T) {
   uint32_t sign_bias = 0;
   uint64_t ix = asuint64(x);
   const uint64_t iy = asuint64(y);
@@ -314,10 +324,16 @@ HBG_FN double pow(double x, double y) {
     }
   }
   double lo;
-  const double hi = pow_log_inline(ix, &lo);
+  const double hi = pow_log_inline(ix, &lo, T);
   const double ehi = y * hi;
   const double elo = __builtin_fma(y, lo, __builtin_fma(y, hi, -ehi));
-  return pow_exp_inline(ehi, elo, sign_bias);
+  return pow_exp_inline(ehi, elo, sign_bias, T);
 }
+
+// the same functions with the constant-memory tables
+HBG_FN Tabs const_tabs() { return Tabs{kExpTab, kLogTab, kPowTab}; }
+HBG_FN double exp(double x) { return exp(x, const_tabs()); }
+HBG_FN double log(double x) { return log(x, const_tabs()); }
+HBG_FN double pow(double x, double y) { return pow(x, y, const_tabs()); }
 
 }  // namespace hbglibc
