@@ -65,6 +65,9 @@ def parse():
     ap.add_argument("--event-every", type=int, default=10,
                     help="bracket every k-th timed step's kernels with HIP events (an event pair costs "
                          "~5 us of stream time on this runtime; 1 = every step)")
+    ap.add_argument("--sampler-iters", type=int, default=100,
+                    help="also time the whole PT-MCMC iteration (mcmc_wrapper2.c loop) at the workload's W and N: "
+                         "device-resident sampler vs the host sampler + GPU likelihood (0 = skip)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
                     help="per-launch HBM bytes measured by rocprofv3 --pmc (see profiles/README.md)")
     return ap.parse_args()
@@ -151,6 +154,53 @@ class _HipEvent:
     def __del__(self):
         if getattr(self, "h", None):
             self._lib.hb_timer_destroy(self.h)
+
+
+def sampler_e2e(L, w, iters, warm=20):
+    """Whole PT-MCMC iterations per second on this light curve: the device-
+    resident loop (hb_dsampler: proposals, walls, priors, likelihood, Hastings,
+    history, tempering swaps as kernels) and the host loop (16 threads) driving
+    the same GPU likelihood.  Both are bit-identical to the reference's
+    bookkeeping (tests/test_dsampler.py); 50-rung ladder repeated (W > 2000)."""
+    from hb_mcmc_amd.dsampler import DeviceSampler
+    from hb_mcmc_amd.sampler import SlotSampler
+
+    logp = float(synth.THETA_STAR[2])
+    out = {"walkers": w, "iters_timed": iters, "unit": "walker-steps/s (1 likelihood eval each)"}
+    S = SlotSampler(warm + iters, w, logp, 0, w, run=0, npast=500, ladder=1, nthreads=16)
+    with DeviceSampler(S, L) as D:
+        D.init_logl()
+        for it in range(warm):
+            D.step(it)
+        D.sync()
+        t0 = time.perf_counter()
+        for it in range(warm, warm + iters):
+            D.step(it)
+        D.sync()
+        dt = time.perf_counter() - t0
+    out["device_loop"] = {"ms_per_iter": dt / iters * 1e3, "value": w * iters / dt}
+    S.close()
+    S = SlotSampler(warm + iters, w, logp, 0, w, run=0, npast=500, ladder=1, nthreads=16)
+    x, _, _ = S.get()
+    S.set_logl(L.loglike(x))
+
+    def host_iter(it):
+        y = S.propose(it)
+        S.accept(it, L.loglike(y))
+        _, ll, _ = S.get()
+        perm, _ = S.swap(ll)
+        S.apply_perm(perm)
+        S.end_iter(it)
+
+    for it in range(warm):
+        host_iter(it)
+    t0 = time.perf_counter()
+    for it in range(warm, warm + iters):
+        host_iter(it)
+    dt = time.perf_counter() - t0
+    out["host_loop_16_threads"] = {"ms_per_iter": dt / iters * 1e3, "value": w * iters / dt}
+    S.close()
+    return out
 
 
 def make_event(kind):
@@ -348,6 +398,8 @@ def main():
             "kernel_only_evals_per_s": w / ((eval_ms + prep_ms) * 1e-3),
             "nonfinite_logl_last_batch": nonfinite,
         }
+        if world == 1 and a.sampler_iters > 0:
+            line["sampler_end_to_end"] = sampler_e2e(L, w, a.sampler_iters)
         if world == 1 and not a.no_cpu_baseline:
             line["cpu_baseline"] = run_cpu_baseline(n, a.cpu_seconds)
         print(json.dumps(line), flush=True)
