@@ -371,6 +371,9 @@ __device__ __forceinline__ void model_pass(const double* __restrict__ t, const d
     for (int k = 0; k < K; ++k) v[k] = tk[k] * w.kb + w.kr0;
     bad = false;
 #else
+#if HB_SPLIT_LIVE
+    __asm__ volatile("" ::: "memory");  // walker constants reloaded per tile (see hb_cadence_flux_k)
+#endif
     hb_cadence_flux_k<K>(tk, pk, tab, w, v, bad);
 #endif
     if (__any(bad)) {  // out-of-domain angles: reference-order ocml path
