@@ -41,13 +41,19 @@ namespace hbds {
 constexpr int kNp = 21;
 constexpr int NTAB = 32;
 constexpr int IM1 = 2147483563, IM2 = 2147483399, IMM1 = IM1 - 1;
-constexpr int IA1 = 40014, IA2 = 40692, IQ1 = 53668, IQ2 = 52774, IR1 = 12211, IR2 = 3791;
+constexpr int IA1 = 40014, IA2 = 40692, IQ1 = 53668, IR1 = 12211;  // IQ2/IR2: idum2 advances by jump-ahead
 constexpr int NDIV = 1 + IMM1 / NTAB;
 constexpr double AM = 1.0 / IM1;
 constexpr double RNMX = 1.0 - 1.2e-7;
 constexpr double kSqrt2Pi = 2.5066282746;  // mcmc_wrapper2.h:10
 constexpr int kBlk = 64;                   // slots per workgroup of the gather kernel
-constexpr int kPW = 4;                     // slots per propose wave (lanes 0..3 draw, 64 share walls and priors)
+#ifndef HB_DS_ABL  // experiment builds only: timing ablations of ds_propose (results are wrong)
+#define HB_DS_ABL 0
+#endif
+#ifndef HB_DS_KPW
+#define HB_DS_KPW 4
+#endif
+constexpr int kPW = HB_DS_KPW;             // propose waves (one slot each) per workgroup
 constexpr int kSwapThreads = 1024;
 constexpr int kMaxLevels = 255;            // swap levels staged in LDS (W = 4096 needs ~10)
 constexpr int kEvCap = 1024;               // big-jump records between drains (<= 6 per iteration)
@@ -119,59 +125,142 @@ struct Dev {
 };
 
 // ---------------------------------------------------------------------------
-// ran2_parallel / gasdev2_parallel (:894-974), one slot per lane
+// ran2_parallel / gasdev2_parallel (:894-974) for one slot per wave
 // ---------------------------------------------------------------------------
-struct Rng {
-  int idum, idum2, iy, iset;
-  double gset;
-  long long cts;
-  int* iv;  // LDS column, stride kPW (ds_propose)
-};
-
-__device__ double ran2(Rng& r) {
-  r.cts += 1;
-  if (r.idum <= 0) {
-    r.idum = (-(r.idum) < 1) ? 1 : -(r.idum);
-    r.idum2 = r.idum;
-    for (int j = NTAB + 7; j >= 0; --j) {
-      const int k = r.idum / IQ1;
-      r.idum = IA1 * (r.idum - k * IQ1) - k * IR1;
-      if (r.idum < 0) r.idum += IM1;
-      if (j < NTAB) r.iv[j * kPW] = r.idum;
-    }
-    r.iy = r.iv[0];
-  }
-  int k = r.idum / IQ1;
-  r.idum = IA1 * (r.idum - k * IQ1) - k * IR1;
-  if (r.idum < 0) r.idum += IM1;
-  k = r.idum2 / IQ2;
-  r.idum2 = IA2 * (r.idum2 - k * IQ2) - k * IR2;
-  if (r.idum2 < 0) r.idum2 += IM2;
-  const int j = r.iy / NDIV;
-  r.iy = r.iv[j * kPW] - r.idum2;
-  r.iv[j * kPW] = r.idum;
-  if (r.iy < 1) r.iy += IMM1;
-  const double temp = AM * (double)r.iy;
+// The stream of a slot is a fixed sequence of integers; which draws become
+// uniforms, polar attempts or DE indices only decides how many are consumed.
+// ran2 is two L'Ecuyer LCGs plus a Bays-Durham shuffle.  The LCG terms of
+// draw base + k come lane-parallel by jump-ahead (lane k multiplies the base
+// state by IA^(k+1) mod IM, a constant table); Schrage's product (:919-925)
+// is the exact residue, and so is the modular product here.  Only the shuffle
+// (iy -> table slot -> iy) is serial: it runs in scalar registers with the
+// 32-entry table in one VGPR (lane t = iv[t], read by v_readlane, written by
+// a lane select), on demand, into a 64-draw window (lane k = draw base + k).
+// The transforms then run lane-parallel: up to 32 polar attempts at once,
+// log / sqrt / division only on the accepted ones.  The state handed back is
+// the state after exactly the consumed draws: the table at the window base is
+// advanced by replaying the consumed draws' writes (slot iy_(k-1) / NDIV,
+// value idum_k).
+__device__ __forceinline__ int rl(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
+// lane l of old := v (uniform v, l); a compare + select, so the compiler owns the SGPR hazards
+__device__ __forceinline__ int wl(int v, int l, int old) { return (int)(threadIdx.x & 63) == l ? v : old; }
+__device__ __forceinline__ double rld(double v, int l) {
+  const uint64_t u = __builtin_bit_cast(uint64_t, v);
+  const uint32_t lo = (uint32_t)rl((int)(uint32_t)u, l), hi = (uint32_t)rl((int)(uint32_t)(u >> 32), l);
+  return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+__device__ __forceinline__ int shfli(int v, int src) { return __builtin_amdgcn_ds_bpermute(src << 2, v); }
+__device__ __forceinline__ double uni_of(int iy) {  // ran2's return value (:940-941)
+  const double temp = AM * (double)iy;
   return temp > RNMX ? RNMX : temp;
 }
+__device__ __forceinline__ int ndiv(int iy) { return (int)((unsigned)iy / (unsigned)NDIV); }  // iy >= 1
 
-__device__ double gasdev(Rng& r, const hbglibc::Tabs& T) {
-  if (r.idum < 0) r.iset = 0;
-  if (r.iset == 0) {
-    double v1, v2, rsq;
-    do {
-      v1 = 2.0 * ran2(r) - 1.0;
-      v2 = 2.0 * ran2(r) - 1.0;
-      rsq = v1 * v1 + v2 * v2;
-    } while (rsq >= 1.0 || rsq == 0.0);
-    const double fac = sqrt(-2.0 * hbglibc::log(rsq, T) / rsq);
-    r.gset = v1 * fac;
-    r.iset = 1;
-    return v2 * fac;
+// IA^(k+1) mod IM, k < 64, for both generators
+struct LcgPow {
+  int a1[64], a2[64];
+};
+constexpr LcgPow make_lcg_pow() {
+  LcgPow t{};
+  long long p1 = 1, p2 = 1;
+  for (int k = 0; k < 64; ++k) {
+    p1 = p1 * IA1 % IM1;
+    p2 = p2 * IA2 % IM2;
+    t.a1[k] = (int)p1;
+    t.a2[k] = (int)p2;
   }
-  r.iset = 0;
-  return r.gset;
+  return t;
 }
+__constant__ LcgPow kLcgPow = make_lcg_pow();
+
+// a * z mod (2^31 - c) for 0 <= a, z < 2^31 - c: two folds of the high bits
+// (2^31 = c mod m), one conditional subtraction
+template <unsigned C>
+__device__ __forceinline__ int mulmod31(int a, int z) {
+  uint64_t x = (uint64_t)(uint32_t)a * (uint32_t)z;
+  x = (x >> 31) * C + (x & 0x7fffffffu);
+  x = (x >> 31) * C + (x & 0x7fffffffu);
+  uint32_t r = (uint32_t)x;
+  const uint32_t m = 0x80000000u - C;
+  if (r >= m) r -= m;
+  return (int)r;
+}
+static_assert(IM1 == 2147483648LL - 85 && IM2 == 2147483648LL - 249, "moduli are 2^31 - c");
+
+struct WaveStream {
+  // window base: the state after the last consumed draw (wave-uniform; table in a VGPR)
+  int b_idum, b_idum2, b_iy, b_tab;
+  // generator head: the shuffle state after draw base + gend - 1
+  int g_iy, g_tab;
+  // lane k: LCG states (idum, idum2) of draw base + k (all lanes) and its iy (k < gend)
+  int w_idum, w_idum2, w_iy;
+  int gend;            // generated draws in the window
+  int cur;             // next unconsumed lane (uniform)
+  long long consumed;  // draws consumed this kernel (cts increment)
+
+  __device__ void jump() {  // LCG lanes from the base state
+    const int k = threadIdx.x & 63;
+    w_idum = mulmod31<85>(kLcgPow.a1[k], b_idum);
+    w_idum2 = mulmod31<249>(kLcgPow.a2[k], b_idum2);
+  }
+  __device__ void gen_to(int n) {  // the serial shuffle for lanes gend .. n-1
+    for (int k = gend; k < n; ++k) {
+      const int j = ndiv(g_iy);
+      g_iy = rl(g_tab, j) - rl(w_idum2, k);
+      g_tab = wl(rl(w_idum, k), j, g_tab);
+      if (g_iy < 1) g_iy += IMM1;
+      w_iy = wl(g_iy, k, w_iy);
+    }
+    if (n > gend) gend = n;
+  }
+  // start from (idum, idum2, iy, table); the table initialisation of
+  // :905-916 runs here when idum <= 0 (a propose always consumes draws)
+  __device__ void init(int idum, int idum2, int iy, int tab) {
+    if (idum <= 0) {
+      idum = (-idum < 1) ? 1 : -idum;
+      idum2 = idum;
+      for (int j = NTAB + 7; j >= 0; --j) {
+        const int q = idum / IQ1;
+        idum = IA1 * (idum - q * IQ1) - q * IR1;
+        if (idum < 0) idum += IM1;
+        if (j < NTAB) tab = wl(idum, j, tab);
+      }
+      iy = rl(tab, 0);
+    }
+    b_idum = idum;
+    b_idum2 = idum2;
+    g_iy = b_iy = iy;
+    g_tab = b_tab = tab;
+    w_iy = 0;
+    gend = cur = 0;
+    consumed = 0;
+    jump();
+  }
+  // retire lanes 0..cur-1: the base state advances past them, the window slides down
+  __device__ void slide() {
+    const int s = cur;
+    if (s == 0) return;
+    int prev = b_iy;
+    for (int k = 0; k < s; ++k) {
+      b_tab = wl(rl(w_idum, k), ndiv(prev), b_tab);
+      prev = rl(w_iy, k);
+    }
+    b_iy = prev;
+    b_idum = rl(w_idum, s - 1);
+    b_idum2 = rl(w_idum2, s - 1);
+    w_iy = shfli(w_iy, min((int)(threadIdx.x & 63) + s, 63));
+    gend -= s;
+    consumed += s;
+    cur = 0;
+    jump();
+  }
+  __device__ double uniform() {  // one ran2() call
+    if (cur == 64) slide();
+    if (cur >= gend) gen_to(min(64, cur + 8));
+    return uni_of(rl(w_iy, cur++));
+  }
+  __device__ int idum_now() const { return cur == 0 ? b_idum : rl(w_idum, cur - 1); }
+};
 
 // gaussian() (:1175-1178) and get_logP (:703-765)
 __device__ double gauss_pdf(double x, double mean, double sigma, const hbglibc::Tabs& T) {
@@ -191,191 +280,190 @@ __device__ double prior_term(int i, double xi, const hbglibc::Tabs& T) {
   return hbglibc::log(gauss_pdf(xi, mean, sig, T), T);
 }
 
-// Per-lane parameter vectors live in LDS columns: v[n * kPW] is slot n.
-// gaussian_proposal_parallel (:1062-1088); dx is drawn and added in one pass
-// (the draws come in n order either way)
-__device__ void gaussian_step(const double* x, double* y, Rng& r, const Params* P, double scale, double temp,
-                              const hbglibc::Tabs& T) {
-  const double sqtemp = sqrt(temp);
-  for (int n = 0; n < kNp; ++n) y[n * kPW] = x[n * kPW] + gasdev(r, T) * P->sigma_p[n] * sqtemp * scale;
-}
-
-// differential_evolution_proposal_parallel (:1091-1140) as compiled (see
-// hb_sampler.cpp de_step: a == 0, the uninitialised c == 0).  The 0.9 draw
-// precedes the per-parameter Gaussians, as in the reference.
-__device__ void de_step(const double* x, double* y, Rng& r, const double* hist, int npast, const hbglibc::Tabs& T) {
-  int a = (int)(ran2(r) * npast);
-  a = (int)ran2(r);
-  int b = a;
-  while (b == a) b = (int)(ran2(r) * npast);
-  const double g0 = gauss_pdf(0, 0, 1.e-4, T) - 0.5;
-  const bool scaled = ran2(r) < 0.9;
-  const double gamma = 2.388 / sqrt(2. * kNp);  // GAMMA, mcmc_wrapper2.h:13
-  const double* hb = hist + (size_t)b * kNp;
-  const double* ha = hist + (size_t)a * kNp;
-  for (int n = 0; n < kNp; ++n) {
-    double dx = hb[n] - ha[n];
-    const double eps = dx * g0;
-    if (scaled) dx *= gasdev(r, T) * gamma;
-    dx += eps;
-    y[n * kPW] = x[n * kPW] + dx;
+// kNp successive gasdev2_parallel() values (:947-974); lane n < kNp gets
+// value n.  iset/gset are the slot's Gaussian carry (wave-uniform).  Each
+// round tests up to 32 polar attempts (draws 2m, 2m+1 of the window) at once.
+__device__ double gauss_batch(WaveStream& S, int& iset, double& gset, const hbglibc::Tabs& T, double* gs) {
+  const int lane = threadIdx.x & 63;
+  int pos = 0;
+  if (S.idum_now() < 0) iset = 0;  // :951
+  if (iset) {
+    if (lane == 0) gs[0] = gset;
+    pos = 1;
+    iset = 0;
   }
+  while (pos < kNp && HB_DS_ABL != 3) {
+    S.slide();
+    const int need = (kNp - pos + 1) / 2;          // pairs still to generate
+    const int att = min(32, need + need / 2 + 2);  // attempts tested this round (acceptance pi/4)
+    S.gen_to(2 * att);
+    const int m = lane & 31;
+    const double v1 = 2.0 * uni_of(shfli(S.w_iy, 2 * m)) - 1.0;
+    const double v2 = 2.0 * uni_of(shfli(S.w_iy, 2 * m + 1)) - 1.0;
+    const double rsq = v1 * v1 + v2 * v2;
+    const bool ok = lane < att && !(rsq >= 1.0 || rsq == 0.0);
+    const uint64_t mask = __ballot(ok);
+    const int avail = __popcll(mask);
+    const int take = min(need, avail);
+    const int rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0));
+    double g1 = 0.0;
+    if (ok && rank < take) {
+      const double fac = sqrt(-2.0 * hbglibc::log(rsq, T) / rsq);
+      g1 = v1 * fac;
+      const int o = pos + 2 * rank;
+      gs[o] = v2 * fac;
+      if (o + 1 < kNp) gs[o + 1] = g1;
+    }
+    if (take > 0) {
+      // lane of the take-th accepted attempt: its v1 * fac is the new gset
+      uint64_t mm = mask;
+      for (int r = 1; r < take; ++r) mm &= mm - 1;
+      const int last = __builtin_ctzll(mm);
+      gset = rld(g1, last);
+      S.cur = (take == need) ? 2 * (last + 1) : 2 * att;
+      const int got = 2 * take;
+      if (take == need && pos + got > kNp) iset = 1;  // the last pair's v1 * fac is carried
+      pos += got;
+    } else {
+      S.cur = 2 * att;
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  return lane < kNp ? gs[lane] : 0.0;
 }
-
 
 // ---------------------------------------------------------------------------
 // kernels
 // ---------------------------------------------------------------------------
-// proposals (:386-485) for kPW slots per wave: lanes 0..kPW-1 run the slots'
-// random streams (inherently sequential per slot), then all 64 lanes share
-// the prior terms (4 lanes per slot), summed per slot in the reference's
-// order.  Vectors and shuffle tables are staged in LDS; y leaves coalesced.
-__global__ __launch_bounds__(64) void ds_propose(Dev D, int W, int NPAST, long long iter) {
-  __shared__ int ivs[NTAB * kPW];
-  __shared__ double xs[kNp * kPW], ys[kNp * kPW];
-  __shared__ double terms[2][kNp][kPW];
-  __shared__ int chain_s[kPW], needx_s[kPW];
+// proposals (:386-485), one slot per wave, kPW waves per workgroup sharing the
+// LDS copy of the exp/log/pow tables.  Lane n < 21 holds coordinate n of x
+// and y; walls and prior terms run one coordinate per lane.  Slots are
+// interleaved over the workgroup's waves (slot = block + w * grid) so the
+// hot rungs' wall runs spread over the machine.
+__global__ __launch_bounds__(64 * kPW) void ds_propose(Dev D, int W, int NPAST, long long iter) {
   __shared__ uint64_t tab_s[hbglibc::kTabWords];  // exp / log / pow tables (divergent lookups)
+  __shared__ double gs_s[kPW][32];
   const Params* P = D.P;
   const hbglibc::Tabs T{tab_s, tab_s + 256, tab_s + 512};
-  const int lane = threadIdx.x;
-  // slots blockIdx.x + w gridDim.x (w < kPW): each wave mixes ladder rungs, so
-  // the hot chains' long wall runs spread over the waves instead of piling up
-  // in the blocks of the hottest rungs
-  const int G = gridDim.x;
-  auto slot = [&](int w) { return (int)blockIdx.x + w * G; };
-  const int nw = (W - (int)blockIdx.x + G - 1) / G;  // valid w are 0 .. nw-1 (nw <= kPW)
-#ifdef HB_DS_TIMING  // experiment builds only: per-phase shader clocks of a few blocks
-  long long tclk[8];
-#define DS_T(k) tclk[k] = clock64()
-#else
-#define DS_T(k)
-#endif
-  DS_T(0);
-  if (lane < kPW) {
-    const int c = lane < nw ? D.idx[slot(lane)] : 0;
-    chain_s[lane] = c;
-    needx_s[lane] = lane < nw ? !D.logP_ok[c] : 0;
-  }
   {
     const hbglibc::Tabs C = hbglibc::const_tabs();
-    for (int q = lane; q < 256; q += 64) {
+    for (int q = threadIdx.x; q < 256; q += 64 * kPW) {
       tab_s[q] = C.exp[q];
       tab_s[256 + q] = C.log[q];
       tab_s[512 + q] = C.pow[q];
       tab_s[768 + q] = C.pow[256 + q];
     }
   }
-  for (int q = lane; q < NTAB * kPW; q += 64) {  // one 128-B row per slot
-    const int w = q / NTAB, t = q % NTAB;
-    ivs[t * kPW + w] = w < nw ? D.iv[(size_t)slot(w) * NTAB + t] : 0;
-  }
   __syncthreads();
-  for (int q = lane; q < kNp * kPW; q += 64) {
-    const int w = q / kNp, n = q % kNp;
-    xs[n * kPW + w] = w < nw ? D.x[(size_t)chain_s[w] * kNp + n] : 0.0;
+#if HB_DS_ABL == 4
+  return;
+#endif
+  const int lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int j = (int)blockIdx.x + wv * (int)gridDim.x;
+  if (j >= W) return;
+  double* gs = gs_s[wv];
+  const int chain = D.idx[j];
+  const bool needx = !D.logP_ok[chain];
+  const double xn = lane < kNp ? D.x[(size_t)chain * kNp + lane] : 0.0;
+  const double temp = D.temp[j];
+  int iset = D.iset[j];
+  double gset = D.gset[j];
+  WaveStream S;
+  S.init(D.idum[j], D.idum2[j], D.iy[j], lane < NTAB ? D.iv[(size_t)j * NTAB + lane] : 0);
+
+  const double a = S.uniform();
+  const double jscale = hbglibc::pow(10., -6. + 6. * a, T);
+  int jmp = 0, jt = 0;
+  if ((S.uniform() < 0.5) && (iter > NPAST)) jmp = 1;
+  double yn = xn;
+  // gaussian_proposal_parallel (:1062-1088)
+  auto gaussian_step = [&]() {
+    const double sqtemp = sqrt(temp);
+    const double g = gauss_batch(S, iset, gset, T, gs);
+    if (lane < kNp) yn = xn + g * P->sigma_p[lane] * sqtemp * jscale;
+  };
+  if (jmp == 0) {
+    gaussian_step();
+    jt = 1;
   }
-  __syncthreads();
-  DS_T(1);
-  if (lane < nw) {
-    const int j = slot(lane);
-    const int chain = chain_s[lane];
-    Rng r{D.idum[j], D.idum2[j], D.iy[j], D.iset[j], D.gset[j], D.cts[j], &ivs[lane]};
-    const double* x = &xs[lane];
-    double* y = &ys[lane];
-    const double temp = D.temp[j];
-    const double a = ran2(r);
-    const double jscale = hbglibc::pow(10., -6. + 6. * a, T);
-    int jmp = 0, jt = 0;
-    if ((ran2(r) < 0.5) && (iter > NPAST)) jmp = 1;
-    if (jmp == 0) {
-      gaussian_step(x, y, r, P, jscale, temp, T);
+  if (jmp == 1) {
+    if (chain == 0 && lane == 0) {
+      D.DEtrial_arr[j]++;
+      atomicAdd((unsigned long long*)&D.ctr->DEtrial_tot, 1ull);
+    }
+    // differential_evolution_proposal_parallel (:1091-1140) as compiled (see
+    // hb_sampler.cpp de_step: a == 0, the uninitialised c == 0).  The 0.9
+    // draw precedes the per-parameter Gaussians, as in the reference.
+    int ia = (int)(S.uniform() * NPAST);
+    ia = (int)S.uniform();
+    int ib = ia;
+    while (ib == ia) ib = (int)(S.uniform() * NPAST);
+    const double g0 = gauss_pdf(0, 0, 1.e-4, T) - 0.5;
+    const bool scaled = S.uniform() < 0.9;
+    const double gamma = 2.388 / sqrt(2. * kNp);  // GAMMA, mcmc_wrapper2.h:13
+    const double gd = scaled ? gauss_batch(S, iset, gset, T, gs) : 0.0;
+    if (lane < kNp) {
+      const double* hist = &D.hist[(size_t)j * NPAST * kNp];
+      double dx = hist[(size_t)ib * kNp + lane] - hist[(size_t)ia * kNp + lane];
+      const double eps = dx * g0;
+      if (scaled) dx *= gd * gamma;
+      dx += eps;
+      yn = xn + dx;
+    }
+    jt = 2;
+    double dx_mag = 0;  // summed in coordinate order
+    const double d = xn - yn;
+    for (int i = 0; i < kNp; ++i) {
+      const double di = rld(d, i);
+      dx_mag += di * di;
+    }
+    if (dx_mag < 1e-6) {
+      gaussian_step();
       jt = 1;
     }
-    if (jmp == 1) {
-      if (chain == 0) {
-        D.DEtrial_arr[j]++;
-        atomicAdd((unsigned long long*)&D.ctr->DEtrial_tot, 1ull);
-      }
-      de_step(x, y, r, &D.hist[(size_t)j * NPAST * kNp], NPAST, T);
-      jt = 2;
-      double dx_mag = 0;
-      for (int i = 0; i < kNp; ++i) dx_mag += (x[i * kPW] - y[i * kPW]) * (x[i * kPW] - y[i * kPW]);
-      if (dx_mag < 1e-6) {
-        gaussian_step(x, y, r, P, jscale, temp, T);
-        jt = 1;
-      }
+  }
+  const double alpha2 = S.uniform();  // drawn after the likelihood calls in the reference; same stream order
+  S.slide();
+  // walls (:440-467), one coordinate per lane
+#if HB_DS_ABL != 1
+  if (lane < kNp) yn = hbwall::apply_wall(yn, P->lim_lo[lane], P->lim_hi[lane], P->fl_lo[lane], P->fl_hi[lane]);
+#endif
+  // "order the masses" (:470-475) as written: y[1] = y[0]; period fixed; T0 folded
+  const double y0 = rld(yn, 0), y1 = rld(yn, 1);
+  if (lane == 1 && y1 > y0) yn = y0;
+  if (lane == 2) yn = P->log_lc_period;
+  if (lane == 6) yn = fmod(yn, P->LC_PERIOD);
+  // prior terms (:444, :477), summed per slot in the reference's order
+  const bool prior = lane < kNp && P->gpflag[lane] == 1 && HB_DS_ABL != 2;
+  const double ty = prior ? prior_term(lane, yn, T) : 0.0;
+  const double tx = (needx && prior) ? prior_term(lane, xn, T) : 0.0;
+  double lpy = 0., lpx = 0.;
+  for (int i = 0; i < kNp; ++i) {
+    if (P->gpflag[i] != 1) continue;
+    lpy += rld(ty, i);
+    if (needx) lpx += rld(tx, i);
+  }
+  if (lane < kNp) D.y[(size_t)j * kNp + lane] = yn;
+  if (lane < NTAB) D.iv[(size_t)j * NTAB + lane] = S.b_tab;
+  if (lane == 0) {
+    D.logPy[j] = lpy;
+    if (needx) {
+      D.logP[chain] = lpx;
+      D.logP_ok[chain] = 1;
     }
     D.jump[j] = jmp;
     D.jtype[j] = jt;
-    D.alpha2[j] = ran2(r);  // drawn after the likelihood calls in the reference; same stream order
-    D.idum[j] = r.idum;
-    D.idum2[j] = r.idum2;
-    D.iy[j] = r.iy;
-    D.iset[j] = r.iset;
-    D.gset[j] = r.gset;
-    D.cts[j] = r.cts;
+    D.alpha2[j] = alpha2;
+    D.idum[j] = S.b_idum;
+    D.idum2[j] = S.b_idum2;
+    D.iy[j] = S.b_iy;
+    D.iset[j] = iset;
+    D.gset[j] = gset;
+    D.cts[j] += S.consumed;
   }
-  __syncthreads();
-  DS_T(2);
-  // walls (:440-467): the kPW x 21 coordinates spread over all 64 lanes
-  for (int q = lane; q < kNp * kPW; q += 64) {
-    const int i = q / kPW, w = q % kPW;
-    if (w < nw) ys[q] = hbwall::apply_wall(ys[q], P->lim_lo[i], P->lim_hi[i], P->fl_lo[i], P->fl_hi[i]);
-  }
-  __syncthreads();
-  DS_T(3);
-  if (lane < nw) {
-    double* y = &ys[lane];
-    if (y[kPW] > y[0]) y[kPW] = y[0];  // "order the masses" (:470-475) as written: y[1] = y[0]
-    y[2 * kPW] = P->log_lc_period;
-    y[6 * kPW] = fmod(y[6 * kPW], P->LC_PERIOD);
-  }
-  __syncthreads();
-  DS_T(4);
-  // prior terms: lane group g = lane / kPW takes slots i = g, g + 4, ... of walker lane % kPW
-  {
-    const int w = lane % kPW;
-    for (int i = lane / kPW; i < kNp; i += 64 / kPW) {
-      if (P->gpflag[i] != 1 || w >= nw) continue;
-#ifdef HB_DS_ABL_NOPRIOR  // experiment builds only (timing ablation)
-      terms[0][i][w] = 0.0; terms[1][i][w] = 0.0; continue;
-#endif
-      terms[0][i][w] = prior_term(i, ys[i * kPW + w], T);
-      if (needx_s[w]) terms[1][i][w] = prior_term(i, xs[i * kPW + w], T);  // :444, first use of a state
-    }
-  }
-  __syncthreads();
-  DS_T(5);
-  if (lane < nw) {
-    const int j = slot(lane);
-    double lpy = 0., lpx = 0.;
-    for (int i = 0; i < kNp; ++i) {
-      if (P->gpflag[i] != 1) continue;
-      lpy += terms[0][i][lane];
-      lpx += terms[1][i][lane];
-    }
-    D.logPy[j] = lpy;
-    if (needx_s[lane]) {
-      D.logP[chain_s[lane]] = lpx;
-      D.logP_ok[chain_s[lane]] = 1;
-    }
-  }
-  for (int q = lane; q < kNp * nw; q += 64) {
-    const int w = q / kNp, n = q % kNp;
-    D.y[(size_t)slot(w) * kNp + n] = ys[n * kPW + w];
-  }
-  for (int q = lane; q < NTAB * kPW; q += 64) {
-    const int w = q / NTAB, t = q % NTAB;
-    if (w < nw) D.iv[(size_t)slot(w) * NTAB + t] = ivs[t * kPW + w];
-  }
-#ifdef HB_DS_TIMING
-  DS_T(6);
-  if (lane == 0 && iter == 100 && blockIdx.x % 32 == 0)
-    printf("propose blk %d: load %lld draws %lld walls %lld quirks %lld priors %lld store %lld\n", blockIdx.x,
-           tclk[1] - tclk[0], tclk[2] - tclk[1], tclk[3] - tclk[2], tclk[4] - tclk[3], tclk[5] - tclk[4],
-           tclk[6] - tclk[5]);
-#endif
 }
 
 // Hastings test and history (:492-546); 64 slots per block, the state and
@@ -948,7 +1036,7 @@ extern "C" int hb_dsampler_step(hb_dsampler* d, long iter) {
   const int* d_off = reinterpret_cast<const int*>(d->d_sched[r] + sizeof(SwapEnt) * (size_t)W);
 
   const int NPAST = d->NPAST;
-  ds_propose<<<(W + kPW - 1) / kPW, 64, 0, s>>>(D, W, NPAST, (long long)iter);
+  ds_propose<<<(W + kPW - 1) / kPW, 64 * kPW, 0, s>>>(D, W, NPAST, (long long)iter);
   DS_TRY(hipGetLastError(), "ds_propose");
   const int rc = hb_loglik_batch_dev(d->ctx, D.y, W, D.logLy, (void*)s);
   if (rc) return rc;

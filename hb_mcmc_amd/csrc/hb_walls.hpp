@@ -58,50 +58,79 @@ HBW_FN double floor_div(double num, double den) {
 // K_j + c1 >= 2^52 + 1 (c1 = rlo or -rhi), K_j - D >= 2^52 + 1, and at the
 // top K_0 + c1 <= 2^53 - 2.  Every magnitude of the binade exceeds
 // 2 max(|lo|, |hi|), so each value lies outside [lo, hi] on its sign's side.
-HBW_FN double ff_double_folds(double v, double lo, double hi, int folds_left, int& m_out) {
-  m_out = 0;
+//
+// `bottom` receives 2^eb, the lower edge of v's binade.  When no fast-forward
+// is possible the caller folds one at a time; `mode` says for how long:
+//   kFfTop   -- a margin at the binade top: a few folds, then try again;
+//   kFfBinade -- a rounding-tie binade or too little room above the bottom:
+//               fold until |v| drops below `bottom` (the next binade);
+//   kFfNear  -- v's binade is within 2 max(|lo|, |hi|): no lower binade can
+//               fast-forward either, fold to the end.
+enum { kFfDone = 0, kFfTop = 1, kFfBinade = 2, kFfNear = 3 };
+HBW_FN double ff_double_folds(double v, double lo, double hi, int folds_left, int& m_out, int& mode,
+                              double& bottom) {
+  // every quantity is computed unconditionally and the outcome selected at
+  // the end (no early exits: on a GPU lane the tests would serialise into
+  // exec-mask branches); garbage from a failed test is discarded
   const double av = fabs(v);
-  if (!(av < 0x1p1000) || !(av > 0.0)) return v;
+  const bool finite = av < 0x1p1000 && av > 0.0;
   int e;
   frexp(av, &e);                       // av = f 2^e, f in [0.5, 1): binade [2^(e-1), 2^e)
-  const int eb = e - 1;                // av in [2^eb, 2^(eb+1))
+  const int eb = finite ? e - 1 : 0;   // av in [2^eb, 2^(eb+1))
+  bottom = finite ? ldexp(1.0, eb) : 0.0;
   const double lim = fabs(lo) > fabs(hi) ? fabs(lo) : fabs(hi);
-  if (!(ldexp(1.0, eb) > 2.0 * lim)) return v;
+  const bool far = bottom > 2.0 * lim;
   const double scale = ldexp(1.0, 52 - eb);  // 1/g
   const double clo = 2.0 * lo * scale, chi = 2.0 * hi * scale;  // exact (power-of-2 scaling), |.| < 2^52
-  if (clo - floor(clo) == 0.5 || chi - floor(chi) == 0.5) return v;  // rounding ties: no translation
+  const bool tie = clo - floor(clo) == 0.5 || chi - floor(chi) == 0.5;  // rounding ties: no translation
   const double rlo = rint(clo), rhi = rint(chi);
   const double D = rhi - rlo;                  // exact integer
-  if (!(D > 0.0)) return v;
   const double K = av * scale;                 // exact integer in [2^52, 2^53)
   const double c1 = v < 0.0 ? rlo : -rhi;
-  if (!(K + (c1 > 0.0 ? c1 : 0.0) <= 0x1p53 - 2.0)) return v;
+  const bool fits = D > 0.0 && K + (c1 > 0.0 ? c1 : 0.0) <= 0x1p53 - 2.0;
   // m pairs: K - (m-1) D + c1 >= 2^52 + 1 and K - m D >= 2^52 + 1
   const double n1 = K - 0x1p52 - 1.0, n2 = K + c1 - 0x1p52 - 1.0;
-  if (!(n1 >= D) || !(n2 >= 0.0)) return v;
+  const bool room = n1 >= D && n2 >= 0.0;
   double m = floor_div(n1, D);
   const double m2 = floor_div(n2, D) + 1.0;
   if (m2 < m) m = m2;
   const double cap = (double)(folds_left / 2);
   if (m > cap) m = cap;
-  if (!(m >= 1.0)) return v;
-  m_out = (int)m;
-  return copysign((K - m * D) / scale, v);  // exact: integers below 2^53, power-of-2 scaling
+  const bool go = finite && far && !tie && fits && room && m >= 1.0;
+  mode = go ? kFfDone
+            : !finite ? kFfTop : !far ? kFfNear : tie ? kFfBinade : !fits ? kFfTop : !room ? kFfBinade : kFfTop;
+  m_out = go ? (int)m : 0;
+  // exact: integers below 2^53 times a power of two (g = 2^(eb-52))
+  return go ? copysign((K - m * D) * ldexp(1.0, eb - 52), v) : v;
 }
 
 // v after the walls of one coordinate (flags: 1 reflecting, 2 periodic).
-// Each pass: one fast-forward through the current binade, then up to four
-// single folds (a binade crossing, a rounding-tie binade, the last approach);
-// the fold count and stopping rule are those of the plain loop.
+// Each pass: one fast-forward through the current binade, then single folds
+// (a binade crossing, a rounding-tie binade, the last approach); the fold
+// count and stopping rule are those of the plain loop.
 HBW_FN double apply_wall(double v, double lo, double hi, double fl, double fh) {
   int guard = 0;
   if (fl == 1 && fh == 1) {
+    const double lim2 = 2.0 * (fabs(lo) > fabs(hi) ? fabs(lo) : fabs(hi));
+    const double lo2 = 2.0 * lo, hi2 = 2.0 * hi;  // exact
     while (guard < kGuard && (v < lo || v > hi)) {
-      int m;
-      v = ff_double_folds(v, lo, hi, kGuard - guard, m);
+      int m, mode;
+      double bottom;
+      v = ff_double_folds(v, lo, hi, kGuard - guard, m, mode, bottom);
       guard += 2 * m;
-      for (int s = 0; s < 4 && guard < kGuard && (v < lo || v > hi); ++s, ++guard)
-        v = (v < lo) ? 2.0 * lo - v : 2.0 * hi - v;
+      // single folds (the plain loop's own steps): at least 4, then while
+      // |v| > stop and fewer than smax.  After a fast-forward (v at the bottom
+      // of its binade) or at a binade top, up to 16 take v below the next
+      // binade edge by the fold reach 2 max(|lo|, |hi|), so the next pass can
+      // fast-forward at once; a binade that cannot be fast-forwarded is folded
+      // through (see ff_double_folds)
+      const double edge = (mode == kFfDone ? bottom : 2.0 * bottom);
+      const double stop = mode == kFfNear ? -1.0
+                          : mode == kFfBinade ? bottom * (1.0 - 0x1p-53)  // |v| >= bottom
+                                              : edge - lim2 - edge * 0x1p-48;
+      const int smax = mode >= kFfBinade ? kGuard : 16;
+      for (int s = 0; guard < kGuard && (v < lo || v > hi) && (s < 4 || (s < smax && fabs(v) > stop)); ++s, ++guard)
+        v = (v < lo ? lo2 : hi2) - v;
     }
   } else {
     for (; guard < kGuard; ++guard) {
