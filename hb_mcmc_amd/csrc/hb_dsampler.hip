@@ -142,6 +142,9 @@ struct Dev {
 // advanced by replaying the consumed draws' writes (slot iy_(k-1) / NDIV,
 // value idum_k).
 __device__ __forceinline__ int rl(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
+// a wave-uniform int the compiler cannot prove uniform: pin it to an SGPR so
+// loops over it stay scalar (s_cbranch) instead of exec-mask loops
+__device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
 // lane l of old := v (uniform v, l); a compare + select, so the compiler owns the SGPR hazards
 __device__ __forceinline__ int wl(int v, int l, int old) { return (int)(threadIdx.x & 63) == l ? v : old; }
 __device__ __forceinline__ double rld(double v, int l) {
@@ -204,14 +207,17 @@ struct WaveStream {
     w_idum2 = mulmod31<249>(kLcgPow.a2[k], b_idum2);
   }
   __device__ void gen_to(int n) {  // the serial shuffle for lanes gend .. n-1
-    for (int k = gend; k < n; ++k) {
-      const int j = ndiv(g_iy);
-      g_iy = rl(g_tab, j) - rl(w_idum2, k);
+    n = uni(n);
+    int iy = uni(g_iy);
+    for (int k = uni(gend); k < n; ++k) {
+      const int j = uni(ndiv(iy));
+      iy = uni(rl(g_tab, j) - rl(w_idum2, k));
       g_tab = wl(rl(w_idum, k), j, g_tab);
-      if (g_iy < 1) g_iy += IMM1;
-      w_iy = wl(g_iy, k, w_iy);
+      if (iy < 1) iy += IMM1;
+      w_iy = wl(iy, k, w_iy);
     }
-    if (n > gend) gend = n;
+    g_iy = iy;
+    gend = uni(max(n, gend));
   }
   // start from (idum, idum2, iy, table); the table initialisation of
   // :905-916 runs here when idum <= 0 (a propose always consumes draws)
@@ -238,25 +244,26 @@ struct WaveStream {
   }
   // retire lanes 0..cur-1: the base state advances past them, the window slides down
   __device__ void slide() {
-    const int s = cur;
+    const int s = uni(cur);
     if (s == 0) return;
-    int prev = b_iy;
+    int prev = uni(b_iy);
     for (int k = 0; k < s; ++k) {
-      b_tab = wl(rl(w_idum, k), ndiv(prev), b_tab);
+      b_tab = wl(rl(w_idum, k), uni(ndiv(prev)), b_tab);
       prev = rl(w_iy, k);
     }
     b_iy = prev;
     b_idum = rl(w_idum, s - 1);
     b_idum2 = rl(w_idum2, s - 1);
     w_iy = shfli(w_iy, min((int)(threadIdx.x & 63) + s, 63));
-    gend -= s;
+    gend = uni(gend - s);
     consumed += s;
     cur = 0;
     jump();
   }
   __device__ double uniform() {  // one ran2() call
+    cur = uni(cur);
     if (cur == 64) slide();
-    if (cur >= gend) gen_to(min(64, cur + 8));
+    if (cur >= uni(gend)) gen_to(min(64, cur + 8));
     return uni_of(rl(w_iy, cur++));
   }
   __device__ int idum_now() const { return cur == 0 ? b_idum : rl(w_idum, cur - 1); }
@@ -292,10 +299,10 @@ __device__ double gauss_batch(WaveStream& S, int& iset, double& gset, const hbgl
     pos = 1;
     iset = 0;
   }
-  while (pos < kNp && HB_DS_ABL != 3) {
+  while (pos < kNp && HB_DS_ABL != 3 && HB_DS_ABL < 6) {
     S.slide();
-    const int need = (kNp - pos + 1) / 2;          // pairs still to generate
-    const int att = min(32, need + need / 2 + 2);  // attempts tested this round (acceptance pi/4)
+    const int need = uni((kNp - pos + 1) / 2);          // pairs still to generate
+    const int att = uni(min(32, need + need / 2 + 2));  // attempts tested this round (acceptance pi/4)
     S.gen_to(2 * att);
     const int m = lane & 31;
     const double v1 = 2.0 * uni_of(shfli(S.w_iy, 2 * m)) - 1.0;
@@ -304,7 +311,7 @@ __device__ double gauss_batch(WaveStream& S, int& iset, double& gset, const hbgl
     const bool ok = lane < att && !(rsq >= 1.0 || rsq == 0.0);
     const uint64_t mask = __ballot(ok);
     const int avail = __popcll(mask);
-    const int take = min(need, avail);
+    const int take = uni(min(need, avail));
     const int rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0));
     double g1 = 0.0;
     if (ok && rank < take) {
@@ -318,7 +325,7 @@ __device__ double gauss_batch(WaveStream& S, int& iset, double& gset, const hbgl
       // lane of the take-th accepted attempt: its v1 * fac is the new gset
       uint64_t mm = mask;
       for (int r = 1; r < take; ++r) mm &= mm - 1;
-      const int last = __builtin_ctzll(mm);
+      const int last = uni(__builtin_ctzll(mm));
       gset = rld(g1, last);
       S.cur = (take == need) ? 2 * (last + 1) : 2 * att;
       const int got = 2 * take;
@@ -365,6 +372,19 @@ __global__ __launch_bounds__(64 * kPW) void ds_propose(Dev D, int W, int NPAST, 
   const int j = (int)blockIdx.x + wv * (int)gridDim.x;
   if (j >= W) return;
   double* gs = gs_s[wv];
+#ifdef HB_DS_TIMING  // experiment builds only: per-phase shader clocks of two slots at iteration 100
+  long long tclk[8], tw0 = wall_clock64();
+#define DS_T(k) tclk[k] = clock64()
+#define DS_PRINT()                                                                                              \
+  if (lane == 0 && iter == 100 && (j == 1 || j == 49 || j == 99))                                                \
+    printf("slot %d: init %lld u2 %lld gauss %lld alpha %lld walls %lld priors %lld store %lld total %lld wall %lld\n", \
+           j, tclk[1] - tclk[0], tclk[2] - tclk[1], tclk[3] - tclk[2], tclk[4] - tclk[3], tclk[5] - tclk[4],        \
+           tclk[6] - tclk[5], tclk[7] - tclk[6], tclk[7] - tclk[0], wall_clock64() - tw0);
+#else
+#define DS_T(k)
+#define DS_PRINT()
+#endif
+  DS_T(0);
   const int chain = D.idx[j];
   const bool needx = !D.logP_ok[chain];
   const double xn = lane < kNp ? D.x[(size_t)chain * kNp + lane] : 0.0;
@@ -373,9 +393,15 @@ __global__ __launch_bounds__(64 * kPW) void ds_propose(Dev D, int W, int NPAST, 
   double gset = D.gset[j];
   WaveStream S;
   S.init(D.idum[j], D.idum2[j], D.iy[j], lane < NTAB ? D.iv[(size_t)j * NTAB + lane] : 0);
+  DS_T(1);
 
   const double a = S.uniform();
+  DS_T(2);
+#if HB_DS_ABL >= 7
+  const double jscale = a;
+#else
   const double jscale = hbglibc::pow(10., -6. + 6. * a, T);
+#endif
   int jmp = 0, jt = 0;
   if ((S.uniform() < 0.5) && (iter > NPAST)) jmp = 1;
   double yn = xn;
@@ -425,10 +451,12 @@ __global__ __launch_bounds__(64 * kPW) void ds_propose(Dev D, int W, int NPAST, 
       jt = 1;
     }
   }
+  DS_T(3);
   const double alpha2 = S.uniform();  // drawn after the likelihood calls in the reference; same stream order
   S.slide();
+  DS_T(4);
   // walls (:440-467), one coordinate per lane
-#if HB_DS_ABL != 1
+#if HB_DS_ABL != 1 && HB_DS_ABL < 5
   if (lane < kNp) yn = hbwall::apply_wall(yn, P->lim_lo[lane], P->lim_hi[lane], P->fl_lo[lane], P->fl_hi[lane]);
 #endif
   // "order the masses" (:470-475) as written: y[1] = y[0]; period fixed; T0 folded
@@ -436,8 +464,9 @@ __global__ __launch_bounds__(64 * kPW) void ds_propose(Dev D, int W, int NPAST, 
   if (lane == 1 && y1 > y0) yn = y0;
   if (lane == 2) yn = P->log_lc_period;
   if (lane == 6) yn = fmod(yn, P->LC_PERIOD);
+  DS_T(5);
   // prior terms (:444, :477), summed per slot in the reference's order
-  const bool prior = lane < kNp && P->gpflag[lane] == 1 && HB_DS_ABL != 2;
+  const bool prior = lane < kNp && P->gpflag[lane] == 1 && HB_DS_ABL != 2 && HB_DS_ABL < 5;
   const double ty = prior ? prior_term(lane, yn, T) : 0.0;
   const double tx = (needx && prior) ? prior_term(lane, xn, T) : 0.0;
   double lpy = 0., lpx = 0.;
@@ -446,6 +475,7 @@ __global__ __launch_bounds__(64 * kPW) void ds_propose(Dev D, int W, int NPAST, 
     lpy += rld(ty, i);
     if (needx) lpx += rld(tx, i);
   }
+  DS_T(6);
   if (lane < kNp) D.y[(size_t)j * kNp + lane] = yn;
   if (lane < NTAB) D.iv[(size_t)j * NTAB + lane] = S.b_tab;
   if (lane == 0) {
@@ -463,14 +493,17 @@ __global__ __launch_bounds__(64 * kPW) void ds_propose(Dev D, int W, int NPAST, 
     D.iset[j] = iset;
     D.gset[j] = gset;
     D.cts[j] += S.consumed;
+  DS_T(7);
+  DS_PRINT();
   }
 }
 
-// Hastings test and history (:492-546); 64 slots per block, the state and
-// history rows copied cooperatively
-__global__ __launch_bounds__(64) void ds_accept(Dev D, int W, int NPAST, long long iter) {
+// Hastings test and history (:492-546); 64 slots per block (one lane each),
+// the state and history rows copied by the whole block
+constexpr int kAccThreads = 256;
+__global__ __launch_bounds__(kAccThreads) void ds_accept(Dev D, int W, int NPAST, long long iter) {
   __shared__ int chain_s[64], acc_s[64];
-  const int lane = threadIdx.x;
+  const int tid = threadIdx.x, lane = tid;
   const int j0 = blockIdx.x * 64;
   const int nw = min(64, W - j0);
   const int k = (int)(iter - (iter / NPAST) * NPAST);
@@ -516,19 +549,28 @@ __global__ __launch_bounds__(64) void ds_accept(Dev D, int W, int NPAST, long lo
     }
   }
   __syncthreads();
-  // x[chain] = y (accepted), history row k = x[chain] (:533-546)
-  for (int q = lane; q < kNp * nw; q += 64) {
-    const int w = q / kNp, n = q % kNp;
-    const int j = j0 + w;
-    double* xc = &D.x[(size_t)chain_s[w] * kNp];
-    double v;
-    if (acc_s[w]) {
-      v = D.y[(size_t)j * kNp + n];
-      xc[n] = v;
-    } else {
-      v = xc[n];
+  // x[chain] = y (accepted), history row k = x[chain] (:533-546): every
+  // element's load is issued before any store, so the block waits for one
+  // memory round trip instead of one per element
+  constexpr int kPer = (kNp * 64 + kAccThreads - 1) / kAccThreads;
+  double v[kPer];
+#pragma unroll
+  for (int r = 0; r < kPer; ++r) {
+    const int q = tid + r * kAccThreads;
+    v[r] = 0.0;
+    if (q < kNp * nw) {
+      const int w = q / kNp, n = q % kNp;
+      v[r] = acc_s[w] ? D.y[(size_t)(j0 + w) * kNp + n] : D.x[(size_t)chain_s[w] * kNp + n];
     }
-    D.hist[((size_t)j * NPAST + k) * kNp + n] = v;
+  }
+#pragma unroll
+  for (int r = 0; r < kPer; ++r) {
+    const int q = tid + r * kAccThreads;
+    if (q < kNp * nw) {
+      const int w = q / kNp, n = q % kNp;
+      if (acc_s[w]) D.x[(size_t)chain_s[w] * kNp + n] = v[r];
+      D.hist[((size_t)(j0 + w) * NPAST + k) * kNp + n] = v[r];
+    }
   }
 }
 
@@ -558,6 +600,9 @@ __global__ __launch_bounds__(kSwapThreads) void ds_swap(Dev D, int W, const Swap
   __shared__ int off_s[kMaxLevels + 1];
   __shared__ uint64_t exp_s[256];  // exp table for the divergent lookups of the level loop
   const int tid = threadIdx.x;
+#ifdef HB_DS_TIMING
+  const long long sstart = clock64();
+#endif
   for (int q = tid; q < 256; q += kSwapThreads) exp_s[q] = hbglibc::kExpTab[q];
   const hbglibc::Tabs T{exp_s, hbglibc::kLogTab, hbglibc::kPowTab};
   const bool off_lds = nlv <= kMaxLevels;
@@ -586,6 +631,9 @@ __global__ __launch_bounds__(kSwapThreads) void ds_swap(Dev D, int W, const Swap
   }
   if (tid == 0) nacc_s = 0;
   __syncthreads();
+#ifdef HB_DS_TIMING
+  const long long sw0 = clock64();
+#endif
   int nacc = 0;
   for (int lv = 0; lv < nlv; ++lv) {
     const int e0 = off_lds ? off_s[lv] : off[lv];
@@ -606,6 +654,9 @@ __global__ __launch_bounds__(kSwapThreads) void ds_swap(Dev D, int W, const Swap
     __syncthreads();
   }
   if (nacc) atomicAdd(&nacc_s, nacc);
+#ifdef HB_DS_TIMING
+  const long long sw1 = clock64();
+#endif
   if (LDS) {
     for (int c = tid; c < W; c += kSwapThreads) D.idx[c] = idx.ld(c);
     idx.p = D.idx;
@@ -637,6 +688,10 @@ __global__ __launch_bounds__(kSwapThreads) void ds_swap(Dev D, int W, const Swap
   }
   if (reset)
     for (int c = tid; c < W; c += kSwapThreads) D.DEacc_arr[c] = D.DEtrial_arr[c] = 0;
+#ifdef HB_DS_TIMING
+  if (tid == 0 && iter == 100)
+    printf("swap: start->staged %lld levels(%d) %lld tail %lld\n", sw0 - sstart, nlv, sw1 - sw0, clock64() - sw1);
+#endif
 }
 
 // states and logL by slot (writer / verbose / download)
@@ -1040,7 +1095,7 @@ extern "C" int hb_dsampler_step(hb_dsampler* d, long iter) {
   DS_TRY(hipGetLastError(), "ds_propose");
   const int rc = hb_loglik_batch_dev(d->ctx, D.y, W, D.logLy, (void*)s);
   if (rc) return rc;
-  ds_accept<<<(W + 63) / 64, 64, 0, s>>>(D, W, NPAST, (long long)iter);
+  ds_accept<<<(W + 63) / 64, kAccThreads, 0, s>>>(D, W, NPAST, (long long)iter);
   DS_TRY(hipGetLastError(), "ds_accept");
   DS_TRY(hipStreamWaitEvent(s, d->ev_copy[r], 0), "schedule wait");
   if (d->lds_swap)
