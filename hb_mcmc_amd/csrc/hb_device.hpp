@@ -177,6 +177,12 @@ __device__ __forceinline__ double radius_spread_of_mass(double m) {  // envelope
   const double ex = 4.22, sl = 15.68, lo = 0.01, knee = 1.055, hi = 0.17;
   return 1.0 / (1.0 / hi + 1.0 / (sl * pow(pow(m, ex) + pow(knee, ex), 1.0 / ex) - (sl * knee - lo)));
 }
+// the same law from lm = log10 m: m^ex = 10^(ex lm) does not wait for m = 10^lm
+// (a few ulp from pow(10^lm, ex); the prep kernel's latency-critical chain)
+__device__ __forceinline__ double radius_spread_of_logmass(double lm) {
+  const double ex = 4.22, sl = 15.68, lo = 0.01, knee = 1.055, hi = 0.17;
+  return 1.0 / (1.0 / hi + 1.0 / (sl * pow(exp10(ex * lm) + pow(knee, ex), 1.0 / ex) - (sl * knee - lo)));
+}
 
 // get_alpha_beam (likelihood3.c:194-209)
 __device__ __forceinline__ double beam_coeff(double lt) {

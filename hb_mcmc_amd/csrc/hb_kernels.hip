@@ -54,17 +54,22 @@ using namespace hbdev;
 namespace hbk {
 
 // ---------------------------------------------------------------------------
-// kernel 1: per-walker constants.  64 walkers per 128-thread block; wave 0
-// evaluates star 1 of all 64 walkers, wave 1 star 2 (lane = walker), so the
-// two stars' transcendental chains run in parallel and the star-specific tails
-// (orbit + Gaia term on wave 0, eclipse geometry + Roche test on wave 1) are
-// wave-uniform instead of divergent.  The stars swap their results through
-// LDS; parameters and records move through LDS so HBM accesses coalesce.
+// kernel 1: per-walker constants.  64 walkers per 256-thread block, lane =
+// walker, four waves with wave-uniform roles: wave s (s = star 0/1) runs the
+// star's radius law and then its photometric coefficients; wave 2 + s runs
+// the star's Teff law and beaming factor, then a star-specific tail (wave 2:
+// Gaia term and sin/cos omega; wave 3: eclipse geometry, Roche test and
+// phase-table rotations).  The block is latency-bound (one wave per SIMD), so
+// splitting the independent chains over four waves shortens the critical
+// path; the formulas and their operand order are those of the 2-wave version
+// (bit-identical records).  Results cross waves through LDS; parameters and
+// records move through LDS so HBM accesses coalesce.
 // ---------------------------------------------------------------------------
 #ifndef HB_PREP_W
 #define HB_PREP_W 64
 #endif
-constexpr int kPrepWalkers = HB_PREP_W;  // walkers per prep block (2 lanes each)
+constexpr int kPrepWalkers = HB_PREP_W;  // walkers per prep block (4 lanes each)
+constexpr int kPrepThreads = 4 * kPrepWalkers;
 constexpr int kWcDoubles = (int)(sizeof(WalkerConst) / sizeof(double));
 
 // sin/cos of a phase-table angle: the branch-free reduction for |x| < 2^19,
@@ -79,103 +84,147 @@ __device__ __forceinline__ void sincos_table(double x, double& sv, double& cv) {
   }
 }
 
-__global__ __launch_bounds__(2 * kPrepWalkers) void hb_prep_kernel(const double* __restrict__ params,
-                                                                    int nwalk, MagArgs ma,
-                                                                    WalkerConst* __restrict__ out,
-                                                                    const TargetDesc* __restrict__ tab,
-                                                                    const int* __restrict__ wt,
-                                                                    const double* __restrict__ tcad, int ncad,
-                                                                    double2* __restrict__ ph,
-                                                                    const int* __restrict__ w0, int ntargets) {
+__global__ __launch_bounds__(kPrepThreads) void hb_prep_kernel(const double* __restrict__ params,
+                                                              int nwalk, MagArgs ma,
+                                                              WalkerConst* __restrict__ out,
+                                                              const TargetDesc* __restrict__ tab,
+                                                              const int* __restrict__ wt,
+                                                              const double* __restrict__ tcad, int ncad,
+                                                              double2* __restrict__ ph,
+                                                              const int* __restrict__ w0, int ntargets) {
   __shared__ double sp[kPrepWalkers * kNpars];
   __shared__ double so[kPrepWalkers * kWcDoubles];
-  __shared__ double xs[2][16][kPrepWalkers];  // per-star results for the partner: [star][item][walker]
+  // per-star results: [star][item][walker]; items 0 m, 1 r, 2 tk, 3 ab, 4..15 star-2 terms
+  __shared__ double xs[2][16][kPrepWalkers];
+  __shared__ double gs[3][kPrepWalkers];  // wave 2's Gaia term and sin/cos omega
   const int tid = threadIdx.x;
   const int base = blockIdx.x * kPrepWalkers;
   const int nb = min(kPrepWalkers, nwalk - base);
+#ifdef HB_PREP_TIMING  // experiment builds only: phase clocks of block 0 / block 32
+  long long pc[8];
+  pc[0] = clock64();
+#define PT(k) pc[k] = clock64()
+#else
+#define PT(k)
+#endif
+  // wave 2's first phase-table operands (single context), in flight with the parameters
+  double t_first = 0.0, lp0 = 0.0;
+  if (ph != nullptr && tab == nullptr && tid >= 2 * kPrepWalkers && tid < 3 * kPrepWalkers) {
+    const int i0 = blockIdx.x + gridDim.x * (tid - 2 * kPrepWalkers);
+    if (i0 < ncad) t_first = tcad[i0];
+    lp0 = params[2];
+  }
   {  // all loads in flight before the first LDS write (a rolled loop serialises on vmcnt(0))
-    constexpr int U = (kPrepWalkers * kNpars + 2 * kPrepWalkers - 1) / (2 * kPrepWalkers);
+    constexpr int U = (kPrepWalkers * kNpars + kPrepThreads - 1) / kPrepThreads;
     double v[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int i = tid + u * 2 * kPrepWalkers;
+      const int i = tid + u * kPrepThreads;
       v[u] = i < nb * kNpars ? params[(size_t)base * kNpars + i] : 0.0;
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int i = tid + u * 2 * kPrepWalkers;
+      const int i = tid + u * kPrepThreads;
       if (i < nb * kNpars) sp[i] = v[u];
     }
   }
   __syncthreads();
+  PT(1);
 #if HB_PREP_ABL == 4  // experiment builds only: data movement, no math
   {
     double* dst = reinterpret_cast<double*>(out) + (size_t)base * kWcDoubles;
-    for (int i = tid; i < nb * kWcDoubles; i += 2 * kPrepWalkers) dst[i] = sp[i % (nb * kNpars)];
+    for (int i = tid; i < nb * kWcDoubles; i += kPrepThreads) dst[i] = sp[i % (nb * kNpars)];
     return;
   }
 #endif
   const int j = tid & (kPrepWalkers - 1);
-  const int star = tid / kPrepWalkers;  // wave-uniform
+  const int wv = tid / kPrepWalkers;  // wave-uniform
+  const int star = wv & 1;
+  const bool chainR = wv < 2;         // radius law + coefficients; else Teff law + tail
   const bool live = j < nb;
   const double* p = &sp[(live ? j : 0) * kNpars];
 
-  // ---- this wave's star (calc_radii_and_Teffs + get_alpha_beam) ----
+  // ---- this wave's half of the star (calc_radii_and_Teffs + get_alpha_beam) ----
   const double m = exp10(p[star]);
+  if (chainR) {
 #if HB_PREP_ABL == 3
-  const double r = m + p[7 + star];
+    const double r = m + p[7 + star];
 #else
-  const double r = exp10(logradius_of_mass(m) + p[7 + star] * radius_spread_of_mass(m));
+    const double r = exp10(logradius_of_mass(m) + p[7 + star] * radius_spread_of_logmass(p[star]));
 #endif
-  const double lt = logteff_of_mass(m) + p[17 + star] * teff_spread();
-  const double tk = exp10(lt);
-  const double lum = sq(r) * sq(sq(tk));
-  const double ab = beam_coeff(lt) * exp(p[15 + star]);
+    xs[star][0][j] = m;
+    xs[star][1][j] = r;
+  } else {
+    const double lt = logteff_of_mass(m) + p[17 + star] * teff_spread();
+    xs[star][2][j] = exp10(lt);
+    xs[star][3][j] = beam_coeff(lt) * exp(p[15 + star]);
+  }
   const double pd = exp10(p[2]);
   const double e = p[3];
-  double si, ci;
-  sincos(p[4], &si, &ci);
-  xs[star][0][j] = m;
-  xs[star][1][j] = r;
-  xs[star][2][j] = tk;
-  xs[star][3][j] = lum;
+  PT(2);
   __syncthreads();
+  PT(3);
   const int o = star ^ 1;
-  const double mo = xs[o][0][j], ro = xs[o][1][j], tko = xs[o][2][j], lumo = xs[o][3][j];
-  // the same sum in both waves: star-1 luminosity first
+  const double r = xs[star][1][j], tk = xs[star][2][j], ab = xs[star][3][j];
+  const double mo = xs[o][0][j], ro = xs[o][1][j], tko = xs[o][2][j];
+  const double lum = sq(r) * sq(sq(tk));
+  const double lumo = sq(ro) * sq(sq(tko));
+  // the same sum in every wave: star-1 luminosity first
   const double lsum = star ? (lumo + lum) : (lum + lumo);
-  const double nself = lum / lsum;
-#if HB_PREP_ABL == 2
-  StarCoef c;
-  c.kb = pd * m; c.am1 = mo * e; c.am2 = si * r; c.c21 = ro * ab; c.am3 = p[9 + 2 * star]; c.c22 = p[10 + 2 * star];
-  c.c4 = p[13 + star]; c.s1 = pd; c.s3 = m; c.kref = r;
-#else
-  const StarCoef c = star_coef(pd, m, mo, e, si, r, ro, p[9 + 2 * star], p[10 + 2 * star], p[13 + star], ab);
-#endif
-  // star 2 sees u + pi: odd harmonics flip sign
-  const double sg = star ? -1.0 : 1.0;
-  const double terms[12] = {nself * c.am1, nself * c.kb * sg, nself * c.kref, sg * nself * c.kref,
-                            nself * c.am2, nself * c.c21, sg * nself * c.s1, sg * nself * c.s3,
-                            nself * c.am3, nself * c.c22, nself * c.c4, nself};
-  if (star == 1) {
-#pragma unroll
-    for (int q = 0; q < 12; ++q) xs[1][4 + q][j] = terms[q];
-  }
   const double m1 = star ? mo : m, m2 = star ? m : mo;
   const double r1 = star ? ro : r, r2 = star ? r : ro;
   const double t1 = star ? tko : tk, t2 = star ? tk : tko;
-  const double mtot_cgs = m1 * kMsun + m2 * kMsun;
-  const double Pc = pd * kDay;
-  const double a_cgs = cbrt(kG * mtot_cgs * (Pc * Pc) / (kTwoPi * kTwoPi));
   double* w = &so[(live ? j : 0) * kWcDoubles];
   WalkerConst* wc = reinterpret_cast<WalkerConst*>(w);
-  double gr = 0.0, sw_ = 0.0, cw_ = 0.0;
-  if (star == 1) {
+  double terms[12];
+  double si = 0.0, ci = 0.0;
+  double aR = 0.0, sq1me2 = 0.0, inv1me2 = 0.0, mA = 0.0;  // wave 0's orbit fields, off the last phase
+  if (chainR) {
+    sincos(p[4], &si, &ci);
+    if (star == 0) {
+      const double mtot_cgs = m1 * kMsun + m2 * kMsun;
+      const double Pc = pd * kDay;
+      aR = cbrt(kG * mtot_cgs * (Pc * Pc) / (kTwoPi * kTwoPi)) / kRsun;
+      sq1me2 = sqrt(1.0 - e * e);
+      inv1me2 = 1.0 / (1.0 - e * e);
+      mA = kTwoPi / Pc;
+    }
+    const double nself = lum / lsum;
+#if HB_PREP_ABL == 2
+    StarCoef c;
+    c.kb = pd * m; c.am1 = mo * e; c.am2 = si * r; c.c21 = ro * ab; c.am3 = p[9 + 2 * star]; c.c22 = p[10 + 2 * star];
+    c.c4 = p[13 + star]; c.s1 = pd; c.s3 = m; c.kref = r;
+#else
+    const StarCoef c = star_coef(pd, m, mo, e, si, r, ro, p[9 + 2 * star], p[10 + 2 * star], p[13 + star], ab);
+#endif
+    // star 2 sees u + pi: odd harmonics flip sign
+    const double sg = star ? -1.0 : 1.0;
+    terms[0] = nself * c.am1;
+    terms[1] = nself * c.kb * sg;
+    terms[2] = nself * c.kref;
+    terms[3] = sg * nself * c.kref;
+    terms[4] = nself * c.am2;
+    terms[5] = nself * c.c21;
+    terms[6] = sg * nself * c.s1;
+    terms[7] = sg * nself * c.s3;
+    terms[8] = nself * c.am3;
+    terms[9] = nself * c.c22;
+    terms[10] = nself * c.c4;
+    terms[11] = nself;
+    if (star == 1) {
+#pragma unroll
+      for (int q = 0; q < 12; ++q) xs[1][4 + q][j] = terms[q];
+    }
+  } else if (star == 1) {
     if (live) {
+      const double mtot_cgs = m1 * kMsun + m2 * kMsun;
+      const double Pc = pd * kDay;
+      const double a_cgs = cbrt(kG * mtot_cgs * (Pc * Pc) / (kTwoPi * kTwoPi));
       // eclipse geometry
       wc->r1 = r1;
       wc->r2 = r2;
-      const double n1 = lumo / lsum, n2 = lum / lsum;
+      const double lum1 = star ? lumo : lum, lum2 = star ? lum : lumo;
+      const double n1 = lum1 / lsum, n2 = lum2 / lsum;
       wc->ecl1 = n1 / (kPi * (r1 * r1));
       wc->ecl2 = n2 / (kPi * (r2 * r2));
       wc->rbig = r2 > r1 ? r2 : r1;
@@ -203,7 +252,7 @@ __global__ __launch_bounds__(2 * kPrepWalkers) void hb_prep_kernel(const double*
       wc->pad[0] = wc->pad[1] = 0.0;
     }
   } else {
-    // Gaia G term (loglikelihood :834-848) while wave 1 does the eclipse/Roche part
+    // Gaia G term (loglikelihood :834-848)
     double dist = ma.mag[0], gobs = ma.mag[1], gerr = ma.magerr[0];
     if (tab != nullptr && live) {  // catalog mode: this walker's target
       const TargetDesc& td = tab[wt[base + j]];
@@ -216,27 +265,48 @@ __global__ __launch_bounds__(2 * kPrepWalkers) void hb_prep_kernel(const double*
 #else
     const double g = ab_mag(band_flux(673.0, r1 * kRsun, r2 * kRsun, t1, t2, dist, p[19]));
 #endif
-    gr = (g - gobs) / gerr;
+    double sw_, cw_;
     sincos(p[5], &sw_, &cw_);
+    gs[0][j] = (g - gobs) / gerr;
+    gs[1][j] = sw_;
+    gs[2][j] = cw_;
+    // Shared-period phase table (WalkerConst::tab) of a single context, in
+    // this wave's slack: ph[i] = (sin, cos)(t_i DAY 2pi/Pc0) for the period of
+    // walker 0, entries dealt round-robin over the blocks (t_i and P0 were
+    // loaded at kernel start)
+    if (ph != nullptr && tab == nullptr) {
+      const double mA0 = kTwoPi / (exp10(lp0) * kDay);
+      const int G = gridDim.x;
+      double ti = t_first;
+      for (int i = blockIdx.x + G * j; i < ncad; i += G * kPrepWalkers) {
+        double sv, cv;
+        sincos_table((ti * kDay) * mA0, sv, cv);
+        ph[i] = make_double2(sv, cv);
+        if (i + G * kPrepWalkers < ncad) ti = tcad[i + G * kPrepWalkers];
+      }
+    }
   }
-  __syncthreads();  // star-2 terms are in LDS
-  if (star == 0 && live) {
+  PT(4);
+  __syncthreads();  // star-2 terms and the Gaia term are in LDS
+  PT(5);
+  if (wv == 0 && live) {
     double tt[12];
 #pragma unroll
     for (int q = 0; q < 12; ++q) tt[q] = terms[q] + xs[1][4 + q][j];  // star-1 term first
+    const double gr = gs[0][j];
     // orbit
-    wc->Pc = Pc;
+    wc->Pc = pd * kDay;
     wc->T0c = p[6] * kDay;
     wc->e = e;
     wc->e085 = 0.85 * e;
-    wc->sq1me2 = sqrt(1.0 - e * e);
-    wc->inv1me2 = 1.0 / (1.0 - e * e);
-    wc->sw = sw_;
-    wc->cw = cw_;
+    wc->sq1me2 = sq1me2;
+    wc->inv1me2 = inv1me2;
+    wc->sw = gs[1][j];
+    wc->cw = gs[2][j];
     wc->ci = ci;
     wc->si = si;
-    wc->aR = a_cgs / kRsun;
-    wc->mA = kTwoPi / Pc;
+    wc->aR = aR;
+    wc->mA = mA;
     wc->mB = -wc->T0c;
     // polynomial coefficients
     const double s2 = si * si;
@@ -259,33 +329,27 @@ __global__ __launch_bounds__(2 * kPrepWalkers) void hb_prep_kernel(const double*
   __syncthreads();
   {
     double* dst = reinterpret_cast<double*>(out) + (size_t)base * kWcDoubles;
-    constexpr int U = (kPrepWalkers * kWcDoubles + 2 * kPrepWalkers - 1) / (2 * kPrepWalkers);
+    constexpr int U = (kPrepWalkers * kWcDoubles + kPrepThreads - 1) / kPrepThreads;
     double v[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int i = tid + u * 2 * kPrepWalkers;
+      const int i = tid + u * kPrepThreads;
       v[u] = i < nb * kWcDoubles ? so[i] : 0.0;
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int i = tid + u * 2 * kPrepWalkers;
+      const int i = tid + u * kPrepThreads;
       if (i < nb * kWcDoubles) dst[i] = v[u];
     }
   }
-  // Shared-period phase table (WalkerConst::tab), written after the walker
-  // records so its latency overlaps their stores: per light curve, for the
-  // period of its first walker in this batch, ph[i] = (sin, cos)(t_i DAY 2pi/Pc0).
-  // Single context: walker 0, cadences [0, ncad).  Catalog: target k's first
-  // walker w0[k] (-1: no walkers), its slice of the concatenated arrays.
-  if (ph) {
-    if (tab == nullptr) {
-      const double mA0 = kTwoPi / (exp10(params[2]) * kDay);
-      for (int i = blockIdx.x * blockDim.x + tid; i < ncad; i += gridDim.x * blockDim.x) {
-        double sv, cv;
-        sincos_table((tcad[i] * kDay) * mA0, sv, cv);
-        ph[i] = make_double2(sv, cv);
-      }
-    } else {
+  PT(6);
+  // Catalog phase table (WalkerConst::tab), written after the walker records
+  // so its latency overlaps their stores: per target k, for the period of its
+  // first walker w0[k] in this batch (-1: no walkers), ph[i] = (sin, cos)(t_i
+  // DAY 2pi/Pc0) over its slice of the concatenated arrays.  (A single
+  // context's table is written by wave 2 above.)
+  if (ph && tab != nullptr) {
+    {
       for (int k = blockIdx.x; k < ntargets; k += gridDim.x) {
         if (w0[k] < 0) continue;
         const double mA0 = kTwoPi / (exp10(params[(size_t)w0[k] * kNpars + 2]) * kDay);
@@ -298,6 +362,13 @@ __global__ __launch_bounds__(2 * kPrepWalkers) void hb_prep_kernel(const double*
       }
     }
   }
+#ifdef HB_PREP_TIMING
+  PT(7);
+  if ((blockIdx.x == 0 || blockIdx.x == 32) && (tid == 0 || tid == kPrepWalkers))
+    printf("prep blk %d star %d: load %lld chain %lld sync %lld coef %lld sync2 %lld store %lld table %lld total %lld\n",
+           blockIdx.x, tid / kPrepWalkers, pc[1] - pc[0], pc[2] - pc[1], pc[3] - pc[2], pc[4] - pc[3], pc[5] - pc[4],
+           pc[6] - pc[5], pc[7] - pc[6], pc[7] - pc[0]);
+#endif
 }
 
 // ---------------------------------------------------------------------------
@@ -1332,7 +1403,7 @@ hipError_t launch_prep(const double* d_params, int nwalk, const MagArgs& ma, Wal
                        double2* ph, const int* w0, int ntargets) {
   if (nwalk <= 0) return hipSuccess;
   if (t == nullptr || (tab != nullptr && w0 == nullptr) || !HB_PHASE_TAB) ph = nullptr;
-  hipLaunchKernelGGL(hb_prep_kernel, dim3((nwalk + kPrepWalkers - 1) / kPrepWalkers), dim3(2 * kPrepWalkers), 0, s,
+  hipLaunchKernelGGL(hb_prep_kernel, dim3((nwalk + kPrepWalkers - 1) / kPrepWalkers), dim3(kPrepThreads), 0, s,
                      d_params, nwalk, ma, d_wc, tab, wt, t, (int)n, ph, w0, ntargets);
   return hipGetLastError();
 }
