@@ -88,11 +88,17 @@ struct Event {  // LogSuspiciousJumps (:520-528) arguments
   double xo[kNp], xn[kNp];
 };
 
+// one tempering attempt of the level schedule: pair (b, b+1) and ln(beta) of
+// its acceptance draw (beta itself is kept in a global-only array beside it)
 struct SwapEnt {
   int b;
   int pad;
-  double beta;
+  double lnb;
 };
+// schedule buffer: SwapEnt[W] | int off[W + 2] | (8-byte aligned) double beta[W]
+__host__ __device__ inline size_t sched_beta_off(size_t W) {
+  return (sizeof(SwapEnt) * W + sizeof(int) * (W + 2) + 7) & ~(size_t)7;
+}
 
 // device state (pointers into one allocation set)
 struct Dev {
@@ -607,6 +613,8 @@ __global__ __launch_bounds__(kSwapThreads) void ds_swap(Dev D, int W, const Swap
   const hbglibc::Tabs T{exp_s, hbglibc::kLogTab, hbglibc::kPowTab};
   const bool off_lds = nlv <= kMaxLevels;
   const SwapEnt* S = sched;
+  const double* betas = reinterpret_cast<const double*>(reinterpret_cast<const unsigned char*>(sched) +
+                                                         sched_beta_off((size_t)W));
   const double* L = D.logL;
   const double* hs = D.hs;
   IdxRef<LDS> idx{D.idx};
@@ -635,23 +643,57 @@ __global__ __launch_bounds__(kSwapThreads) void ds_swap(Dev D, int W, const Swap
   const long long sw0 = clock64();
 #endif
   int nacc = 0;
-  for (int lv = 0; lv < nlv; ++lv) {
-    const int e0 = off_lds ? off_s[lv] : off[lv];
-    const int e1 = off_lds ? off_s[lv + 1] : off[lv + 1];
-    for (int s = e0 + tid; s < e1; s += kSwapThreads) {
-      const int b = S[s].b, a = b + 1;
-      const double be = S[s].beta;
-      const int olda = idx.ld(a), oldb = idx.ld(b);
-      const double dlogL = L[oldb] - L[olda];
-      const double Hs = hs[b];  // (temp[b] - temp[a]) / (temp[b] temp[a]), fixed ladder (:803)
-      const double al = hbglibc::exp(dlogL * Hs, T);
-      if (al >= be) {
-        idx.st(a, oldb);
-        idx.st(b, olda);
-        ++nacc;
-      }
+  // one attempt: exp(x) >= beta (:803-806) decided by x against ln(beta)
+  // outside a band of 1e-12 (1 + |ln beta|), far wider than the ulp errors of
+  // the host log and of exp; inside the band (or beta = 0, NaN x) the
+  // glibc-exact exp is compared with beta itself
+  auto attempt = [&](int s, int b, double lnb, double Hs) {
+    const int a = b + 1;
+    const int olda = idx.ld(a), oldb = idx.ld(b);
+    const double x = (L[oldb] - L[olda]) * Hs;  // Hs = (temp[b] - temp[a]) / (temp[b] temp[a]) (:803)
+    bool acc;
+    const double dl = 1e-12 * (1.0 + fabs(lnb));
+    if (lnb > -HUGE_VAL && x >= lnb + dl) acc = true;
+    else if (lnb > -HUGE_VAL && x <= lnb - dl) acc = false;
+    else acc = hbglibc::exp(x, T) >= betas[s];
+    if (acc) {
+      idx.st(a, oldb);
+      idx.st(b, olda);
+      ++nacc;
     }
+  };
+  auto offset = [&](int l) { return off_lds ? off_s[l] : off[l]; };
+  // software pipeline: a thread's first attempt of level lv + 1 (pair, ln beta,
+  // pair factor -- none depends on index[]) is loaded while level lv runs, so
+  // a level waits only for its index[] and logL reads
+  int s_cur = nlv > 0 ? offset(0) + tid : 0;
+  int e_cur = nlv > 0 ? offset(1) : 0;
+  int b_cur = 0;
+  double lnb_cur = 0.0, hs_cur = 0.0;
+  if (s_cur < e_cur) {
+    b_cur = S[s_cur].b;
+    lnb_cur = S[s_cur].lnb;
+    hs_cur = hs[b_cur];
+  }
+  for (int lv = 0; lv < nlv; ++lv) {
+    const int e0 = s_cur - tid;
+    const int s_nx = e_cur + tid;
+    const int e_nx = lv + 1 < nlv ? offset(lv + 2) : 0;
+    int b_nx = 0;
+    double lnb_nx = 0.0, hs_nx = 0.0;
+    if (s_nx < e_nx) {
+      b_nx = S[s_nx].b;
+      lnb_nx = S[s_nx].lnb;
+      hs_nx = hs[b_nx];
+    }
+    if (s_cur < e_cur) attempt(s_cur, b_cur, lnb_cur, hs_cur);
+    for (int s = e0 + tid + kSwapThreads; s < e_cur; s += kSwapThreads) attempt(s, S[s].b, S[s].lnb, hs[S[s].b]);
     __syncthreads();
+    s_cur = s_nx;
+    e_cur = e_nx;
+    b_cur = b_nx;
+    lnb_cur = lnb_nx;
+    hs_cur = hs_nx;
   }
   if (nacc) atomicAdd(&nacc_s, nacc);
 #ifdef HB_DS_TIMING
@@ -836,7 +878,7 @@ extern "C" hb_dsampler* hb_dsampler_create(hb_sampler* s, hb_ctx* ctx) {
     return fail("hipMalloc", e);
   D.P = d->d_params;
   if ((e = hipStreamCreateWithFlags(&d->cst, hipStreamNonBlocking)) != hipSuccess) return fail("stream", e);
-  d->sched_bytes = sizeof(SwapEnt) * Wz + sizeof(int) * (Wz + 2);
+  d->sched_bytes = sched_beta_off(Wz) + sizeof(double) * Wz;
   for (int r = 0; r < hb_dsampler::R; ++r) {
     if ((e = d->alloc(&d->d_sched[r], d->sched_bytes))) return fail("hipMalloc", e);
     if ((e = hipHostMalloc((void**)&d->pin[r], d->sched_bytes, hipHostMallocDefault))) return fail("pinned", e);
@@ -1070,6 +1112,7 @@ extern "C" int hb_dsampler_step(hb_dsampler* d, long iter) {
   if (d->used[r]) DS_TRY(hipEventSynchronize(d->ev_used[r]), "schedule ring");  // entry r free again
   SwapEnt* ent = reinterpret_cast<SwapEnt*>(d->pin[r]);
   int* off = reinterpret_cast<int*>(d->pin[r] + sizeof(SwapEnt) * (size_t)W);
+  double* betas = reinterpret_cast<double*>(d->pin[r] + sched_beta_off(W));
   std::fill(d->cnt.begin(), d->cnt.begin() + nlv + 2, 0);
   for (int i = 0; i < W; ++i)
     if (d->lvl[i] > 0) d->cnt[d->lvl[i]]++;
@@ -1079,12 +1122,14 @@ extern "C" int hb_dsampler_step(hb_dsampler* d, long iter) {
   for (int i = 0; i < W; ++i) {
     const int l = d->lvl[i];
     if (l <= 0) continue;
-    SwapEnt& e = ent[d->cnt[l - 1]++];
+    const int q = d->cnt[l - 1]++;
+    SwapEnt& e = ent[q];
     e.b = d->b[i];
     e.pad = 0;
-    e.beta = d->beta[i];
+    e.lnb = log(d->beta[i]);
+    betas[q] = d->beta[i];
   }
-  const size_t used_bytes = sizeof(SwapEnt) * (size_t)W + sizeof(int) * (size_t)(nlv + 1);
+  const size_t used_bytes = sched_beta_off(W) + sizeof(double) * (size_t)W;
   DS_TRY(hipMemcpyAsync(d->d_sched[r], d->pin[r], used_bytes, hipMemcpyHostToDevice, d->cst), "schedule upload");
   DS_TRY(hipEventRecord(d->ev_copy[r], d->cst), "schedule ring");
   const SwapEnt* d_ent = reinterpret_cast<const SwapEnt*>(d->d_sched[r]);
