@@ -109,6 +109,7 @@ struct Dev {
   double* logP;    // [W] by chain
   int* logP_ok;    // [W] by chain
   int* idx;        // [W] slot -> chain
+  int* order;      // [W] propose wave -> slot, hottest rungs first (dispatch order)
   double* temp;    // [W]
   int* idum;       // [W] ran2 state by slot
   int* idum2;
@@ -352,9 +353,10 @@ __device__ double gauss_batch(WaveStream& S, int& iset, double& gset, const hbgl
 // ---------------------------------------------------------------------------
 // proposals (:386-485), one slot per wave, kPW waves per workgroup sharing the
 // LDS copy of the exp/log/pow tables.  Lane n < 21 holds coordinate n of x
-// and y; walls and prior terms run one coordinate per lane.  Slots are
-// interleaved over the workgroup's waves (slot = block + w * grid) so the
-// hot rungs' wall runs spread over the machine.
+// and y; walls and prior terms run one coordinate per lane.  Wave w of block
+// b takes slot order[b + w * grid], order = slots by descending temperature:
+// the hot rungs' long wall runs sit one per workgroup and are dispatched
+// first.
 __global__ __launch_bounds__(64 * kPW) void ds_propose(Dev D, int W, int NPAST, long long iter) {
   __shared__ uint64_t tab_s[hbglibc::kTabWords];  // exp / log / pow tables (divergent lookups)
   __shared__ double gs_s[kPW][32];
@@ -369,14 +371,12 @@ __global__ __launch_bounds__(64 * kPW) void ds_propose(Dev D, int W, int NPAST, 
       tab_s[768 + q] = C.pow[256 + q];
     }
   }
-  __syncthreads();
-#if HB_DS_ABL == 4
-  return;
-#endif
+  // the slot's state loads overlap the table staging; the barrier follows them
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int j = (int)blockIdx.x + wv * (int)gridDim.x;
-  if (j >= W) return;
+  const int k = (int)blockIdx.x + wv * (int)gridDim.x;
+  const bool act = k < W;
+  const int j = act ? D.order[k] : 0;
   double* gs = gs_s[wv];
 #ifdef HB_DS_TIMING  // experiment builds only: per-phase shader clocks of two slots at iteration 100
   long long tclk[8], tw0 = wall_clock64();
@@ -399,6 +399,11 @@ __global__ __launch_bounds__(64 * kPW) void ds_propose(Dev D, int W, int NPAST, 
   double gset = D.gset[j];
   WaveStream S;
   S.init(D.idum[j], D.idum2[j], D.iy[j], lane < NTAB ? D.iv[(size_t)j * NTAB + lane] : 0);
+  __syncthreads();  // tables staged
+#if HB_DS_ABL == 4
+  return;
+#endif
+  if (!act) return;
   DS_T(1);
 
   const double a = S.uniform();
@@ -797,7 +802,7 @@ struct hb_dsampler {
   bool used[R] = {};
   int ring = 0;
   size_t sched_bytes = 0;
-  std::vector<int> b, last, lvl, cnt;
+  std::vector<int> b, last, lvl, cnt, order;
   std::vector<double> beta;
   // staging for gathers / counters / events
   double* d_xs = nullptr;
@@ -865,7 +870,7 @@ extern "C" hb_dsampler* hb_dsampler_create(hb_sampler* s, hb_ctx* ctx) {
   const size_t Wz = (size_t)W;
   Dev& D = d->D;
   if ((e = d->alloc(&D.x, Wz * kNp)) || (e = d->alloc(&D.logL, Wz)) || (e = d->alloc(&D.logP, Wz)) ||
-      (e = d->alloc(&D.logP_ok, Wz)) || (e = d->alloc(&D.idx, Wz)) || (e = d->alloc(&D.temp, Wz)) ||
+      (e = d->alloc(&D.logP_ok, Wz)) || (e = d->alloc(&D.idx, Wz)) || (e = d->alloc(&D.order, Wz)) || (e = d->alloc(&D.temp, Wz)) ||
       (e = d->alloc(&D.idum, Wz)) || (e = d->alloc(&D.idum2, Wz)) || (e = d->alloc(&D.iy, Wz)) ||
       (e = d->alloc(&D.iset, Wz)) || (e = d->alloc(&D.gset, Wz)) || (e = d->alloc(&D.cts, Wz)) ||
       (e = d->alloc(&D.iv, Wz * NTAB)) || (e = d->alloc(&D.y, Wz * kNp)) || (e = d->alloc(&D.logPy, Wz)) ||
@@ -970,6 +975,13 @@ static int ds_upload(hb_dsampler* d) {
   DS_TRY(hipMemcpyAsync(D.logP_ok, ok.data(), sizeof(int) * Wz, hipMemcpyHostToDevice, s), "upload");
   DS_TRY(hipMemcpyAsync(D.idx, idx.data(), sizeof(int) * Wz, hipMemcpyHostToDevice, s), "upload");
   DS_TRY(hipMemcpyAsync(D.temp, v.temp, sizeof(double) * Wz, hipMemcpyHostToDevice, s), "upload");
+  // propose waves in descending temperature: the hot rungs' long wall runs
+  // are dispatched first (ds_propose lasts as long as its latest-finishing
+  // wave), one per workgroup (wave 0 of blocks 0, 1, ...)
+  d->order.resize(Wz);
+  for (size_t i = 0; i < Wz; ++i) d->order[i] = (int)i;
+  std::stable_sort(d->order.begin(), d->order.end(), [&](int a, int b) { return v.temp[a] > v.temp[b]; });
+  DS_TRY(hipMemcpyAsync(D.order, d->order.data(), sizeof(int) * Wz, hipMemcpyHostToDevice, s), "upload");
   std::vector<double> hs(Wz, 0.0);
   for (int b = 0; b + 1 < W; ++b) {  // ptmcmc's H (:803) for the pair (a, b) = (b+1, b): same IEEE ops
     const double heat1 = v.temp[b + 1], heat2 = v.temp[b];
