@@ -49,6 +49,8 @@ FP64_PEAK_TFLOPS = 78.6    # MI355X fp64 vector (spec), SURVEY.md 8(d)
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--backend", choices=("nccl", "gloo"), default="nccl",
+                    help="process group for N > 1 (nccl = RCCL; gloo only to rehearse ranks sharing one GPU)")
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", choices=("C2", "C5"), default="C2",
@@ -285,7 +287,8 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
-        dist.init_process_group("nccl")
+        dist.init_process_group(a.backend)
+    local = local % max(1, torch.cuda.device_count())  # rehearsal: several ranks may share one GPU (gloo)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if a.config == "C5":
@@ -306,24 +309,39 @@ def main():
     nb = 4
     P_host = [synth.walkers(w, seed=1000 + 97 * rank + k) for k in range(nb)]
     P = [torch.from_numpy(x).to(dev) for x in P_host]
-    out = torch.empty(w, dtype=torch.float64, device=dev)
-    gathered = torch.empty(world * w, dtype=torch.float64, device=dev)
+    # logL and all-gather buffers alternate between steps: step k's all-gather
+    # (async, on the communicator's stream) overlaps step k+1's kernels, and
+    # step k+2 waits for it before it overwrites the buffer
+    outs = [torch.empty(w, dtype=torch.float64, device=dev) for _ in range(2)]
+    gathered = [torch.empty(world * w, dtype=torch.float64, device=dev) for _ in range(2)]
+    pending = [None, None]
     stream = torch.cuda.current_stream()
 
     def step(k, ev=None):
+        b = k & 1
+        if pending[b] is not None:
+            pending[b].wait()
+            pending[b] = None
         if ev is not None:
             ev[0].record(stream)
         L.prepare_dev(P[k % nb], stream)
         if ev is not None:
             ev[1].record(stream)
-        L.evaluate_dev(w, out, 0, stream)
+        L.evaluate_dev(w, outs[b], 0, stream)
         if ev is not None:
             ev[2].record(stream)
         if world > 1:
-            dist.all_gather_into_tensor(gathered, out)
+            pending[b] = dist.all_gather_into_tensor(gathered[b], outs[b], async_op=True)
+
+    def drain():
+        for b in range(2):
+            if pending[b] is not None:
+                pending[b].wait()
+                pending[b] = None
 
     for k in range(a.warmup):
         step(k)
+    drain()
     torch.cuda.synchronize()
     evs = [[make_event(a.timer) for _ in range(3)] for _ in range(a.steps)]
     ev_on = [k % max(1, a.event_every) == 0 for k in range(a.steps)]
@@ -333,6 +351,7 @@ def main():
     t0 = time.perf_counter()
     for k in range(a.steps):
         step(k, evs[k] if ev_on[k] else None)
+    drain()  # every step's all-gather is inside the timed region
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -346,7 +365,10 @@ def main():
         wall, eval_ms, prep_ms = (float(x) for x in tt.tolist())
     # sanity: the reference's model itself yields NaN for a rare walker (eclipse_area's asin
     # outside its domain, likelihood3.c:353-389) -- reproduced, counted, never more than a trace
-    lv = out.cpu().numpy()
+    lv = outs[(a.steps - 1) & 1].cpu().numpy()
+    if world > 1:  # the last all-gather holds every rank's logL of that batch, this rank's at its offset
+        gl = gathered[(a.steps - 1) & 1].cpu().numpy()
+        assert np.array_equal(gl[rank * w:(rank + 1) * w], lv, equal_nan=True), "all-gather mismatch"
     nonfinite = int((~np.isfinite(lv)).sum())
     assert nonfinite <= max(1, w // 100), f"{nonfinite} non-finite logL of {w}"
 
@@ -383,8 +405,9 @@ def main():
             "config": {"workload": f"{'C3' if n > 2048 else 'C2'}: synthetic {n}-cadence HB light curve, "
                                    f"{w} walkers per GPU",
                        "ncad": n, "walkers_per_gpu": w, "global_walkers": world * w,
-                       "parallelism": f"walker-sharded x{world}, logL all-gather over RCCL" if world > 1
-                       else "single GPU",
+                       "parallelism": (f"walker-sharded x{world}, logL all-gather over "
+                                       f"{'RCCL' if a.backend == 'nccl' else a.backend} each step, overlapped "
+                                       f"with the next step's kernels") if world > 1 else "single GPU",
                        "evals_per_walker_step": 1,
                        "note": "reference sampler spends 2 evals per walker-step (mcmc_wrapper2.c:488-489)"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
