@@ -354,9 +354,10 @@ __device__ double gauss_batch(WaveStream& S, int& iset, double& gset, const hbgl
 // proposals (:386-485), one slot per wave, kPW waves per workgroup sharing the
 // LDS copy of the exp/log/pow tables.  Lane n < 21 holds coordinate n of x
 // and y; walls and prior terms run one coordinate per lane.  Wave w of block
-// b takes slot order[b + w * grid], order = slots by descending temperature:
-// the hot rungs' long wall runs sit one per workgroup and are dispatched
-// first.
+// b takes slot order[kPW b + w], order = slots by descending temperature: the
+// hot rungs' long wall runs are dispatched first, a workgroup's four on the
+// four SIMDs of its CU, each sharing its SIMD with colder slots of the CU's
+// later workgroups.
 __global__ __launch_bounds__(64 * kPW) void ds_propose(Dev D, int W, int NPAST, long long iter) {
   __shared__ uint64_t tab_s[hbglibc::kTabWords];  // exp / log / pow tables (divergent lookups)
   __shared__ double gs_s[kPW][32];
@@ -374,7 +375,7 @@ __global__ __launch_bounds__(64 * kPW) void ds_propose(Dev D, int W, int NPAST, 
   // the slot's state loads overlap the table staging; the barrier follows them
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int k = (int)blockIdx.x + wv * (int)gridDim.x;
+  const int k = (int)blockIdx.x * kPW + wv;
   const bool act = k < W;
   const int j = act ? D.order[k] : 0;
   double* gs = gs_s[wv];
@@ -977,7 +978,7 @@ static int ds_upload(hb_dsampler* d) {
   DS_TRY(hipMemcpyAsync(D.temp, v.temp, sizeof(double) * Wz, hipMemcpyHostToDevice, s), "upload");
   // propose waves in descending temperature: the hot rungs' long wall runs
   // are dispatched first (ds_propose lasts as long as its latest-finishing
-  // wave), one per workgroup (wave 0 of blocks 0, 1, ...)
+  // wave), kPW consecutive ones per workgroup
   d->order.resize(Wz);
   for (size_t i = 0; i < Wz; ++i) d->order[i] = (int)i;
   std::stable_sort(d->order.begin(), d->order.end(), [&](int a, int b) { return v.temp[a] > v.temp[b]; });
