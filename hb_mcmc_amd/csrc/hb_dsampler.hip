@@ -384,7 +384,7 @@ __global__ __launch_bounds__(64 * kPW) void ds_propose(Dev D, int W, int NPAST, 
 #define DS_T(k) tclk[k] = clock64()
 #define DS_PRINT()                                                                                              \
   if (lane == 0 && iter == 100 && (j == 1 || j == 49 || j == 99))                                                \
-    printf("slot %d: init %lld u2 %lld gauss %lld alpha %lld walls %lld priors %lld store %lld total %lld wall %lld\n", \
+    printf("slot %d: init %lld u2 %lld gauss %lld - %lld walls %lld priors %lld alpha+store %lld total %lld wall %lld\n", \
            j, tclk[1] - tclk[0], tclk[2] - tclk[1], tclk[3] - tclk[2], tclk[4] - tclk[3], tclk[5] - tclk[4],        \
            tclk[6] - tclk[5], tclk[7] - tclk[6], tclk[7] - tclk[0], wall_clock64() - tw0);
 #else
@@ -464,8 +464,6 @@ __global__ __launch_bounds__(64 * kPW) void ds_propose(Dev D, int W, int NPAST, 
     }
   }
   DS_T(3);
-  const double alpha2 = S.uniform();  // drawn after the likelihood calls in the reference; same stream order
-  S.slide();
   DS_T(4);
   // walls (:440-467), one coordinate per lane
 #if HB_DS_ABL != 1 && HB_DS_ABL < 5
@@ -488,6 +486,10 @@ __global__ __launch_bounds__(64 * kPW) void ds_propose(Dev D, int W, int NPAST, 
     if (needx) lpx += rld(tx, i);
   }
   DS_T(6);
+  // the alpha draw and the retirement of the consumed draws only feed the
+  // stored state, so they follow the walls (off the hot slots' critical path)
+  const double alpha2 = S.uniform();  // drawn after the likelihood calls in the reference; same stream order
+  S.slide();
   if (lane < kNp) D.y[(size_t)j * kNp + lane] = yn;
   if (lane < NTAB) D.iv[(size_t)j * NTAB + lane] = S.b_tab;
   if (lane == 0) {
