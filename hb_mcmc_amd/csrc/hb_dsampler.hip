@@ -355,9 +355,9 @@ __device__ double gauss_batch(WaveStream& S, int& iset, double& gset, const hbgl
 // LDS copy of the exp/log/pow tables.  Lane n < 21 holds coordinate n of x
 // and y; walls and prior terms run one coordinate per lane.  Wave w of block
 // b takes slot order[kPW b + w], order = slots by descending temperature: the
-// hot rungs' long wall runs are dispatched first, a workgroup's four on the
-// four SIMDs of its CU, each sharing its SIMD with colder slots of the CU's
-// later workgroups.
+// hot rungs' long wall runs are dispatched first, and a workgroup's waves
+// (spread over its CU's SIMDs) share each SIMD with colder slots of the CU's
+// later workgroups (measured 37.5 -> 35.2 us against order[b + w grid]).
 __global__ __launch_bounds__(64 * kPW) void ds_propose(Dev D, int W, int NPAST, long long iter) {
   __shared__ uint64_t tab_s[hbglibc::kTabWords];  // exp / log / pow tables (divergent lookups)
   __shared__ double gs_s[kPW][32];
