@@ -62,11 +62,12 @@ HBW_FN double floor_div(double num, double den) {
 // `bottom` receives 2^eb, the lower edge of v's binade.  When no fast-forward
 // is possible the caller folds one at a time; `mode` says for how long:
 //   kFfTop   -- a margin at the binade top: a few folds, then try again;
-//   kFfBinade -- a rounding-tie binade or too little room above the bottom:
-//               fold until |v| drops below `bottom` (the next binade);
+//   kFfBinade -- too little room above the bottom: fold until |v| drops
+//               below `bottom` (the next binade);
 //   kFfNear  -- v's binade is within 2 max(|lo|, |hi|): no lower binade can
-//               fast-forward either, fold to the end.
-enum { kFfDone = 0, kFfTop = 1, kFfBinade = 2, kFfNear = 3 };
+//               fast-forward either, fold to the end;
+//   kFfTie   -- a rounding-tie binade: tie_double_folds.
+enum { kFfDone = 0, kFfTop = 1, kFfBinade = 2, kFfNear = 3, kFfTie = 4 };
 HBW_FN double ff_double_folds(double v, double lo, double hi, int folds_left, int& m_out, int& mode,
                               double& bottom) {
   // every quantity is computed unconditionally and the outcome selected at
@@ -98,10 +99,50 @@ HBW_FN double ff_double_folds(double v, double lo, double hi, int folds_left, in
   if (m > cap) m = cap;
   const bool go = finite && far && !tie && fits && room && m >= 1.0;
   mode = go ? kFfDone
-            : !finite ? kFfTop : !far ? kFfNear : tie ? kFfBinade : !fits ? kFfTop : !room ? kFfBinade : kFfTop;
+            : !finite ? kFfTop : !far ? kFfNear : tie ? kFfTie : !fits ? kFfTop : !room ? kFfBinade : kFfTop;
   m_out = go ? (int)m : 0;
   // exact: integers below 2^53 times a power of two (g = 2^(eb-52))
   return go ? copysign((K - m * D) * ldexp(1.0, eb - 52), v) : v;
+}
+
+// Rounding-tie binade [B, 2B) far from the range (mode kFfTie): 2lo/g or
+// 2hi/g is a half-integer, so that fold rounds half to even and its result
+// depends on the parity of K.  The tie fold's result is always even, so after
+// two plain folds the parity entering every later fold is fixed and each pair
+// of folds again moves the magnitude by constants (first fold c1, the pair
+// -D), which the next plain pair measures.  The remaining pairs that keep
+// every value inside the binade (the margins of ff_double_folds) are then
+// taken at once.  Returns v after the folds made; guard counts them.  A fold
+// that leaves the binade ends it early (the caller folds on one at a time).
+HBW_FN double tie_double_folds(double v, double lo, double hi, double bottom, int& guard) {
+  const double lo2 = 2.0 * lo, hi2 = 2.0 * hi, top = 2.0 * bottom;
+  double x0 = v, xa = v, x1 = v;
+  for (int n = 0; n < 4; ++n) {  // two settling folds, then the measured pair
+    if (guard >= kGuard) return v;
+    v = (v < lo ? lo2 : hi2) - v;
+    ++guard;
+    if (!(fabs(v) >= bottom && fabs(v) < top)) return v;
+    if (n == 1) xa = v;
+    if (n == 2) x1 = v;
+  }
+  (void)x0;
+  int e;
+  frexp(bottom, &e);
+  const int eb = e - 1;
+  const double scale = ldexp(1.0, 52 - eb);  // 1/g
+  const double Ka = fabs(xa) * scale, K1 = fabs(x1) * scale, K2 = fabs(v) * scale;  // exact integers
+  const double c1 = K1 - Ka, D = Ka - K2;
+  if (!(D > 0.0) || !(K2 + (c1 > 0.0 ? c1 : 0.0) <= 0x1p53 - 2.0)) return v;
+  const double n1 = K2 - 0x1p52 - 1.0, n2 = K2 + c1 - 0x1p52 - 1.0;
+  if (!(n1 >= D) || !(n2 >= 0.0)) return v;
+  double m = floor_div(n1, D);
+  const double m2 = floor_div(n2, D) + 1.0;
+  if (m2 < m) m = m2;
+  const double cap = (double)((kGuard - guard) / 2);
+  if (m > cap) m = cap;
+  if (!(m >= 1.0)) return v;
+  guard += 2 * (int)m;
+  return copysign((K2 - m * D) * ldexp(1.0, eb - 52), v);
 }
 
 // v after the walls of one coordinate (flags: 1 reflecting, 2 periodic).
@@ -118,6 +159,10 @@ HBW_FN double apply_wall(double v, double lo, double hi, double fl, double fh) {
       double bottom;
       v = ff_double_folds(v, lo, hi, kGuard - guard, m, mode, bottom);
       guard += 2 * m;
+      if (mode == kFfTie) {  // then fold on until the next binade
+        v = tie_double_folds(v, lo, hi, bottom, guard);
+        mode = kFfBinade;
+      }
       // single folds (the plain loop's own steps): at least 4, then while
       // |v| > stop and fewer than smax.  After a fast-forward (v at the bottom
       // of its binade) or at a binade top, up to 16 take v below the next

@@ -94,3 +94,23 @@ def test_fold_guard_and_endless_runs():
     lo = np.array([0.12, 0.3, 0.12, -1.5])
     hi = np.array([0.20, 0.38, 0.20, 2.0])
     check(v, lo, hi, np.ones(4), np.ones(4))
+
+
+def test_tie_binades_within_reach():
+    """Bounds whose doubled value is a half-integer number of ulps in a binade
+    the excursion crosses (lo = odd * 2^(eb-54), eb in [1, 10]): the folds of
+    those binades round half to even (hb_walls.hpp tie_double_folds)."""
+    rng = np.random.default_rng(5)
+    n = 20000
+    eb = rng.integers(1, 11, n)
+    span = np.ldexp(1.0, 54 - eb)
+    odd = np.floor(rng.uniform(0.05, 2.0, n) * span / 2) * 2 + 1
+    lo = np.ldexp(odd, eb - 54) * np.where(rng.integers(0, 2, n) == 1, 1.0, -1.0)
+    width = 10 ** rng.uniform(-2, 0.5, n)
+    hi = lo + width
+    swap = rng.integers(0, 2, n) == 1  # the tie on the upper bound instead
+    lo, hi = np.where(swap, lo - width, lo), np.where(swap, lo, hi)
+    dist = width * 10 ** rng.uniform(1, 4, n)
+    v = np.where(rng.integers(0, 2, n) == 1, hi + dist, lo - dist)
+    out = check(v, lo, hi, np.ones(n), np.ones(n))
+    assert np.all((out >= lo) & (out <= hi))
