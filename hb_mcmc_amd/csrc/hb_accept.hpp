@@ -1,0 +1,113 @@
+// hb_accept.hpp -- the Hastings test and history write of mcmc_wrapper2.c
+// (:492-546) for one slot, shared by the device sampler's ds_accept kernel
+// (hb_dsampler.hip) and the likelihood kernel's fused epilogue
+// (hb_eval_wave_kernel<..., ACC = true>, hb_kernels.hip), plus the sampler
+// state types both need.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "hb_glibc_math.hpp"
+
+namespace hbds {
+
+constexpr int kNp = 21;
+constexpr int kEvCap = 1024;  // big-jump records between drains (<= 6 per iteration)
+
+struct Counters {
+  long long acc, DEacc, DEtrial, atrial, cold_acc, nswap;
+  long long DEacc_tot, DEtrial_tot;  // sum over slots of DEacc_arr / DEtrial_arr
+  long long acc_it;                  // cold-chain acceptances of this iteration
+  long long snap[4];                 // {acc, DEacc, DEtrial, atrial} as printed at :577-579
+  double logLmap;
+  double xmap[kNp];
+  int nev;
+  int pad;
+};
+
+struct Event {  // LogSuspiciousJumps (:520-528) arguments
+  long long iter;
+  int chain, jtype, slot, pad;
+  double H, alpha, tmp, lx, ly, px, py;
+  double xo[kNp], xn[kNp];
+};
+
+// what the Hastings step of one iteration reads and writes (device pointers)
+struct AccArgs {
+  const int* idx;      // [W] slot -> chain
+  double* logL;        // [W] by chain
+  double* logP;        // [W] by chain
+  const double* logPy; // [W] by slot
+  const double* temp;  // [W]
+  const double* alpha2;
+  const int* jump;
+  const int* jtype;
+  double* x;           // [W][21] by chain
+  const double* y;     // [W][21] by slot
+  double* hist;        // [W][NPAST][21] by slot
+  int* DEacc_arr;
+  Counters* ctr;
+  Event* ev;
+  int log_on, NPAST;
+  long long iter;
+};
+
+// Hastings test of slot j whose proposal has logL ly, by one wave: lane n < 21
+// moves coordinate n (x[chain] = y if accepted, history row k = x[chain]);
+// lane 0 does the scalar bookkeeping.  Same operations and order of effects
+// as ds_accept.
+__device__ inline void accept_slot_wave(const AccArgs& A, int j, double ly, int lane) {
+  const int chain = A.idx[j];
+  const double lx = A.logL[chain];
+  const double H = hbglibc::exp((ly - lx) / A.temp[j] + (A.logPy[j] - A.logP[chain]));
+  const bool acc = A.alpha2[j] <= H;
+  const int k = (int)(A.iter - (A.iter / A.NPAST) * A.NPAST);
+  double xo = 0.0, yn = 0.0;
+  if (lane < kNp) {
+    xo = A.x[(size_t)chain * kNp + lane];
+    yn = A.y[(size_t)j * kNp + lane];
+  }
+  if (acc) {
+    if ((lx / ly <= 0.5) && (A.iter > 10000) && (j <= 5) && A.log_on) {
+      int e = 0;
+      if (lane == 0) e = atomicAdd(&A.ctr->nev, 1);
+      e = __shfl(e, 0);
+      if (e < kEvCap) {
+        Event& ev = A.ev[e];
+        if (lane == 0) {
+          ev.iter = A.iter;
+          ev.chain = chain;
+          ev.jtype = A.jtype[j];
+          ev.slot = j;
+          ev.H = H;
+          ev.alpha = A.alpha2[j];
+          ev.tmp = A.temp[j];
+          ev.lx = lx;
+          ev.ly = ly;
+          ev.px = A.logP[chain];
+          ev.py = A.logPy[j];
+        }
+        if (lane < kNp) {
+          ev.xo[lane] = xo;
+          ev.xn[lane] = yn;
+        }
+      }
+    }
+    if (lane == 0) {
+      if (chain == 0) atomicAdd((unsigned long long*)&A.ctr->acc_it, 1ull);
+      A.logL[chain] = ly;
+      A.logP[chain] = A.logPy[j];
+      if ((A.jump[j] == 1) && (chain == 0)) {
+        A.DEacc_arr[j]++;
+        atomicAdd((unsigned long long*)&A.ctr->DEacc_tot, 1ull);
+      }
+    }
+  }
+  if (lane < kNp) {
+    const double v = acc ? yn : xo;
+    if (acc) A.x[(size_t)chain * kNp + lane] = v;
+    A.hist[((size_t)j * A.NPAST + k) * kNp + lane] = v;
+  }
+}
+
+}  // namespace hbds

@@ -283,7 +283,7 @@ extern "C" int hb_ctx_eval_kind(const hb_ctx* c) {
 }
 
 static int run_batch(hb_ctx* c, const double* d_params, int w, double* d_logl, double* d_tmpl,
-                     hipStream_t s) {
+                     hipStream_t s, const hbds::AccArgs* acc = nullptr) {
   if (!c) return set_err_msg("null context");
   if (w < 0) return set_err_msg("negative walker count");
   if (w == 0) return 0;
@@ -296,9 +296,20 @@ static int run_batch(hb_ctx* c, const double* d_params, int w, double* d_logl, d
   HB_TRY(hbk::launch_prep(d_params, w, c->mags, c->d_wc, s, nullptr, nullptr, c->d_t, c->plan.n, c->d_ph),
          "hb_prep_kernel");
   HB_TRY(hbk::launch_eval(c->plan, c->d_t, c->d_ph, c->d_f, c->d_s, c->d_wc, w, d_logl, d_tmpl, c->d_scratch,
-                          d_tmpl ? 1 : 0, s),
+                          d_tmpl ? 1 : 0, s, acc),
          "hb_eval_kernel");
   return 0;
+}
+
+// internal (device sampler): hb_loglik_batch_dev whose eval waves also run
+// their slot's Hastings test (acc: hbds::AccArgs).  1 when the context's plan
+// has no one-wave path (N > 2048): the caller then launches its own accept.
+extern "C" int hbx_loglik_accept_dev(hb_ctx* c, const double* d_params, int w, double* d_logl, const void* acc,
+                                     void* stream) {
+  if (!c) return set_err_msg("null context");
+  if (c->plan.vpt == 0) return 1;
+  return run_batch(c, d_params, w, d_logl, nullptr, (hipStream_t)stream,
+                   static_cast<const hbds::AccArgs*>(acc));
 }
 
 extern "C" int hb_prepare_dev(hb_ctx* c, const double* d_params, int w, void* stream) {

@@ -29,16 +29,18 @@
 
 #include "../../include/hb_sampler.h"
 #include "../../include/hbmi.h"
+#include "hb_accept.hpp"
 #include "hb_glibc_math.hpp"
 #include "hb_sampler_view.hpp"
 #include "hb_walls.hpp"
 
 extern "C" int hbx_set_error(const char* msg);
 extern "C" int hbx_ctx_device(const hb_ctx* c);
+extern "C" int hbx_loglik_accept_dev(hb_ctx* c, const double* d_params, int w, double* d_logl, const void* acc,
+                                     void* stream);
 
 namespace hbds {
 
-constexpr int kNp = 21;
 constexpr int NTAB = 32;
 constexpr int IM1 = 2147483563, IM2 = 2147483399, IMM1 = IM1 - 1;
 constexpr int IA1 = 40014, IA2 = 40692, IQ1 = 53668, IR1 = 12211;  // IQ2/IR2: idum2 advances by jump-ahead
@@ -56,7 +58,6 @@ constexpr int kBlk = 64;                   // slots per workgroup of the gather 
 constexpr int kPW = HB_DS_KPW;             // propose waves (one slot each) per workgroup
 constexpr int kSwapThreads = 1024;
 constexpr int kMaxLevels = 255;            // swap levels staged in LDS (W = 4096 needs ~10)
-constexpr int kEvCap = 1024;               // big-jump records between drains (<= 6 per iteration)
 
 // run constants (kernel argument)
 struct Params {
@@ -70,23 +71,7 @@ struct Params {
   int gpflag[kNp];
 };
 
-struct Counters {
-  long long acc, DEacc, DEtrial, atrial, cold_acc, nswap;
-  long long DEacc_tot, DEtrial_tot;  // sum over slots of DEacc_arr / DEtrial_arr
-  long long acc_it;                  // cold-chain acceptances of this iteration
-  long long snap[4];                 // {acc, DEacc, DEtrial, atrial} as printed at :577-579
-  double logLmap;
-  double xmap[kNp];
-  int nev;
-  int pad;
-};
-
-struct Event {  // LogSuspiciousJumps (:520-528) arguments
-  long long iter;
-  int chain, jtype, slot, pad;
-  double H, alpha, tmp, lx, ly, px, py;
-  double xo[kNp], xn[kNp];
-};
+// Counters, Event, AccArgs: hb_accept.hpp
 
 // one tempering attempt of the level schedule: pair (b, b+1) and ln(beta) of
 // its acceptance draw (beta itself is kept in a global-only array beside it)
@@ -1153,10 +1138,19 @@ extern "C" int hb_dsampler_step(hb_dsampler* d, long iter) {
   const int NPAST = d->NPAST;
   ds_propose<<<(W + kPW - 1) / kPW, 64 * kPW, 0, s>>>(D, W, NPAST, (long long)iter);
   DS_TRY(hipGetLastError(), "ds_propose");
-  const int rc = hb_loglik_batch_dev(d->ctx, D.y, W, D.logLy, (void*)s);
-  if (rc) return rc;
-  ds_accept<<<(W + 63) / 64, kAccThreads, 0, s>>>(D, W, NPAST, (long long)iter);
-  DS_TRY(hipGetLastError(), "ds_accept");
+  // likelihood with the Hastings test fused into its waves' epilogue
+  // (hb_accept.hpp); ds_accept only where the plan has no one-wave kernel
+  const AccArgs acc{D.idx, D.logL, D.logP, D.logPy, D.temp, D.alpha2, D.jump, D.jtype, D.x, D.y, D.hist,
+                    D.DEacc_arr, D.ctr, D.ev, d->P.log_on, NPAST, (long long)iter};
+  int rc = hbx_loglik_accept_dev(d->ctx, D.y, W, D.logLy, &acc, (void*)s);
+  if (rc == 1) {
+    rc = hb_loglik_batch_dev(d->ctx, D.y, W, D.logLy, (void*)s);
+    if (rc) return rc;
+    ds_accept<<<(W + 63) / 64, kAccThreads, 0, s>>>(D, W, NPAST, (long long)iter);
+    DS_TRY(hipGetLastError(), "ds_accept");
+  } else if (rc) {
+    return rc;
+  }
   DS_TRY(hipStreamWaitEvent(s, d->ev_copy[r], 0), "schedule wait");
   if (d->lds_swap)
     ds_swap<true><<<1, kSwapThreads, d->swap_lds, s>>>(D, W, d_ent, d_off, nlv, (long long)iter);

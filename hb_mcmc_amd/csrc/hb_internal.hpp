@@ -6,6 +6,10 @@
 
 #include "hb_device.hpp"
 
+namespace hbds {
+struct AccArgs;
+}
+
 namespace hbk {
 
 struct MagArgs {
@@ -92,9 +96,12 @@ hipError_t launch_eval_multi(int vpt, size_t slab_bytes, const double* t, const 
                              const hbdev::WalkerConst* wc, double* logl, hipStream_t s);
 int wave_vpt_for(long n);  // cadences per lane of the one-wave path, 0 if n > 2048
 size_t wave_slab_bytes(long n);
+// acc (device sampler, one-wave path only): each wave also runs its slot's
+// Hastings test and history write (hb_accept.hpp); hipErrorNotSupported on the
+// multi-wave path
 hipError_t launch_eval(const EvalPlan& pl, const double* t, const double2* ph, const double* f, const double* sg,
                        const hbdev::WalkerConst* wc, int nwalk, double* logl, double* tmpl,
-                       double* scratch, int mode, hipStream_t s);
+                       double* scratch, int mode, hipStream_t s, const hbds::AccArgs* acc = nullptr);
 hipError_t launch_traj(const double* d_times, int nt, const TrajArgs& ta, double* d, double* z1,
                        double* z2, double* rr, double* ff, hipStream_t s);
 hipError_t launch_probe(int op, const double* d_in, double* d_out, hipStream_t s);

@@ -19,6 +19,7 @@
 #include <stdint.h>
 #include <string.h>
 
+#include "hb_accept.hpp"
 #include "hb_device.hpp"
 #include "hb_internal.hpp"
 
@@ -992,13 +993,16 @@ __device__ __forceinline__ int key_index(int v, int lane) {
 
 // MULTI (catalog mode): the walker is list[blockIdx.x] and its light curve is
 // its target's slice (tab[wt[walker]]); n and kth come from the descriptor.
-template <int VPT, bool MULTI>
+// ACC (device sampler): the wave then runs the Hastings test and history write
+// of its slot (hb_accept.hpp) on the logL it just computed, in place of a
+// separate ds_accept launch.
+template <int VPT, bool MULTI, bool ACC = false>
 __global__ __launch_bounds__(64) HB_WPE_ATTR void hb_eval_wave_kernel(
     const double* __restrict__ t, const double2* __restrict__ ph, const double* __restrict__ f,
     const double* __restrict__ isg,
     long n, long kth, const WalkerConst* __restrict__ wcs, double* __restrict__ logl,
     double* __restrict__ tmpl_out, int mode, int slab_bytes, const TargetDesc* __restrict__ tab,
-    const int* __restrict__ wt, const int* __restrict__ list) {
+    const int* __restrict__ wt, const int* __restrict__ list, hbds::AccArgs hst) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int lane = threadIdx.x;
   int wv = blockIdx.x;
@@ -1018,6 +1022,7 @@ __global__ __launch_bounds__(64) HB_WPE_ATTR void hb_eval_wave_kernel(
   const WalkerConst& w = wcs[wv];
   if (mode == 0 && w.roche != 0.0) {  // likelihood3.c:866-869, see hb_eval_kernel
     if (lane == 0) logl[wv] = -kBig / 2.0;
+    if (ACC) hbds::accept_slot_wave(hst, wv, -kBig / 2.0, lane);
     return;
   }
 
@@ -1093,6 +1098,11 @@ __global__ __launch_bounds__(64) HB_WPE_ATTR void hb_eval_wave_kernel(
     double c = chi2 + w.chi2_extra;
     if (w.roche != 0.0) c = kBig;
     logl[wv] = -c / 2.0;
+  }
+  if (ACC) {
+    double c = chi2 + w.chi2_extra;  // wave-uniform (the DPP sum ends in readlanes)
+    if (w.roche != 0.0) c = kBig;
+    hbds::accept_slot_wave(hst, wv, __shfl(-c / 2.0, 0), lane);
   }
 }
 
@@ -1450,7 +1460,17 @@ static hipError_t launch_wave_t(const EvalPlan& pl, const double* t, const doubl
                                 const WalkerConst* wc, int nwalk, double* logl, double* tmpl, int mode,
                                 hipStream_t s) {
   hipLaunchKernelGGL((hb_eval_wave_kernel<VPT, false>), dim3(nwalk), dim3(64), pl.lds_bytes, s, t, ph, f, sg,
-                     pl.n, pl.kth, wc, logl, tmpl, mode, (int)pl.slab_bytes, nullptr, nullptr, nullptr);
+                     pl.n, pl.kth, wc, logl, tmpl, mode, (int)pl.slab_bytes, nullptr, nullptr, nullptr,
+                     hbds::AccArgs{});
+  return hipGetLastError();
+}
+
+template <int VPT>
+static hipError_t launch_wave_acc_t(const EvalPlan& pl, const double* t, const double2* ph, const double* f,
+                                    const double* sg, const WalkerConst* wc, int nwalk, double* logl,
+                                    hipStream_t s, const hbds::AccArgs& acc) {
+  hipLaunchKernelGGL((hb_eval_wave_kernel<VPT, false, true>), dim3(nwalk), dim3(64), pl.lds_bytes, s, t, ph, f,
+                     sg, pl.n, pl.kth, wc, logl, nullptr, 0, (int)pl.slab_bytes, nullptr, nullptr, nullptr, acc);
   return hipGetLastError();
 }
 
@@ -1461,7 +1481,7 @@ static hipError_t launch_multi_t(size_t slab, const double* t, const double2* ph
                                  const WalkerConst* wc, double* logl, hipStream_t s) {
   const size_t lds = slab + 8 * kCandMax;
   hipLaunchKernelGGL((hb_eval_wave_kernel<VPT, true>), dim3(count), dim3(64), lds, s, t, ph, f, sg, 0L, 0L,
-                     wc, logl, nullptr, 0, (int)slab, tab, wt, list);
+                     wc, logl, nullptr, 0, (int)slab, tab, wt, list, hbds::AccArgs{});
   return hipGetLastError();
 }
 
@@ -1483,8 +1503,20 @@ hipError_t launch_eval_multi(int vpt, size_t slab, const double* t, const double
 
 hipError_t launch_eval(const EvalPlan& pl, const double* t, const double2* ph, const double* f, const double* sg,
                        const WalkerConst* wc, int nwalk, double* logl, double* tmpl, double* scratch,
-                       int mode, hipStream_t s) {
+                       int mode, hipStream_t s, const hbds::AccArgs* acc) {
   if (nwalk <= 0) return hipSuccess;
+  if (acc != nullptr) {  // fused Hastings epilogue: one-wave path only
+    if (mode != 0) return hipErrorInvalidValue;
+    switch (pl.vpt) {
+      case 1: return launch_wave_acc_t<1>(pl, t, ph, f, sg, wc, nwalk, logl, s, *acc);
+      case 2: return launch_wave_acc_t<2>(pl, t, ph, f, sg, wc, nwalk, logl, s, *acc);
+      case 4: return launch_wave_acc_t<4>(pl, t, ph, f, sg, wc, nwalk, logl, s, *acc);
+      case 8: return launch_wave_acc_t<8>(pl, t, ph, f, sg, wc, nwalk, logl, s, *acc);
+      case 16: return launch_wave_acc_t<16>(pl, t, ph, f, sg, wc, nwalk, logl, s, *acc);
+      case 32: return launch_wave_acc_t<32>(pl, t, ph, f, sg, wc, nwalk, logl, s, *acc);
+      default: return hipErrorNotSupported;
+    }
+  }
   switch (pl.vpt) {
     case 0: break;
     case 1: return launch_wave_t<1>(pl, t, ph, f, sg, wc, nwalk, logl, tmpl, mode, s);
