@@ -107,13 +107,12 @@ def test_device_sampler_reproduces_reference_trace(tmp_path):
     assert_gpu_run_matches_reference(tmp_path, g)
 
 
-def _host_vs_device(W, niter, ladder, seed_run=0):
+def _host_vs_device(W, niter, ladder, seed_run=0, n=256):
     from hb_mcmc_amd import synth
     from hb_mcmc_amd.dsampler import DeviceSampler
     from hb_mcmc_amd.likelihood import HBLikelihood
     from hb_mcmc_amd.sampler import SlotSampler
 
-    n = 256
     t = synth.cadences(n)
     with HBLikelihood(t, np.ones(n), np.ones(n)) as tmp:
         truth = tmp.light_curve(synth.THETA_STAR[None, :])[0]
@@ -150,13 +149,18 @@ def _host_vs_device(W, niter, ladder, seed_run=0):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("W,niter,ladder", [(50, 60, 0), (4096, 30, 1), (6000, 24, 1)])
-def test_device_sampler_state_equals_host_sampler(W, niter, ladder):
-    (hx, hl, hc, hs, ha), (dx, dl, dc, ds, da) = _host_vs_device(W, niter, ladder)
+@pytest.mark.parametrize("W,niter,ladder,n", [(50, 60, 0, 256), (4096, 30, 1, 256), (6000, 24, 1, 256),
+                                              (64, 30, 0, 2500)])
+def test_device_sampler_state_equals_host_sampler(W, niter, ladder, n):
+    """n = 2500 takes the multi-wave likelihood plan, where the Hastings test
+    runs as its own ds_accept launch instead of the eval kernel's epilogue."""
+    (hx, hl, hc, hs, ha), (dx, dl, dc, ds, da) = _host_vs_device(W, niter, ladder, n=n)
     assert np.array_equal(hc, dc), "chain ids by slot"
     assert np.array_equal(hx, dx), "states"
     assert np.array_equal(hl, dl), "logL"
     assert hs == ds, (hs, ds)
     for k in ha:
         assert np.array_equal(ha[k], da[k]), k
-    assert hs["cold_acc"] > 0 and hs["nswap"] > 0
+    assert hs["nswap"] > 0
+    if n == 256:  # the sharper 2500-cadence posterior may reject every cold proposal in 30 iterations
+        assert hs["cold_acc"] > 0
