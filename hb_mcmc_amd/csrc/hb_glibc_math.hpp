@@ -1,3 +1,14 @@
+// Derived from the GNU C Library 2.35 (sysdeps/ieee754/dbl-64/e_exp.c, e_log.c,
+// e_pow.c and their data files), which take these algorithms from Arm's
+// optimized-routines:
+//   Copyright (C) 2018-2022 Free Software Foundation, Inc.
+//   Copyright (c) 2018, Arm Limited.
+// The GNU C Library is free software; you can redistribute it and/or modify it
+// under the terms of the GNU Lesser General Public License as published by the
+// Free Software Foundation; either version 2.1 of the License, or (at your
+// option) any later version.  It is distributed WITHOUT ANY WARRANTY; see the
+// GNU Lesser General Public License (LGPL-2.1-or-later) for details.
+//
 // hb_glibc_math.hpp -- glibc 2.35's exp, log and pow, bit for bit, on the
 // host and on gfx950.
 //

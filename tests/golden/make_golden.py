@@ -221,8 +221,21 @@ def limits_fixture(ref: Reference):
 
 
 def pyhb_fixture(g):
-    sys.path.insert(0, os.path.join(ROOT, "oracle", "_ref", "pyhb"))
-    import pyHB  # the reference Cython module, compiled from src/pyHB.pyx
+    # the reference Cython module, compiled from src/pyHB.pyx into a temporary
+    # directory outside the repository and deleted once the vectors are saved
+    tmp = tempfile.mkdtemp(prefix="hb_ref_pyhb_")
+    try:
+        subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "pyhb", f"PYHB_DIR={tmp}"], check=True)
+        sys.path.insert(0, tmp)
+        import pyHB
+        _pyhb_capture(pyHB)
+    finally:
+        if tmp in sys.path:
+            sys.path.remove(tmp)
+        shutil.rmtree(tmp, ignore_errors=True)
+
+
+def _pyhb_capture(pyHB):
 
     th = synth.THETA_STAR
     t = synth.cadences(300)

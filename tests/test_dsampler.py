@@ -125,6 +125,7 @@ def _host_vs_device(W, niter, ladder, seed_run=0, n=256):
     # host loop with the GPU likelihood
     H = SlotSampler(niter, W, logp, 0, W, run=seed_run, npast=npast, ladder=ladder, nthreads=8)
     x, _, _ = H.get()
+    x0 = x.copy()
     H.set_logl(L.loglike(x))
     for it in range(niter):
         y = H.propose(it)
@@ -145,16 +146,17 @@ def _host_vs_device(W, niter, ladder, seed_run=0, n=256):
         xs, ls, cid = S.get()
         out.append((xs, ls, cid, S.stats(), S.state_arrays()))
     L.close()
-    return out
+    return out, x0
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("W,niter,ladder,n", [(50, 60, 0, 256), (4096, 30, 1, 256), (6000, 24, 1, 256),
-                                              (64, 30, 0, 2500)])
+                                              (100, 30, 0, 2500)])
 def test_device_sampler_state_equals_host_sampler(W, niter, ladder, n):
     """n = 2500 takes the multi-wave likelihood plan, where the Hastings test
-    runs as its own ds_accept launch instead of the eval kernel's epilogue."""
-    (hx, hl, hc, hs, ha), (dx, dl, dc, ds, da) = _host_vs_device(W, niter, ladder, n=n)
+    runs as its own ds_accept launch instead of the eval kernel's epilogue;
+    W = 100 leaves the last workgroup partly filled (36 of 64 slots)."""
+    ((hx, hl, hc, hs, ha), (dx, dl, dc, ds, da)), x0 = _host_vs_device(W, niter, ladder, n=n)
     assert np.array_equal(hc, dc), "chain ids by slot"
     assert np.array_equal(hx, dx), "states"
     assert np.array_equal(hl, dl), "logL"
@@ -162,5 +164,8 @@ def test_device_sampler_state_equals_host_sampler(W, niter, ladder, n):
     for k in ha:
         assert np.array_equal(ha[k], da[k]), k
     assert hs["nswap"] > 0
+    # some proposal was accepted: a final state that no initial state equals
+    init = {r.tobytes() for r in x0}
+    assert any(r.tobytes() not in init for r in hx), "no proposal accepted: the accept branch never ran"
     if n == 256:  # the sharper 2500-cadence posterior may reject every cold proposal in 30 iterations
         assert hs["cold_acc"] > 0
