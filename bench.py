@@ -8,8 +8,14 @@ when N > 1, by the RCCL all-gather of every walker's logL (what the tempering
 swap of mcmc_wrapper2.c:554-563 needs).  Inputs are resident in HBM before the
 timed region; the walker batches rotate over 4 pre-generated sets.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config C2|C4|C5]
     torchrun --nproc-per-node N bench.py --gpus N ...
+
+`python bench.py --gpus N` (N > 1, no torchrun environment) starts
+torch.distributed.run with N ranks as a child process before anything touches
+the GPU and exits with its status; under torchrun WORLD_SIZE must equal
+--gpus.  --config C4 is BASELINE config 4: 65 536 walkers sharded over 8 GPUs,
+i.e. 8192 walkers per GPU (weak scaling: 8192 x N global).
 
 Rank 0 prints ONE JSON line.  `value` = evals over all ranks / max-over-ranks
 wall time of the K timed steps.  `roofline` prices the dominant kernel
@@ -53,26 +59,69 @@ def parse():
                     help="process group for N > 1 (nccl = RCCL; gloo only to rehearse ranks sharing one GPU)")
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--config", choices=("C2", "C5"), default="C2",
-                    help="C2: one 1k-cadence light curve (the headline); C5: catalog sweep of --targets "
-                         "light curves (N drawn from 82..1861), --walkers-per-target each, dealt over ranks")
+    ap.add_argument("--config", choices=("C2", "C3", "C4", "C5"), default="C2",
+                    help="C2: one 1k-cadence light curve, 4096 walkers per GPU (the headline); C3: 20k cadences; "
+                         "C4: 1k cadences, 8192 walkers per GPU (65 536 over 8 GPUs); C5: catalog sweep of "
+                         "--targets light curves (N drawn from 82..1861), --walkers-per-target each, dealt over ranks")
     ap.add_argument("--targets", type=int, default=256)
     ap.add_argument("--walkers-per-target", type=int, default=64)
-    ap.add_argument("--walkers", type=int, default=4096, help="walkers per GPU")
-    ap.add_argument("--ncad", type=int, default=1024)
+    ap.add_argument("--walkers", type=int, default=None, help="walkers per GPU (default: 4096; C4: 8192)")
+    ap.add_argument("--ncad", type=int, default=None, help="cadences (default: 1024; C3: 20000)")
+    ap.add_argument("--plumbing-check", action="store_true",
+                    help="launch and rendezvous only: every rank all-gathers its rank id (gloo/RCCL) and rank 0 "
+                         "prints n_gpus; no GPU work (tests the --gpus N launcher on a CPU host)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline sample length")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--timer", choices=("hip", "torch"), default="hip",
                     help="hip: libhbmi's fence-free HIP events (hb_timer_*); torch: torch.cuda.Event")
-    ap.add_argument("--event-every", type=int, default=10,
-                    help="bracket every k-th timed step's kernels with HIP events (an event pair costs "
-                         "~5 us of stream time on this runtime; 1 = every step)")
+    ap.add_argument("--kernel-samples", type=int, default=100,
+                    help="steps of the kernel-timing pass after the timed region: HIP events around every "
+                         "step's prep and eval launches (an event pair costs ~5 us of stream time, so the "
+                         "timed steps carry none)")
     ap.add_argument("--sampler-iters", type=int, default=100,
                     help="also time the whole PT-MCMC iteration (mcmc_wrapper2.c loop) at the workload's W and N: "
                          "device-resident sampler vs the host sampler + GPU likelihood (0 = skip)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
                     help="per-launch HBM bytes measured by rocprofv3 --pmc (see profiles/README.md)")
-    return ap.parse_args()
+    a = ap.parse_args()
+    if a.walkers is None:
+        a.walkers = 8192 if a.config == "C4" else 4096
+    if a.ncad is None:
+        a.ncad = 20000 if a.config == "C3" else 1024
+    return a
+
+
+def free_port() -> int:
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(a) -> int:
+    """`python bench.py --gpus N` outside torchrun: run N ranks through
+    torch.distributed.run in a child process.  Nothing here has touched HIP
+    (importing torch does not), so this process only waits for the child."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    return subprocess.run(cmd, env=env).returncode
+
+
+def plumbing_check(a, rank, world):
+    t = torch.tensor([float(rank)], dtype=torch.float64)
+    if world > 1:
+        out = torch.empty(world, dtype=torch.float64)
+        if a.backend == "nccl":
+            t, out = t.cuda(), out.cuda()
+        dist.all_gather_into_tensor(out, t)
+        got = out.cpu().tolist()
+    else:
+        got = [0.0]
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": None, "unit": "evals/s", "n_gpus": world,
+                          "plumbing": True, "ranks_seen": got, "config": {"workload": a.config}}), flush=True)
 
 
 def cpu_threads() -> int:
@@ -238,23 +287,24 @@ def run_c5(a, rank, world, local, dev):
     for k in range(a.warmup):
         cat.loglike_dev(P[k % nb], wpt, out, stream)
     torch.cuda.synchronize()
-    evs = [[make_event(a.timer) for _ in range(2)] for _ in range(a.steps)]
-    ev_on = [k % max(1, a.event_every) == 0 for k in range(a.steps)]
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for k in range(a.steps):
-        if ev_on[k]:
-            evs[k][0].record(stream)
         cat.loglike_dev(P[k % nb], wpt, out, stream)
-        if ev_on[k]:
-            evs[k][1].record(stream)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     wall = time.perf_counter() - t0
-    call_ms = float(np.mean([e[0].elapsed_time(e[1]) for e, on in zip(evs, ev_on) if on]))
+    ks = max(1, a.kernel_samples)  # kernel-timing pass, events around every call
+    evs = [[make_event(a.timer) for _ in range(2)] for _ in range(ks)]
+    for k in range(ks):
+        evs[k][0].record(stream)
+        cat.loglike_dev(P[k % nb], wpt, out, stream)
+        evs[k][1].record(stream)
+    torch.cuda.synchronize()
+    call_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
     if world > 1:
         tt = torch.tensor([wall, call_ms], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -276,18 +326,34 @@ def run_c5(a, rank, world, local, dev):
                 "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                              "frac": achieved / HBM_PEAK_GBS, "traffic": None,
                              "kernel": "hb_catalog call (prep + hb_eval_wave_kernel<VPT,true> per size class), "
-                                       "rank 0", "kernel_ms": call_ms, "kernel_event_samples": sum(ev_on),
+                                       "rank 0", "kernel_ms": call_ms, "kernel_event_samples": ks,
                              "kernel_timer": a.timer, "bytes_per_step_rank0": bytes_step}}
         print(json.dumps(line), flush=True)
 
 
+def workload_label(a, n, w, world):
+    if a.config == "C4":
+        return (f"C4: synthetic {n}-cadence HB light curve, {w} walkers per GPU x {world} GPU(s) = {w * world} "
+                f"walkers (65 536 at 8 GPUs), logL all-gathered every step")
+    return f"{'C3' if n > 2048 else 'C2'}: synthetic {n}-cadence HB light curve, {w} walkers per GPU"
+
+
 def main():
     a = parse()
+    if "WORLD_SIZE" not in os.environ and a.gpus > 1:
+        sys.exit(launch_ranks(a))
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus:
+        sys.exit(f"bench.py: WORLD_SIZE={world} but --gpus {a.gpus}; launch N ranks for --gpus N")
     if world > 1:
         dist.init_process_group(a.backend)
+    if a.plumbing_check:
+        plumbing_check(a, rank, world)
+        if world > 1:
+            dist.destroy_process_group()
+        return
     local = local % max(1, torch.cuda.device_count())  # rehearsal: several ranks may share one GPU (gloo)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
@@ -343,20 +409,29 @@ def main():
         step(k)
     drain()
     torch.cuda.synchronize()
-    evs = [[make_event(a.timer) for _ in range(3)] for _ in range(a.steps)]
-    ev_on = [k % max(1, a.event_every) == 0 for k in range(a.steps)]
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for k in range(a.steps):
-        step(k, evs[k] if ev_on[k] else None)
+        step(k)
     drain()  # every step's all-gather is inside the timed region
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     wall = time.perf_counter() - t0
-    timed = [e for e, on in zip(evs, ev_on) if on]
+    lv = outs[(a.steps - 1) & 1].cpu().numpy()
+    gl = gathered[(a.steps - 1) & 1].cpu().numpy() if world > 1 else None
+    # kernel durations: a separate pass after the timed region with HIP events
+    # around EVERY step's launches on the stream they run on (an event pair
+    # costs ~5 us of stream time, so they stay out of the timed steps)
+    ks = max(1, a.kernel_samples)
+    evs = [[make_event(a.timer) for _ in range(3)] for _ in range(ks)]
+    for k in range(ks):
+        step(k, evs[k])
+    drain()
+    torch.cuda.synchronize()
+    timed = evs
     prep_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in timed]))
     eval_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in timed]))
     if world > 1:
@@ -365,9 +440,7 @@ def main():
         wall, eval_ms, prep_ms = (float(x) for x in tt.tolist())
     # sanity: the reference's model itself yields NaN for a rare walker (eclipse_area's asin
     # outside its domain, likelihood3.c:353-389) -- reproduced, counted, never more than a trace
-    lv = outs[(a.steps - 1) & 1].cpu().numpy()
     if world > 1:  # the last all-gather holds every rank's logL of that batch, this rank's at its offset
-        gl = gathered[(a.steps - 1) & 1].cpu().numpy()
         assert np.array_equal(gl[rank * w:(rank + 1) * w], lv, equal_nan=True), "all-gather mismatch"
     nonfinite = int((~np.isfinite(lv)).sum())
     assert nonfinite <= max(1, w // 100), f"{nonfinite} non-finite logL of {w}"
@@ -402,8 +475,7 @@ def main():
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (SURVEY.md 8(d): truth = test_likelihoods.c:33-36, t_i = 2P i/N, sigma 1e-3)",
-            "config": {"workload": f"{'C3' if n > 2048 else 'C2'}: synthetic {n}-cadence HB light curve, "
-                                   f"{w} walkers per GPU",
+            "config": {"workload": workload_label(a, n, w, world),
                        "ncad": n, "walkers_per_gpu": w, "global_walkers": world * w,
                        "parallelism": (f"walker-sharded x{world}, logL all-gather over "
                                        f"{'RCCL' if a.backend == 'nccl' else a.backend} each step, overlapped "
