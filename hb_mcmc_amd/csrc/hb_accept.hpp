@@ -32,34 +32,40 @@ struct Event {  // LogSuspiciousJumps (:520-528) arguments
   double xo[kNp], xn[kNp];
 };
 
-// what the Hastings step of one iteration reads and writes (device pointers)
+// what the Hastings step of one iteration reads and writes (device pointers).
+// A sampler may own only the slots [lo, lo + nl) of the W-slot ladder (one
+// rank of a sharded run): arrays "by slot" hold those nl slots (local index
+// j - lo), arrays "by chain" and idx/temp keep all W entries.
 struct AccArgs {
   const int* idx;      // [W] slot -> chain
   double* logL;        // [W] by chain
   double* logP;        // [W] by chain
-  const double* logPy; // [W] by slot
+  const double* logPy; // [nl] by slot
   const double* temp;  // [W]
   const double* alpha2;
   const int* jump;
   const int* jtype;
   double* x;           // [W][21] by chain
-  const double* y;     // [W][21] by slot
-  double* hist;        // [W][NPAST][21] by slot
+  const double* y;     // [nl][21] by slot
+  double* hist;        // [nl][NPAST][21] by slot
   int* DEacc_arr;
   Counters* ctr;
   Event* ev;
   int log_on, NPAST;
   long long iter;
+  int lo;              // first owned slot
+  int pad;
 };
 
-// Hastings test of slot j whose proposal has logL ly, by one wave: lane n < 21
-// moves coordinate n (x[chain] = y if accepted, history row k = x[chain]);
-// lane 0 does the scalar bookkeeping.  Same operations and order of effects
-// as ds_accept.
+// Hastings test of local slot j (global slot lo + j) whose proposal has logL
+// ly, by one wave: lane n < 21 moves coordinate n (x[chain] = y if accepted,
+// history row k = x[chain]); lane 0 does the scalar bookkeeping.  Same
+// operations and order of effects as ds_accept.
 __device__ inline void accept_slot_wave(const AccArgs& A, int j, double ly, int lane) {
-  const int chain = A.idx[j];
+  const int jg = j + A.lo;
+  const int chain = A.idx[jg];
   const double lx = A.logL[chain];
-  const double H = hbglibc::exp((ly - lx) / A.temp[j] + (A.logPy[j] - A.logP[chain]));
+  const double H = hbglibc::exp((ly - lx) / A.temp[jg] + (A.logPy[j] - A.logP[chain]));
   const bool acc = A.alpha2[j] <= H;
   const int k = (int)(A.iter - (A.iter / A.NPAST) * A.NPAST);
   double xo = 0.0, yn = 0.0;
@@ -68,7 +74,7 @@ __device__ inline void accept_slot_wave(const AccArgs& A, int j, double ly, int 
     yn = A.y[(size_t)j * kNp + lane];
   }
   if (acc) {
-    if ((lx / ly <= 0.5) && (A.iter > 10000) && (j <= 5) && A.log_on) {
+    if ((lx / ly <= 0.5) && (A.iter > 10000) && (jg <= 5) && A.log_on) {
       int e = 0;
       if (lane == 0) e = atomicAdd(&A.ctr->nev, 1);
       e = __shfl(e, 0);
@@ -78,10 +84,10 @@ __device__ inline void accept_slot_wave(const AccArgs& A, int j, double ly, int 
           ev.iter = A.iter;
           ev.chain = chain;
           ev.jtype = A.jtype[j];
-          ev.slot = j;
+          ev.slot = jg;
           ev.H = H;
           ev.alpha = A.alpha2[j];
-          ev.tmp = A.temp[j];
+          ev.tmp = A.temp[jg];
           ev.lx = lx;
           ev.ly = ly;
           ev.px = A.logP[chain];

@@ -18,6 +18,20 @@
 //     with the exact exp() test, index[] and logL in LDS.
 // State is kept by chain id like the reference (x[chain], logL[chain],
 // index[slot] -> chain), so a swap moves one int, not a 23-double record.
+//
+// Sharded (one rank of R): the rank owns the contiguous slots
+// [lo, lo + nl), lo = W r / R, with their RNG streams, proposals and history
+// (arrays "by slot" hold only those, local index j - lo).  index[] and the
+// arrays by chain keep all W entries; a chain's record is valid where its
+// slot is owned.  Per iteration the rank proposes, evaluates and tests its
+// slots, then ONE all-gather (the caller's collective, RCCL) carries
+//   * logL of every owned slot (the tempering swaps need all W), and
+//   * the records {chain, logP, logP_ok, x[21]} of the chains in the slots
+//     within nlv of the shard's edges: a swap level moves a chain by at most
+//     one slot, so with nlv levels only those chains can leave the shard;
+// every rank then replays the identical swap schedule (same glibc stream,
+// same logL) on its copy of index[] after importing the other ranks' records,
+// so all ranks hold the same index[] and every owned slot's chain record.
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <string.h>
@@ -88,29 +102,30 @@ __host__ __device__ inline size_t sched_beta_off(size_t W) {
 // device state (pointers into one allocation set)
 struct Dev {
   const Params* P; // run constants (device copy)
+  int lo, nl;      // owned slots [lo, lo + nl); arrays "by slot" below are local (j - lo)
   double* hs;      // [W] tempering factor of the pair (b, b+1): (T_b - T_b+1) / (T_b T_b+1)
   double* x;       // [W][21] by chain
   double* logL;    // [W] by chain
   double* logP;    // [W] by chain
   int* logP_ok;    // [W] by chain
   int* idx;        // [W] slot -> chain
-  int* order;      // [W] propose wave -> slot, hottest rungs first (dispatch order)
+  int* order;      // [nl] propose wave -> (global) slot, hottest rungs first (dispatch order)
   double* temp;    // [W]
-  int* idum;       // [W] ran2 state by slot
+  int* idum;       // [nl] ran2 state by slot
   int* idum2;
   int* iy;
   int* iset;
   double* gset;
   long long* cts;
-  int* iv;         // [W][32] (shuffle table row per slot)
-  double* y;       // [W][21] proposals by slot
-  double* logPy;   // [W]
-  double* alpha2;  // [W]
-  double* logLy;   // [W]
-  int* jump;       // [W]
-  int* jtype;      // [W]
-  double* hist;    // [W][NPAST][21] by slot
-  int* DEacc_arr;  // [W]
+  int* iv;         // [nl][32] (shuffle table row per slot)
+  double* y;       // [nl][21] proposals by slot
+  double* logPy;   // [nl]
+  double* alpha2;  // [nl]
+  double* logLy;   // [nl]
+  int* jump;       // [nl]
+  int* jtype;      // [nl]
+  double* hist;    // [nl][NPAST][21] by slot
+  int* DEacc_arr;  // [nl]
   int* DEtrial_arr;
   Counters* ctr;
   Event* ev;
@@ -361,8 +376,9 @@ __global__ __launch_bounds__(64 * kPW) void ds_propose(Dev D, int W, int NPAST, 
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int k = (int)blockIdx.x * kPW + wv;
-  const bool act = k < W;
-  const int j = act ? D.order[k] : 0;
+  const bool act = k < D.nl;
+  const int j = act ? D.order[k] : D.lo;  // global slot
+  const int jl = j - D.lo;                // local slot (arrays by slot)
   double* gs = gs_s[wv];
 #ifdef HB_DS_TIMING  // experiment builds only: per-phase shader clocks of two slots at iteration 100
   long long tclk[8], tw0 = wall_clock64();
@@ -381,10 +397,10 @@ __global__ __launch_bounds__(64 * kPW) void ds_propose(Dev D, int W, int NPAST, 
   const bool needx = !D.logP_ok[chain];
   const double xn = lane < kNp ? D.x[(size_t)chain * kNp + lane] : 0.0;
   const double temp = D.temp[j];
-  int iset = D.iset[j];
-  double gset = D.gset[j];
+  int iset = D.iset[jl];
+  double gset = D.gset[jl];
   WaveStream S;
-  S.init(D.idum[j], D.idum2[j], D.iy[j], lane < NTAB ? D.iv[(size_t)j * NTAB + lane] : 0);
+  S.init(D.idum[jl], D.idum2[jl], D.iy[jl], lane < NTAB ? D.iv[(size_t)jl * NTAB + lane] : 0);
   __syncthreads();  // tables staged
 #if HB_DS_ABL == 4
   return;
@@ -414,7 +430,7 @@ __global__ __launch_bounds__(64 * kPW) void ds_propose(Dev D, int W, int NPAST, 
   }
   if (jmp == 1) {
     if (chain == 0 && lane == 0) {
-      D.DEtrial_arr[j]++;
+      D.DEtrial_arr[jl]++;
       atomicAdd((unsigned long long*)&D.ctr->DEtrial_tot, 1ull);
     }
     // differential_evolution_proposal_parallel (:1091-1140) as compiled (see
@@ -429,7 +445,7 @@ __global__ __launch_bounds__(64 * kPW) void ds_propose(Dev D, int W, int NPAST, 
     const double gamma = 2.388 / sqrt(2. * kNp);  // GAMMA, mcmc_wrapper2.h:13
     const double gd = scaled ? gauss_batch(S, iset, gset, T, gs) : 0.0;
     if (lane < kNp) {
-      const double* hist = &D.hist[(size_t)j * NPAST * kNp];
+      const double* hist = &D.hist[(size_t)jl * NPAST * kNp];
       double dx = hist[(size_t)ib * kNp + lane] - hist[(size_t)ia * kNp + lane];
       const double eps = dx * g0;
       if (scaled) dx *= gd * gamma;
@@ -475,23 +491,23 @@ __global__ __launch_bounds__(64 * kPW) void ds_propose(Dev D, int W, int NPAST, 
   // stored state, so they follow the walls (off the hot slots' critical path)
   const double alpha2 = S.uniform();  // drawn after the likelihood calls in the reference; same stream order
   S.slide();
-  if (lane < kNp) D.y[(size_t)j * kNp + lane] = yn;
-  if (lane < NTAB) D.iv[(size_t)j * NTAB + lane] = S.b_tab;
+  if (lane < kNp) D.y[(size_t)jl * kNp + lane] = yn;
+  if (lane < NTAB) D.iv[(size_t)jl * NTAB + lane] = S.b_tab;
   if (lane == 0) {
-    D.logPy[j] = lpy;
+    D.logPy[jl] = lpy;
     if (needx) {
       D.logP[chain] = lpx;
       D.logP_ok[chain] = 1;
     }
-    D.jump[j] = jmp;
-    D.jtype[j] = jt;
-    D.alpha2[j] = alpha2;
-    D.idum[j] = S.b_idum;
-    D.idum2[j] = S.b_idum2;
-    D.iy[j] = S.b_iy;
-    D.iset[j] = iset;
-    D.gset[j] = gset;
-    D.cts[j] += S.consumed;
+    D.jump[jl] = jmp;
+    D.jtype[jl] = jt;
+    D.alpha2[jl] = alpha2;
+    D.idum[jl] = S.b_idum;
+    D.idum2[jl] = S.b_idum2;
+    D.iy[jl] = S.b_iy;
+    D.iset[jl] = iset;
+    D.gset[jl] = gset;
+    D.cts[jl] += S.consumed;
   DS_T(7);
   DS_PRINT();
   }
@@ -503,17 +519,17 @@ constexpr int kAccThreads = 256;
 __global__ __launch_bounds__(kAccThreads) void ds_accept(Dev D, int W, int NPAST, long long iter) {
   __shared__ int chain_s[64], acc_s[64];
   const int tid = threadIdx.x, lane = tid;
-  const int j0 = blockIdx.x * 64;
-  const int nw = min(64, W - j0);
+  const int j0 = blockIdx.x * 64;  // local slots j0 .. j0 + nw - 1
+  const int nw = min(64, D.nl - j0);
   const int k = (int)(iter - (iter / NPAST) * NPAST);
   if (lane < nw) {
-    const int j = j0 + lane;
+    const int jl = j0 + lane, j = jl + D.lo;
     const int chain = D.idx[j];
-    const double ly = D.logLy[j], lx = D.logL[chain];
+    const double ly = D.logLy[jl], lx = D.logL[chain];
     const double* xc = &D.x[(size_t)chain * kNp];
-    const double* yj = &D.y[(size_t)j * kNp];
-    const double H = hbglibc::exp((ly - lx) / D.temp[j] + (D.logPy[j] - D.logP[chain]));
-    const bool acc = D.alpha2[j] <= H;
+    const double* yj = &D.y[(size_t)jl * kNp];
+    const double H = hbglibc::exp((ly - lx) / D.temp[j] + (D.logPy[jl] - D.logP[chain]));
+    const bool acc = D.alpha2[jl] <= H;
     chain_s[lane] = chain;
     acc_s[lane] = acc;
     if (acc) {
@@ -523,15 +539,15 @@ __global__ __launch_bounds__(kAccThreads) void ds_accept(Dev D, int W, int NPAST
           Event& ev = D.ev[e];
           ev.iter = iter;
           ev.chain = chain;
-          ev.jtype = D.jtype[j];
+          ev.jtype = D.jtype[jl];
           ev.slot = j;
           ev.H = H;
-          ev.alpha = D.alpha2[j];
+          ev.alpha = D.alpha2[jl];
           ev.tmp = D.temp[j];
           ev.lx = lx;
           ev.ly = ly;
           ev.px = D.logP[chain];
-          ev.py = D.logPy[j];
+          ev.py = D.logPy[jl];
           for (int i = 0; i < kNp; ++i) {
             ev.xo[i] = xc[i];
             ev.xn[i] = yj[i];
@@ -540,9 +556,9 @@ __global__ __launch_bounds__(kAccThreads) void ds_accept(Dev D, int W, int NPAST
       }
       if (chain == 0) atomicAdd((unsigned long long*)&D.ctr->acc_it, 1ull);
       D.logL[chain] = ly;
-      D.logP[chain] = D.logPy[j];
-      if ((D.jump[j] == 1) && (chain == 0)) {
-        D.DEacc_arr[j]++;
+      D.logP[chain] = D.logPy[jl];
+      if ((D.jump[jl] == 1) && (chain == 0)) {
+        D.DEacc_arr[jl]++;
         atomicAdd((unsigned long long*)&D.ctr->DEacc_tot, 1ull);
       }
     }
@@ -591,9 +607,44 @@ struct IdxRef {
 // per-iteration bookkeeping of :551-572 / :590 / :639-641
 // LDS mode stages the schedule, logL by chain, the pair factors and index[]
 // (36 W bytes) so that a level costs LDS latency only.
+// Sharded runs: what a rank contributes to the iteration's all-gather
+// (doubles): logL of its slots (padded to m = the largest shard), then K = 2
+// nlv records of kRec doubles {chain, logP, logP_ok, x[21]} -- the chains in
+// the nlv slots at each edge of the shard (record k < nlv: local slot k;
+// k >= nlv: local slot nl - 2 nlv + k), chain -1 where that slot does not
+// exist (shards smaller than nlv).
+constexpr int kRec = 3 + kNp;
+constexpr int kPackThreads = 256;
+__global__ __launch_bounds__(kPackThreads) void ds_pack(Dev D, double* __restrict__ send, int m, int nlv) {
+  const int q = (int)blockIdx.x * kPackThreads + (int)threadIdx.x;
+  if (q < m) {
+    send[q] = q < D.nl ? D.logL[D.idx[D.lo + q]] : 0.0;
+    return;
+  }
+  const int r = q - m;
+  if (r >= 2 * nlv * kRec) return;
+  const int k = r / kRec, f = r - k * kRec;
+  const int jl = k < nlv ? k : D.nl - 2 * nlv + k;
+  double v = f == 0 ? -1.0 : 0.0;
+  if (jl >= 0 && jl < D.nl) {
+    const int c = D.idx[D.lo + jl];
+    v = f == 0 ? (double)c : f == 1 ? D.logP[c] : f == 2 ? (double)D.logP_ok[c] : D.x[(size_t)c * kNp + (f - 3)];
+  }
+  send[m + r] = v;
+}
+
+// what ds_swap imports in a sharded run (G == nullptr: single process)
+struct Gathered {
+  const double* G;  // [R][S]: each rank's ds_pack output
+  long long S;      // doubles per rank
+  int R, me, m;
+  int pad;
+};
+
 template <bool LDS>
 __global__ __launch_bounds__(kSwapThreads) void ds_swap(Dev D, int W, const SwapEnt* __restrict__ sched,
-                                                         const int* __restrict__ off, int nlv, long long iter) {
+                                                         const int* __restrict__ off, int nlv, long long iter,
+                                                         Gathered X) {
   extern __shared__ __align__(16) unsigned char smem[];
   __shared__ int nacc_s;
   __shared__ int off_s[kMaxLevels + 1];
@@ -605,6 +656,31 @@ __global__ __launch_bounds__(kSwapThreads) void ds_swap(Dev D, int W, const Swap
   for (int q = tid; q < 256; q += kSwapThreads) exp_s[q] = hbglibc::kExpTab[q];
   const hbglibc::Tabs T{exp_s, hbglibc::kLogTab, hbglibc::kPowTab};
   const bool off_lds = nlv <= kMaxLevels;
+  if (X.G) {
+    // sharded: logL of every slot (by its chain before the swap), then the
+    // other ranks' edge records -- each chain is owned by one rank, so no two
+    // ranks write the same chain (a rank's overlapping edges repeat a record)
+    for (int r = 0; r < X.R; ++r) {
+      const int lo_r = (int)((long long)W * r / X.R), n_r = (int)((long long)W * (r + 1) / X.R) - lo_r;
+      const double* g = X.G + (size_t)r * X.S;
+      for (int i = tid; i < n_r; i += kSwapThreads) D.logL[D.idx[lo_r + i]] = g[i];
+    }
+    const int nrec = (int)((X.S - X.m) / kRec);
+    for (int r = 0; r < X.R; ++r) {
+      if (r == X.me) continue;
+      const double* g = X.G + (size_t)r * X.S + X.m;
+      for (int q = tid; q < nrec * kRec; q += kSwapThreads) {
+        const int kk = q / kRec, f = q - kk * kRec;
+        const int c = (int)g[(size_t)kk * kRec];
+        if (c < 0 || f == 0) continue;
+        const double v = g[q];
+        if (f == 1) D.logP[c] = v;
+        else if (f == 2) D.logP_ok[c] = (int)v;
+        else D.x[(size_t)c * kNp + (f - 3)] = v;
+      }
+    }
+    __syncthreads();
+  }
   const SwapEnt* S = sched;
   const double* betas = reinterpret_cast<const double*>(reinterpret_cast<const unsigned char*>(sched) +
                                                          sched_beta_off((size_t)W));
@@ -722,18 +798,18 @@ __global__ __launch_bounds__(kSwapThreads) void ds_swap(Dev D, int W, const Swap
     }
   }
   if (reset)
-    for (int c = tid; c < W; c += kSwapThreads) D.DEacc_arr[c] = D.DEtrial_arr[c] = 0;
+    for (int c = tid; c < D.nl; c += kSwapThreads) D.DEacc_arr[c] = D.DEtrial_arr[c] = 0;
 #ifdef HB_DS_TIMING
   if (tid == 0 && iter == 100)
     printf("swap: start->staged %lld levels(%d) %lld tail %lld\n", sw0 - sstart, nlv, sw1 - sw0, clock64() - sw1);
 #endif
 }
 
-// states and logL by slot (writer / verbose / download)
-__global__ __launch_bounds__(kBlk) void ds_gather(int W, Dev D, double* xs, double* ls, double* ps, int* oks) {
+// states and logL of the owned slots, by local slot (writer / verbose / download)
+__global__ __launch_bounds__(kBlk) void ds_gather(Dev D, double* xs, double* ls, double* ps, int* oks) {
   const int j = blockIdx.x * kBlk + threadIdx.x;
-  if (j >= W) return;
-  const int c = D.idx[j];
+  if (j >= D.nl) return;
+  const int c = D.idx[D.lo + j];
   for (int i = 0; i < kNp; ++i) xs[(size_t)j * kNp + i] = D.x[(size_t)c * kNp + i];
   ls[j] = D.logL[c];
   if (ps) ps[j] = D.logP[c];
@@ -775,23 +851,30 @@ struct hb_dsampler {
   Params* d_params = nullptr;
   Dev D{};
   int W = 0, NPAST = 0, device = 0;
+  // sharding: owned slots [lo, lo + nl) of R ranks; m = largest shard,
+  // nlmin = smallest (edge windows are capped at it)
+  int lo = 0, nl = 0, R = 1, rank = 0, m = 0, nlmin = 0;
   bool lds_swap = true;
   size_t swap_lds = 0;
   std::vector<void*> allocs;
   // swap schedules: pinned ring -> device ring, copied on their own stream
   // (they do not depend on GPU results) so the copy overlaps the iteration's
   // kernels; the swap launch waits on the copy's event
-  static constexpr int R = 4;
+  static constexpr int R_RING = 4;
   hipStream_t cst = nullptr;
-  unsigned char* pin[R] = {};
-  unsigned char* d_sched[R] = {};
-  hipEvent_t ev_copy[R] = {};   // copy r done
-  hipEvent_t ev_used[R] = {};   // swap that read ring entry r done
-  bool used[R] = {};
+  unsigned char* pin[R_RING] = {};
+  unsigned char* d_sched[R_RING] = {};
+  hipEvent_t ev_copy[R_RING] = {};   // copy r done
+  hipEvent_t ev_used[R_RING] = {};   // swap that read ring entry r done
+  bool used[R_RING] = {};
   int ring = 0;
   size_t sched_bytes = 0;
   std::vector<int> b, last, lvl, cnt, order;
   std::vector<double> beta;
+  // the iteration between step_begin and step_end
+  int cur_ring = -1, cur_nlv = 0;
+  long cur_iter = -1;
+  long cur_n = 0;
   // staging for gathers / counters / events
   double* d_xs = nullptr;
   double* d_ls = nullptr;
@@ -803,7 +886,7 @@ struct hb_dsampler {
     if (st) (void)hipStreamSynchronize(st);
     if (cst) (void)hipStreamSynchronize(cst);
     for (void* p : allocs) (void)hipFree(p);
-    for (int r = 0; r < R; ++r) {
+    for (int r = 0; r < R_RING; ++r) {
       if (pin[r]) (void)hipHostFree(pin[r]);
       if (ev_copy[r]) (void)hipEventDestroy(ev_copy[r]);
       if (ev_used[r]) (void)hipEventDestroy(ev_used[r]);
@@ -821,9 +904,12 @@ struct hb_dsampler {
   }
 };
 
-static int ds_upload(hb_dsampler* d);
+static int ds_upload(hb_dsampler* d, const int* chain_of_slot);
 
-extern "C" hb_dsampler* hb_dsampler_create(hb_sampler* s, hb_ctx* ctx) {
+// owned slots of rank r of R (hb_mcmc_amd/dist.py shard())
+static inline int shard_lo(int W, int r, int R) { return (int)((long long)W * r / R); }
+
+static hb_dsampler* ds_create(hb_sampler* s, hb_ctx* ctx, const int* chain_of_slot, int R, int rank) {
   if (!s || !ctx) {
     hbx_set_error("hb_dsampler_create: null sampler or context");
     return nullptr;
@@ -833,15 +919,32 @@ extern "C" hb_dsampler* hb_dsampler_create(hb_sampler* s, hb_ctx* ctx) {
   d->ctx = ctx;
   hbx_sampler_view(s, &d->v);
   const HbSamplerView& v = d->v;
-  if (v.lo != 0 || v.hi != v.W) {
-    hbx_set_error("hb_dsampler_create: the sampler must own every slot (one GPU)");
+  if (R < 1 || rank < 0 || rank >= R || v.W < 2 * R) {
+    hbx_set_error("hb_dsampler_create: bad rank / rank count (every rank needs two slots)");
+    delete d;
+    return nullptr;
+  }
+  if (v.lo != shard_lo(v.W, rank, R) || v.hi != shard_lo(v.W, rank + 1, R)) {
+    hbx_set_error(R == 1 ? "hb_dsampler_create: the sampler must own every slot (one GPU)"
+                         : "hb_dsampler_create_shard: the sampler must own slots [W r/R, W (r+1)/R)");
     delete d;
     return nullptr;
   }
   d->W = v.W;
   d->NPAST = v.NPAST;
+  d->R = R;
+  d->rank = rank;
+  d->lo = v.lo;
+  d->nl = v.hi - v.lo;
+  d->m = 0;
+  d->nlmin = v.W;
+  for (int r = 0; r < R; ++r) {
+    const int n = shard_lo(v.W, r + 1, R) - shard_lo(v.W, r, R);
+    d->m = std::max(d->m, n);
+    d->nlmin = std::min(d->nlmin, n);
+  }
   d->device = hbx_ctx_device(ctx);
-  if (hb_reserve(ctx, v.W)) {  // the likelihood workspace, before anything is enqueued
+  if (hb_reserve(ctx, d->nl)) {  // the likelihood workspace, before anything is enqueued
     delete d;
     return nullptr;
   }
@@ -855,24 +958,27 @@ extern "C" hb_dsampler* hb_dsampler_create(hb_sampler* s, hb_ctx* ctx) {
   if (e != hipSuccess) return fail("hipSetDevice", e);
   if ((e = hipStreamCreateWithFlags(&d->st, hipStreamNonBlocking)) != hipSuccess) return fail("stream", e);
   const int W = d->W;
-  const size_t Wz = (size_t)W;
+  const size_t Wz = (size_t)W, Nz = (size_t)d->nl;
   Dev& D = d->D;
+  D.lo = d->lo;
+  D.nl = d->nl;
+  // by chain / ladder: W entries; by slot: the nl owned slots
   if ((e = d->alloc(&D.x, Wz * kNp)) || (e = d->alloc(&D.logL, Wz)) || (e = d->alloc(&D.logP, Wz)) ||
-      (e = d->alloc(&D.logP_ok, Wz)) || (e = d->alloc(&D.idx, Wz)) || (e = d->alloc(&D.order, Wz)) || (e = d->alloc(&D.temp, Wz)) ||
-      (e = d->alloc(&D.idum, Wz)) || (e = d->alloc(&D.idum2, Wz)) || (e = d->alloc(&D.iy, Wz)) ||
-      (e = d->alloc(&D.iset, Wz)) || (e = d->alloc(&D.gset, Wz)) || (e = d->alloc(&D.cts, Wz)) ||
-      (e = d->alloc(&D.iv, Wz * NTAB)) || (e = d->alloc(&D.y, Wz * kNp)) || (e = d->alloc(&D.logPy, Wz)) ||
-      (e = d->alloc(&D.alpha2, Wz)) || (e = d->alloc(&D.logLy, Wz)) || (e = d->alloc(&D.jump, Wz)) ||
-      (e = d->alloc(&D.jtype, Wz)) || (e = d->alloc(&D.hist, Wz * (size_t)d->NPAST * kNp)) ||
-      (e = d->alloc(&D.DEacc_arr, Wz)) || (e = d->alloc(&D.DEtrial_arr, Wz)) || (e = d->alloc(&D.ctr, 1)) ||
-      (e = d->alloc(&D.ev, (size_t)kEvCap)) || (e = d->alloc(&d->d_xs, Wz * kNp)) ||
-      (e = d->alloc(&d->d_ls, Wz)) || (e = d->alloc(&d->d_ps, Wz)) || (e = d->alloc(&d->d_ok, Wz)) ||
-      (e = d->alloc(&D.hs, Wz)) || (e = d->alloc(&d->d_params, 1)))
+      (e = d->alloc(&D.logP_ok, Wz)) || (e = d->alloc(&D.idx, Wz)) || (e = d->alloc(&D.order, Nz)) ||
+      (e = d->alloc(&D.temp, Wz)) || (e = d->alloc(&D.idum, Nz)) || (e = d->alloc(&D.idum2, Nz)) ||
+      (e = d->alloc(&D.iy, Nz)) || (e = d->alloc(&D.iset, Nz)) || (e = d->alloc(&D.gset, Nz)) ||
+      (e = d->alloc(&D.cts, Nz)) || (e = d->alloc(&D.iv, Nz * NTAB)) || (e = d->alloc(&D.y, Nz * kNp)) ||
+      (e = d->alloc(&D.logPy, Nz)) || (e = d->alloc(&D.alpha2, Nz)) || (e = d->alloc(&D.logLy, Nz)) ||
+      (e = d->alloc(&D.jump, Nz)) || (e = d->alloc(&D.jtype, Nz)) ||
+      (e = d->alloc(&D.hist, Nz * (size_t)d->NPAST * kNp)) || (e = d->alloc(&D.DEacc_arr, Nz)) ||
+      (e = d->alloc(&D.DEtrial_arr, Nz)) || (e = d->alloc(&D.ctr, 1)) || (e = d->alloc(&D.ev, (size_t)kEvCap)) ||
+      (e = d->alloc(&d->d_xs, Nz * kNp)) || (e = d->alloc(&d->d_ls, Nz)) || (e = d->alloc(&d->d_ps, Nz)) ||
+      (e = d->alloc(&d->d_ok, Nz)) || (e = d->alloc(&D.hs, Wz)) || (e = d->alloc(&d->d_params, 1)))
     return fail("hipMalloc", e);
   D.P = d->d_params;
   if ((e = hipStreamCreateWithFlags(&d->cst, hipStreamNonBlocking)) != hipSuccess) return fail("stream", e);
   d->sched_bytes = sched_beta_off(Wz) + sizeof(double) * Wz;
-  for (int r = 0; r < hb_dsampler::R; ++r) {
+  for (int r = 0; r < hb_dsampler::R_RING; ++r) {
     if ((e = d->alloc(&d->d_sched[r], d->sched_bytes))) return fail("hipMalloc", e);
     if ((e = hipHostMalloc((void**)&d->pin[r], d->sched_bytes, hipHostMallocDefault))) return fail("pinned", e);
     if ((e = hipEventCreateWithFlags(&d->ev_copy[r], hipEventDisableTiming))) return fail("event", e);
@@ -907,40 +1013,59 @@ extern "C" hb_dsampler* hb_dsampler_create(hb_sampler* s, hb_ctx* ctx) {
     P.sigma_p[i] = v.sigma_p[i];
     P.gpflag[i] = v.gp[i].flag;
   }
-  if (ds_upload(d)) {
+  if (ds_upload(d, chain_of_slot)) {
     delete d;
     return nullptr;
   }
   return d;
 }
 
+extern "C" hb_dsampler* hb_dsampler_create(hb_sampler* s, hb_ctx* ctx) { return ds_create(s, ctx, nullptr, 1, 0); }
+
+extern "C" hb_dsampler* hb_dsampler_create_shard(hb_sampler* s, hb_ctx* ctx, const int* chain_of_slot, int nranks,
+                                                 int rank) {
+  if (!chain_of_slot) {
+    hbx_set_error("hb_dsampler_create_shard: chain_of_slot is required");
+    return nullptr;
+  }
+  return ds_create(s, ctx, chain_of_slot, nranks, rank);
+}
+
 extern "C" void hb_dsampler_destroy(hb_dsampler* d) { delete d; }
 
-// host sampler (by slot) -> device (by chain)
-static int ds_upload(hb_dsampler* d) {
+// host sampler (owned slots, by slot) -> device (by chain); chain_of_slot
+// (all W slots) may be NULL when the sampler owns every slot
+static int ds_upload(hb_dsampler* d, const int* chain_of_slot) {
   const HbSamplerView& v = d->v;
-  const int W = d->W;
-  const size_t Wz = (size_t)W;
+  const int W = d->W, lo = d->lo, nl = d->nl;
+  const size_t Wz = (size_t)W, Nz = (size_t)nl;
   Dev& D = d->D;
-  std::vector<double> x(Wz * kNp), L(Wz), Pp(Wz), gset(Wz);
-  std::vector<int> ok(Wz), idx(Wz), idum(Wz), idum2(Wz), iy(Wz), iset(Wz), iv(Wz * NTAB);
-  std::vector<long long> cts(Wz);
+  std::vector<double> x(Wz * kNp, 0.0), L(Wz, 0.0), Pp(Wz, 0.0), gset(Nz);
+  std::vector<int> ok(Wz, 0), idx(Wz), idum(Nz), idum2(Nz), iy(Nz), iset(Nz), iv(Nz * NTAB);
+  std::vector<long long> cts(Nz);
+  std::vector<char> seen(Wz, 0);
   for (int j = 0; j < W; ++j) {
-    const int c = v.cid[j];
+    const int c = chain_of_slot ? chain_of_slot[j] : v.cid[j];
+    if (c < 0 || c >= W || seen[c]) return hbx_set_error("hb_dsampler: chain_of_slot is not a permutation");
+    seen[c] = 1;
     idx[j] = c;
-    memcpy(&x[(size_t)c * kNp], &v.x[(size_t)j * kNp], sizeof(double) * kNp);
-    L[c] = v.logL[j];
-    Pp[c] = v.logP[j];
-    ok[c] = v.logP_ok[j] ? 1 : 0;
-    const RNG_Vars& r = v.states[j];
-    if (v.seeds[j] > 2147483647L || v.seeds[j] < -2147483647L) return hbx_set_error("hb_dsampler: seed out of range");
-    idum[j] = (int)v.seeds[j];
-    idum2[j] = (int)r.idum2;
-    iy[j] = (int)r.iy;
-    iset[j] = r.iset;
-    gset[j] = r.gset;
-    cts[j] = r.cts;
-    for (int t = 0; t < NTAB; ++t) iv[(size_t)j * NTAB + t] = (int)r.iv[t];
+  }
+  for (int jl = 0; jl < nl; ++jl) {
+    const int c = v.cid[jl];
+    if (idx[lo + jl] != c) return hbx_set_error("hb_dsampler: chain_of_slot disagrees with the sampler's slots");
+    memcpy(&x[(size_t)c * kNp], &v.x[(size_t)jl * kNp], sizeof(double) * kNp);
+    L[c] = v.logL[jl];
+    Pp[c] = v.logP[jl];
+    ok[c] = v.logP_ok[jl] ? 1 : 0;
+    const RNG_Vars& r = v.states[jl];
+    if (v.seeds[jl] > 2147483647L || v.seeds[jl] < -2147483647L) return hbx_set_error("hb_dsampler: seed out of range");
+    idum[jl] = (int)v.seeds[jl];
+    idum2[jl] = (int)r.idum2;
+    iy[jl] = (int)r.iy;
+    iset[jl] = r.iset;
+    gset[jl] = r.gset;
+    cts[jl] = r.cts;
+    for (int t = 0; t < NTAB; ++t) iv[(size_t)jl * NTAB + t] = (int)r.iv[t];
   }
   Counters c{};
   c.acc = *v.acc;
@@ -949,10 +1074,10 @@ static int ds_upload(hb_dsampler* d) {
   c.atrial = *v.atrial;
   c.cold_acc = *v.cold_acc;
   c.nswap = *v.nswap;
-  for (int j = 0; j < W; ++j) {
-    c.DEacc_tot += v.DEacc_arr[j];
-    c.DEtrial_tot += v.DEtrial_arr[j];
-    c.acc_it += v.acc_arr[j];
+  for (int jl = 0; jl < nl; ++jl) {
+    c.DEacc_tot += v.DEacc_arr[jl];
+    c.DEtrial_tot += v.DEtrial_arr[jl];
+    c.acc_it += v.acc_arr[jl];
   }
   c.logLmap = -1.0 / 0.0;
   hipStream_t s = d->st;
@@ -966,10 +1091,10 @@ static int ds_upload(hb_dsampler* d) {
   // propose waves in descending temperature: the hot rungs' long wall runs
   // are dispatched first (ds_propose lasts as long as its latest-finishing
   // wave), kPW consecutive ones per workgroup
-  d->order.resize(Wz);
-  for (size_t i = 0; i < Wz; ++i) d->order[i] = (int)i;
+  d->order.resize(Nz);
+  for (size_t i = 0; i < Nz; ++i) d->order[i] = lo + (int)i;
   std::stable_sort(d->order.begin(), d->order.end(), [&](int a, int b) { return v.temp[a] > v.temp[b]; });
-  DS_TRY(hipMemcpyAsync(D.order, d->order.data(), sizeof(int) * Wz, hipMemcpyHostToDevice, s), "upload");
+  DS_TRY(hipMemcpyAsync(D.order, d->order.data(), sizeof(int) * Nz, hipMemcpyHostToDevice, s), "upload");
   std::vector<double> hs(Wz, 0.0);
   for (int b = 0; b + 1 < W; ++b) {  // ptmcmc's H (:803) for the pair (a, b) = (b+1, b): same IEEE ops
     const double heat1 = v.temp[b + 1], heat2 = v.temp[b];
@@ -977,57 +1102,57 @@ static int ds_upload(hb_dsampler* d) {
   }
   DS_TRY(hipMemcpyAsync(D.hs, hs.data(), sizeof(double) * Wz, hipMemcpyHostToDevice, s), "upload");
   DS_TRY(hipMemcpyAsync(d->d_params, &d->P, sizeof(Params), hipMemcpyHostToDevice, s), "upload");
-  DS_TRY(hipMemcpyAsync(D.idum, idum.data(), sizeof(int) * Wz, hipMemcpyHostToDevice, s), "upload");
-  DS_TRY(hipMemcpyAsync(D.idum2, idum2.data(), sizeof(int) * Wz, hipMemcpyHostToDevice, s), "upload");
-  DS_TRY(hipMemcpyAsync(D.iy, iy.data(), sizeof(int) * Wz, hipMemcpyHostToDevice, s), "upload");
-  DS_TRY(hipMemcpyAsync(D.iset, iset.data(), sizeof(int) * Wz, hipMemcpyHostToDevice, s), "upload");
-  DS_TRY(hipMemcpyAsync(D.gset, gset.data(), sizeof(double) * Wz, hipMemcpyHostToDevice, s), "upload");
-  DS_TRY(hipMemcpyAsync(D.cts, cts.data(), sizeof(long long) * Wz, hipMemcpyHostToDevice, s), "upload");
+  DS_TRY(hipMemcpyAsync(D.idum, idum.data(), sizeof(int) * Nz, hipMemcpyHostToDevice, s), "upload");
+  DS_TRY(hipMemcpyAsync(D.idum2, idum2.data(), sizeof(int) * Nz, hipMemcpyHostToDevice, s), "upload");
+  DS_TRY(hipMemcpyAsync(D.iy, iy.data(), sizeof(int) * Nz, hipMemcpyHostToDevice, s), "upload");
+  DS_TRY(hipMemcpyAsync(D.iset, iset.data(), sizeof(int) * Nz, hipMemcpyHostToDevice, s), "upload");
+  DS_TRY(hipMemcpyAsync(D.gset, gset.data(), sizeof(double) * Nz, hipMemcpyHostToDevice, s), "upload");
+  DS_TRY(hipMemcpyAsync(D.cts, cts.data(), sizeof(long long) * Nz, hipMemcpyHostToDevice, s), "upload");
   DS_TRY(hipMemcpyAsync(D.iv, iv.data(), sizeof(int) * iv.size(), hipMemcpyHostToDevice, s), "upload");
-  DS_TRY(hipMemcpyAsync(D.hist, v.hist, sizeof(double) * Wz * d->NPAST * kNp, hipMemcpyHostToDevice, s),
+  DS_TRY(hipMemcpyAsync(D.hist, v.hist, sizeof(double) * Nz * d->NPAST * kNp, hipMemcpyHostToDevice, s),
          "upload");
-  DS_TRY(hipMemcpyAsync(D.DEacc_arr, v.DEacc_arr, sizeof(int) * Wz, hipMemcpyHostToDevice, s), "upload");
-  DS_TRY(hipMemcpyAsync(D.DEtrial_arr, v.DEtrial_arr, sizeof(int) * Wz, hipMemcpyHostToDevice, s), "upload");
+  DS_TRY(hipMemcpyAsync(D.DEacc_arr, v.DEacc_arr, sizeof(int) * Nz, hipMemcpyHostToDevice, s), "upload");
+  DS_TRY(hipMemcpyAsync(D.DEtrial_arr, v.DEtrial_arr, sizeof(int) * Nz, hipMemcpyHostToDevice, s), "upload");
   DS_TRY(hipMemcpyAsync(D.ctr, &c, sizeof c, hipMemcpyHostToDevice, s), "upload");
   DS_TRY(hipStreamSynchronize(s), "upload sync");
   return 0;
 }
 
-// device -> host sampler (by slot); also drains the big-jump records
+// device -> host sampler (owned slots, by slot); also drains the big-jump records
 static int ds_drain_events(hb_dsampler* d);
 
 extern "C" int hb_dsampler_download(hb_dsampler* d) {
   if (!d) return hbx_set_error("hb_dsampler_download: null");
   const HbSamplerView& v = d->v;
-  const int W = d->W;
-  const size_t Wz = (size_t)W;
+  const int nl = d->nl;
+  const size_t Nz = (size_t)nl;
   Dev& D = d->D;
   hipStream_t s = d->st;
   DS_TRY(hipSetDevice(d->device), "hipSetDevice");
-  ds_gather<<<(W + kBlk - 1) / kBlk, kBlk, 0, s>>>(W, D, d->d_xs, d->d_ls, d->d_ps, d->d_ok);
+  ds_gather<<<(nl + kBlk - 1) / kBlk, kBlk, 0, s>>>(D, d->d_xs, d->d_ls, d->d_ps, d->d_ok);
   DS_TRY(hipGetLastError(), "gather");
-  std::vector<int> idx(Wz), ok(Wz), idum(Wz), idum2(Wz), iy(Wz), iset(Wz), iv(Wz * NTAB);
-  std::vector<double> gset(Wz);
-  std::vector<long long> cts(Wz);
-  DS_TRY(hipMemcpyAsync(v.x, d->d_xs, sizeof(double) * Wz * kNp, hipMemcpyDeviceToHost, s), "download");
-  DS_TRY(hipMemcpyAsync(v.logL, d->d_ls, sizeof(double) * Wz, hipMemcpyDeviceToHost, s), "download");
-  DS_TRY(hipMemcpyAsync(v.logP, d->d_ps, sizeof(double) * Wz, hipMemcpyDeviceToHost, s), "download");
-  DS_TRY(hipMemcpyAsync(ok.data(), d->d_ok, sizeof(int) * Wz, hipMemcpyDeviceToHost, s), "download");
-  DS_TRY(hipMemcpyAsync(idx.data(), D.idx, sizeof(int) * Wz, hipMemcpyDeviceToHost, s), "download");
-  DS_TRY(hipMemcpyAsync(idum.data(), D.idum, sizeof(int) * Wz, hipMemcpyDeviceToHost, s), "download");
-  DS_TRY(hipMemcpyAsync(idum2.data(), D.idum2, sizeof(int) * Wz, hipMemcpyDeviceToHost, s), "download");
-  DS_TRY(hipMemcpyAsync(iy.data(), D.iy, sizeof(int) * Wz, hipMemcpyDeviceToHost, s), "download");
-  DS_TRY(hipMemcpyAsync(iset.data(), D.iset, sizeof(int) * Wz, hipMemcpyDeviceToHost, s), "download");
-  DS_TRY(hipMemcpyAsync(gset.data(), D.gset, sizeof(double) * Wz, hipMemcpyDeviceToHost, s), "download");
-  DS_TRY(hipMemcpyAsync(cts.data(), D.cts, sizeof(long long) * Wz, hipMemcpyDeviceToHost, s), "download");
+  std::vector<int> idx(Nz), ok(Nz), idum(Nz), idum2(Nz), iy(Nz), iset(Nz), iv(Nz * NTAB);
+  std::vector<double> gset(Nz);
+  std::vector<long long> cts(Nz);
+  DS_TRY(hipMemcpyAsync(v.x, d->d_xs, sizeof(double) * Nz * kNp, hipMemcpyDeviceToHost, s), "download");
+  DS_TRY(hipMemcpyAsync(v.logL, d->d_ls, sizeof(double) * Nz, hipMemcpyDeviceToHost, s), "download");
+  DS_TRY(hipMemcpyAsync(v.logP, d->d_ps, sizeof(double) * Nz, hipMemcpyDeviceToHost, s), "download");
+  DS_TRY(hipMemcpyAsync(ok.data(), d->d_ok, sizeof(int) * Nz, hipMemcpyDeviceToHost, s), "download");
+  DS_TRY(hipMemcpyAsync(idx.data(), D.idx + d->lo, sizeof(int) * Nz, hipMemcpyDeviceToHost, s), "download");
+  DS_TRY(hipMemcpyAsync(idum.data(), D.idum, sizeof(int) * Nz, hipMemcpyDeviceToHost, s), "download");
+  DS_TRY(hipMemcpyAsync(idum2.data(), D.idum2, sizeof(int) * Nz, hipMemcpyDeviceToHost, s), "download");
+  DS_TRY(hipMemcpyAsync(iy.data(), D.iy, sizeof(int) * Nz, hipMemcpyDeviceToHost, s), "download");
+  DS_TRY(hipMemcpyAsync(iset.data(), D.iset, sizeof(int) * Nz, hipMemcpyDeviceToHost, s), "download");
+  DS_TRY(hipMemcpyAsync(gset.data(), D.gset, sizeof(double) * Nz, hipMemcpyDeviceToHost, s), "download");
+  DS_TRY(hipMemcpyAsync(cts.data(), D.cts, sizeof(long long) * Nz, hipMemcpyDeviceToHost, s), "download");
   DS_TRY(hipMemcpyAsync(iv.data(), D.iv, sizeof(int) * iv.size(), hipMemcpyDeviceToHost, s), "download");
-  DS_TRY(hipMemcpyAsync(v.hist, D.hist, sizeof(double) * Wz * d->NPAST * kNp, hipMemcpyDeviceToHost, s),
+  DS_TRY(hipMemcpyAsync(v.hist, D.hist, sizeof(double) * Nz * d->NPAST * kNp, hipMemcpyDeviceToHost, s),
          "download");
-  DS_TRY(hipMemcpyAsync(v.DEacc_arr, D.DEacc_arr, sizeof(int) * Wz, hipMemcpyDeviceToHost, s), "download");
-  DS_TRY(hipMemcpyAsync(v.DEtrial_arr, D.DEtrial_arr, sizeof(int) * Wz, hipMemcpyDeviceToHost, s), "download");
+  DS_TRY(hipMemcpyAsync(v.DEacc_arr, D.DEacc_arr, sizeof(int) * Nz, hipMemcpyDeviceToHost, s), "download");
+  DS_TRY(hipMemcpyAsync(v.DEtrial_arr, D.DEtrial_arr, sizeof(int) * Nz, hipMemcpyDeviceToHost, s), "download");
   DS_TRY(hipMemcpyAsync(d->h_ctr, D.ctr, sizeof(Counters), hipMemcpyDeviceToHost, s), "download");
   DS_TRY(hipStreamSynchronize(s), "download sync");
-  for (int j = 0; j < W; ++j) {
+  for (int j = 0; j < nl; ++j) {
     v.cid[j] = idx[j];
     v.logP_ok[j] = (char)ok[j];
     v.seeds[j] = idum[j];
@@ -1071,26 +1196,51 @@ static int ds_drain_events(hb_dsampler* d) {
   return 0;
 }
 
+namespace hbds {
+// logL[chain of owned slot j] = ls[j]
+__global__ __launch_bounds__(kBlk) void ds_scatter_logl(Dev D, const double* __restrict__ ls) {
+  const int j = blockIdx.x * kBlk + threadIdx.x;
+  if (j < D.nl) D.logL[D.idx[D.lo + j]] = ls[j];
+}
+}  // namespace hbds
+
 // iteration-0 recompute (:488): logL of every current state, and the MAP
-// tracker seeded with chain 0's state (:342)
+// tracker seeded with chain 0's state (:342; the rank owning chain 0)
 extern "C" int hb_dsampler_init_logl(hb_dsampler* d) {
   if (!d) return hbx_set_error("hb_dsampler_init_logl: null");
   DS_TRY(hipSetDevice(d->device), "hipSetDevice");
-  const int rc = hb_loglik_batch_dev(d->ctx, d->D.x, d->W, d->D.logL, (void*)d->st);
-  if (rc) return rc;
+  if (d->R == 1) {
+    const int rc = hb_loglik_batch_dev(d->ctx, d->D.x, d->W, d->D.logL, (void*)d->st);
+    if (rc) return rc;
+  } else {  // owned slots only: states by slot -> likelihood -> logL by chain
+    ds_gather<<<(d->nl + kBlk - 1) / kBlk, kBlk, 0, d->st>>>(d->D, d->d_xs, d->d_ls, nullptr, nullptr);
+    DS_TRY(hipGetLastError(), "gather");
+    const int rc = hb_loglik_batch_dev(d->ctx, d->d_xs, d->nl, d->d_ls, (void*)d->st);
+    if (rc) return rc;
+    ds_scatter_logl<<<(d->nl + kBlk - 1) / kBlk, kBlk, 0, d->st>>>(d->D, d->d_ls);
+    DS_TRY(hipGetLastError(), "scatter");
+  }
   // logLmap = logL(x of chain 0), xmap = x of chain 0
   DS_TRY(hipMemcpyAsync(&d->D.ctr->logLmap, d->D.logL, sizeof(double), hipMemcpyDeviceToDevice, d->st), "map");
   DS_TRY(hipMemcpyAsync(d->D.ctr->xmap, d->D.x, sizeof(double) * kNp, hipMemcpyDeviceToDevice, d->st), "map");
   return 0;
 }
 
-// one iteration, enqueued on the sampler's stream (no host wait)
-extern "C" int hb_dsampler_step(hb_dsampler* d, long iter) {
-  if (!d) return hbx_set_error("hb_dsampler_step: null");
+extern "C" long hb_dsampler_exchange_cap(const hb_dsampler* d) {
+  if (!d) return hbx_set_error("hb_dsampler_exchange_cap: null");
+  return (long)d->m + 2L * d->nlmin * kRec;
+}
+
+extern "C" void* hb_dsampler_stream(hb_dsampler* d) { return d ? (void*)d->st : nullptr; }
+
+// first half of an iteration: the swap schedule (host, into the pinned ring),
+// proposals, likelihood + Hastings test of the owned slots; sharded runs
+// also pack the rank's all-gather contribution into send
+static long ds_begin(hb_dsampler* d, long iter, double* send, long cap) {
   const int W = d->W;
-  const Params& P = d->P;
   const Dev& D = d->D;
   hipStream_t s = d->st;
+  if (d->cur_iter >= 0) return hbx_set_error("hb_dsampler: step_begin twice without step_end");
   DS_TRY(hipSetDevice(d->device), "hipSetDevice");
   // swap schedule of this iteration (draws in the reference's order)
   hbx_swap_draws(d->s, d->b.data(), d->beta.data());
@@ -1108,7 +1258,7 @@ extern "C" int hb_dsampler_step(hb_dsampler* d, long iter) {
     nlv = std::max(nlv, l);
   }
   const int r = d->ring;
-  d->ring = (d->ring + 1) % hb_dsampler::R;
+  d->ring = (d->ring + 1) % hb_dsampler::R_RING;
   if (d->used[r]) DS_TRY(hipEventSynchronize(d->ev_used[r]), "schedule ring");  // entry r free again
   SwapEnt* ent = reinterpret_cast<SwapEnt*>(d->pin[r]);
   int* off = reinterpret_cast<int*>(d->pin[r] + sizeof(SwapEnt) * (size_t)W);
@@ -1132,51 +1282,102 @@ extern "C" int hb_dsampler_step(hb_dsampler* d, long iter) {
   const size_t used_bytes = sched_beta_off(W) + sizeof(double) * (size_t)W;
   DS_TRY(hipMemcpyAsync(d->d_sched[r], d->pin[r], used_bytes, hipMemcpyHostToDevice, d->cst), "schedule upload");
   DS_TRY(hipEventRecord(d->ev_copy[r], d->cst), "schedule ring");
-  const SwapEnt* d_ent = reinterpret_cast<const SwapEnt*>(d->d_sched[r]);
-  const int* d_off = reinterpret_cast<const int*>(d->d_sched[r] + sizeof(SwapEnt) * (size_t)W);
 
-  const int NPAST = d->NPAST;
-  ds_propose<<<(W + kPW - 1) / kPW, 64 * kPW, 0, s>>>(D, W, NPAST, (long long)iter);
+  const int NPAST = d->NPAST, nl = d->nl;
+  ds_propose<<<(nl + kPW - 1) / kPW, 64 * kPW, 0, s>>>(D, W, NPAST, (long long)iter);
   DS_TRY(hipGetLastError(), "ds_propose");
   // likelihood with the Hastings test fused into its waves' epilogue
   // (hb_accept.hpp); ds_accept only where the plan has no one-wave kernel
   const AccArgs acc{D.idx, D.logL, D.logP, D.logPy, D.temp, D.alpha2, D.jump, D.jtype, D.x, D.y, D.hist,
-                    D.DEacc_arr, D.ctr, D.ev, d->P.log_on, NPAST, (long long)iter};
-  int rc = hbx_loglik_accept_dev(d->ctx, D.y, W, D.logLy, &acc, (void*)s);
+                    D.DEacc_arr, D.ctr, D.ev, d->P.log_on, NPAST, (long long)iter, d->lo, 0};
+  int rc = hbx_loglik_accept_dev(d->ctx, D.y, nl, D.logLy, &acc, (void*)s);
   if (rc == 1) {
-    rc = hb_loglik_batch_dev(d->ctx, D.y, W, D.logLy, (void*)s);
+    rc = hb_loglik_batch_dev(d->ctx, D.y, nl, D.logLy, (void*)s);
     if (rc) return rc;
-    ds_accept<<<(W + 63) / 64, kAccThreads, 0, s>>>(D, W, NPAST, (long long)iter);
+    ds_accept<<<(nl + 63) / 64, kAccThreads, 0, s>>>(D, W, NPAST, (long long)iter);
     DS_TRY(hipGetLastError(), "ds_accept");
   } else if (rc) {
     return rc;
   }
+  long n = 0;
+  if (d->R > 1) {
+    const int ke = std::min(nlv, d->nlmin);  // edge window (a level moves a chain by one slot)
+    n = (long)d->m + 2L * ke * kRec;
+    if (!send || n > cap) return hbx_set_error("hb_dsampler_step_begin: send buffer missing or too small");
+    const long thr = n;
+    ds_pack<<<(unsigned)((thr + kPackThreads - 1) / kPackThreads), kPackThreads, 0, s>>>(D, send, d->m, ke);
+    DS_TRY(hipGetLastError(), "ds_pack");
+  }
+  d->cur_ring = r;
+  d->cur_nlv = nlv;
+  d->cur_iter = iter;
+  d->cur_n = n;
+  return n;
+}
+
+// second half: import the all-gather (sharded), tempering swaps, bookkeeping
+static int ds_end(hb_dsampler* d, long iter, const double* recv, long n) {
+  const int W = d->W;
+  const Dev& D = d->D;
+  hipStream_t s = d->st;
+  if (d->cur_iter != iter) return hbx_set_error("hb_dsampler_step_end: no step_begin for this iteration");
+  if (d->R > 1 && (!recv || n != d->cur_n))
+    return hbx_set_error("hb_dsampler_step_end: gathered buffer missing or of the wrong size");
+  const int r = d->cur_ring, nlv = d->cur_nlv;
+  d->cur_iter = -1;
+  DS_TRY(hipSetDevice(d->device), "hipSetDevice");
+  const SwapEnt* d_ent = reinterpret_cast<const SwapEnt*>(d->d_sched[r]);
+  const int* d_off = reinterpret_cast<const int*>(d->d_sched[r] + sizeof(SwapEnt) * (size_t)W);
+  const Gathered X{d->R > 1 ? recv : nullptr, (long long)n, d->R, d->rank, d->m, 0};
   DS_TRY(hipStreamWaitEvent(s, d->ev_copy[r], 0), "schedule wait");
   if (d->lds_swap)
-    ds_swap<true><<<1, kSwapThreads, d->swap_lds, s>>>(D, W, d_ent, d_off, nlv, (long long)iter);
+    ds_swap<true><<<1, kSwapThreads, d->swap_lds, s>>>(D, W, d_ent, d_off, nlv, (long long)iter, X);
   else
-    ds_swap<false><<<1, kSwapThreads, 0, s>>>(D, W, d_ent, d_off, nlv, (long long)iter);
+    ds_swap<false><<<1, kSwapThreads, 0, s>>>(D, W, d_ent, d_off, nlv, (long long)iter, X);
   DS_TRY(hipGetLastError(), "ds_swap");
   DS_TRY(hipEventRecord(d->ev_used[r], s), "schedule ring");
   d->used[r] = true;
-  if (P.log_on && iter > 10000 && iter % 100 == 0) return ds_drain_events(d);
+  if (d->P.log_on && iter > 10000 && iter % 100 == 0) return ds_drain_events(d);
   return 0;
 }
 
-// states / logL by slot after the last step, the MAP tracker and the
-// counters as :577-579 print them; synchronises
+extern "C" long hb_dsampler_step_begin(hb_dsampler* d, long iter, double* send, long cap) {
+  if (!d) return hbx_set_error("hb_dsampler_step_begin: null");
+  if (d->R == 1) return hbx_set_error("hb_dsampler_step_begin: single-rank sampler, use hb_dsampler_step");
+  return ds_begin(d, iter, send, cap);
+}
+
+extern "C" int hb_dsampler_step_end(hb_dsampler* d, long iter, const double* recv, long n) {
+  if (!d) return hbx_set_error("hb_dsampler_step_end: null");
+  return ds_end(d, iter, recv, n);
+}
+
+// one iteration, enqueued on the sampler's stream (no host wait)
+extern "C" int hb_dsampler_step(hb_dsampler* d, long iter) {
+  if (!d) return hbx_set_error("hb_dsampler_step: null");
+  if (d->R > 1) return hbx_set_error("hb_dsampler_step: sharded sampler, use step_begin / all-gather / step_end");
+  const long rc = ds_begin(d, iter, nullptr, 0);
+  if (rc < 0) {
+    d->cur_iter = -1;
+    return (int)rc;
+  }
+  return ds_end(d, iter, nullptr, 0);
+}
+
+// states / logL of the owned slots after the last step, the MAP tracker and
+// the counters as :577-579 print them; synchronises
 extern "C" int hb_dsampler_gather(hb_dsampler* d, double* x_slots, double* logl_slots, double* xmap,
                                   double* logLmap, long* stats4) {
   if (!d) return hbx_set_error("hb_dsampler_gather: null");
-  const int W = d->W;
+  const int nl = d->nl;
   hipStream_t s = d->st;
   DS_TRY(hipSetDevice(d->device), "hipSetDevice");
-  ds_gather<<<(W + kBlk - 1) / kBlk, kBlk, 0, s>>>(W, d->D, d->d_xs, d->d_ls, nullptr, nullptr);
+  ds_gather<<<(nl + kBlk - 1) / kBlk, kBlk, 0, s>>>(d->D, d->d_xs, d->d_ls, nullptr, nullptr);
   DS_TRY(hipGetLastError(), "gather");
   if (x_slots)
-    DS_TRY(hipMemcpyAsync(x_slots, d->d_xs, sizeof(double) * W * kNp, hipMemcpyDeviceToHost, s), "gather");
+    DS_TRY(hipMemcpyAsync(x_slots, d->d_xs, sizeof(double) * nl * kNp, hipMemcpyDeviceToHost, s), "gather");
   if (logl_slots)
-    DS_TRY(hipMemcpyAsync(logl_slots, d->d_ls, sizeof(double) * W, hipMemcpyDeviceToHost, s), "gather");
+    DS_TRY(hipMemcpyAsync(logl_slots, d->d_ls, sizeof(double) * nl, hipMemcpyDeviceToHost, s), "gather");
   DS_TRY(hipMemcpyAsync(d->h_ctr, d->D.ctr, sizeof(Counters), hipMemcpyDeviceToHost, s), "gather");
   DS_TRY(hipStreamSynchronize(s), "gather");
   if (xmap) memcpy(xmap, d->h_ctr->xmap, sizeof(double) * kNp);

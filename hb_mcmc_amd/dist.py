@@ -202,6 +202,87 @@ def run_sharded(t, flux, sigma, niter, run_id, log10_period, run=0, nchains=50, 
             gpu.close()
 
 
+def run_sharded_device(t, flux, sigma, niter, run_id, log10_period, run=0, nchains=50, npast=500, ladder=0,
+                       verbose=False, out_root=None, mag_data=None, magerr=None, group=None, device=None):
+    """run_sharded with the device-resident loop on every rank
+    (ShardedDeviceSampler): proposals, likelihood, Hastings test, history and
+    the tempering swaps stay on each rank's GPU; per iteration ONE RCCL
+    all-gather carries logL by slot plus the records of the chains near each
+    shard's edges.  The host joins every 100 iterations for the reference's
+    files (rank 0), as hb_mcmc_run_device does.  Same files, same MAP point and
+    counters as the single-process sampler."""
+    import torch
+
+    from .dsampler import ShardedDeviceSampler
+    from .likelihood import HBLikelihood
+
+    comm = _Comm(group)
+    R, r = comm.world, comm.rank
+    W = int(nchains)
+    if W < 2 * R:
+        raise ValueError(f"nchains={W} must give every one of the {R} ranks at least two slots")
+    lo, hi = shard(W, r, R)
+    t = np.ascontiguousarray(t, dtype=np.float64)
+    flux = np.ascontiguousarray(flux, dtype=np.float64)
+    sigma = np.ascontiguousarray(sigma, dtype=np.float64)
+    if device is None:
+        device = torch.cuda.current_device()
+    gpu = HBLikelihood(t, flux, sigma, mag_data, magerr, device=device)
+    S = SlotSampler(niter, W, log10_period, lo, hi, run=run, npast=npast, ladder=ladder)
+    writer = None
+    D = None
+    try:
+        if r == 0 and out_root:
+            writer = Writer(out_root, run_id, run, W)
+            writer.attach(S)  # big-jump log lines of rank 0's slots (the reference logs slots 0-5)
+        D = ShardedDeviceSampler(S, gpu, group)
+        D.init_logl()
+        if r == 0 and verbose:
+            _, _, _, lmap, _ = D.gather()
+            print("initial chi2 and likelihood %f \t %f" % (-2 * lmap, lmap))
+        t_start = time.perf_counter()
+        model = (lambda p: gpu.light_curve(p[None, :])[0])
+        for it in range(int(niter)):
+            D.step(it)
+            show = verbose and it % 1000 == 0
+            write = bool(out_root) and it % 100 == 0
+            if not (show or write):
+                continue
+            x_all, l_all, xmap, _, st = D.gather_all()
+            if show:  # :575-589 (counters summed over ranks)
+                acc, de_acc, de_trial = comm.allreduce_sum([st["acc"], st["DEacc"], st["DEtrial"]])
+                if r == 0:
+                    with np.errstate(divide="ignore", invalid="ignore"):
+                        print("%d/%d logL=%.10g acc=%.3g DEacc=%.3g" % (
+                            it, niter, l_all[0], np.float64(acc) / np.float64(st["atrial"]),
+                            np.float64(de_acc) / np.float64(de_trial)))
+                    print("Parameter values: ")
+                    print("".join("%f\t" % v for v in x_all[min(10, W - 1), :5]))
+            if write and r == 0:  # :593-649
+                writer.step(it, l_all, x_all)
+                writer.light_curve(t, flux, np.asarray(model(xmap), dtype=np.float64))
+                writer.pars(False, x_all[0])
+        x_all, _, xmap, logLmap, _ = D.gather_all()
+        D.download()
+        seconds = time.perf_counter() - t_start
+        if r == 0 and out_root:  # :655-681
+            writer.light_curve(t, flux, np.asarray(model(xmap), dtype=np.float64))
+            writer.pars(True, x_all[0])
+        st = S.stats()
+        cold_acc = comm.allreduce_sum([st["cold_acc"]])[0]
+        return {"xmap": xmap if r == 0 else None, "logLmap": logLmap if r == 0 else None,
+                "accepted": int(cold_acc), "swaps": st["nswap"], "seconds_total": seconds,
+                "loglik_evals": W * (int(niter) + 1), "slots": (lo, hi),
+                "exchanged_doubles_per_iter": D.exchanged_doubles / max(1, int(niter))}
+    finally:
+        if D is not None:
+            D.close()
+        if writer is not None:
+            writer.close()
+        S.close()
+        gpu.close()
+
+
 def main(argv=None):
     """Multi-GPU counterpart of the hb_mcmc CLI (./HB_MCMC NITER TIC log10P run):
 
@@ -229,12 +310,14 @@ def main(argv=None):
     ap.add_argument("--ladder", type=int, default=0)
     ap.add_argument("--threads", type=int, default=0)
     ap.add_argument("--backend", choices=("nccl", "gloo"), default=None)
+    ap.add_argument("--device-sampler", action="store_true",
+                    help="device-resident loop on every rank (one all-gather per iteration)")
     ap.add_argument("--quiet", action="store_true")
     a = ap.parse_args(argv)
     local = int(os.environ.get("LOCAL_RANK", "0"))
     backend = a.backend or ("nccl" if torch.cuda.device_count() > 0 else "gloo")
-    if backend == "nccl":
-        torch.cuda.set_device(local)
+    if backend == "nccl" or a.device_sampler:
+        torch.cuda.set_device(local % max(1, torch.cuda.device_count()))
     dist.init_process_group(backend)
     try:
         lc = os.path.join(a.root, "data", "lightcurves", "folded_lightcurves", f"{a.tic}_new.txt")
@@ -244,9 +327,17 @@ def main(argv=None):
             return 0
         t, f, e = read_folded_lc(lc)
         mag, magerr = read_mag_file(os.path.join(a.root, "data", "magnitudes", f"{a.tic}.txt"))
-        res = run_sharded(t, f, e, a.niter, a.tic, a.log10P, run=a.run, nchains=a.chains, npast=a.npast,
-                          ladder=a.ladder, nthreads=a.threads, verbose=not a.quiet, out_root=a.root,
-                          mag_data=mag, magerr=magerr, device=local % max(1, torch.cuda.device_count()))
+        dev = local % max(1, torch.cuda.device_count())
+        if a.device_sampler:
+            res = run_sharded_device(t, f, e, a.niter, a.tic, a.log10P, run=a.run, nchains=a.chains, npast=a.npast,
+                                     ladder=a.ladder, verbose=not a.quiet, out_root=a.root, mag_data=mag,
+                                     magerr=magerr, device=dev)
+            res.setdefault("seconds_loglik", -1.0)
+            res.setdefault("seconds_comm", -1.0)
+        else:
+            res = run_sharded(t, f, e, a.niter, a.tic, a.log10P, run=a.run, nchains=a.chains, npast=a.npast,
+                              ladder=a.ladder, nthreads=a.threads, verbose=not a.quiet, out_root=a.root,
+                              mag_data=mag, magerr=magerr, device=dev)
         if dist.get_rank() == 0 and not a.quiet:
             print("done: %d iterations on %d ranks, %d logL evals, %.3f s total, %.3f s in the likelihood, "
                   "%.3f s in collectives; logLmap %.12g" % (a.niter, dist.get_world_size(), res["loglik_evals"],

@@ -119,6 +119,35 @@ int hb_dsampler_gather(hb_dsampler *d, double *x_slots, double *logl_slots, doub
 int hb_dsampler_sync(hb_dsampler *d);
 /* copies the whole device state back into the host sampler */
 int hb_dsampler_download(hb_dsampler *d);
+/* ---- Sharded device-resident sampler: rank `rank` of `nranks` (one per GPU)
+ * owns the slots [W*rank/nranks, W*(rank+1)/nranks) of the ladder (its host
+ * sampler `s` must own exactly those, hb_sampler_create(cfg, lo, hi)).
+ * chain_of_slot[W] is every slot's chain id (all ranks' hb_sampler_get cid,
+ * all-gathered; the identity for a fresh run).  An iteration is two calls
+ * around ONE all-gather the caller runs (RCCL in hb_mcmc_amd/dsampler.py):
+ *   n = hb_dsampler_step_begin(d, it, send, cap)
+ *       enqueues proposals, likelihood, Hastings test and history of the
+ *       owned slots, then writes the rank's contribution into the device
+ *       buffer send[0 .. n) (logL of the owned slots + the records of the
+ *       chains near the shard's edges; n is the same on every rank);
+ *       returns n (> 0) or a negative error; cap = capacity of send
+ *   all-gather: recv[r*n .. (r+1)*n) = rank r's send[0 .. n), on the
+ *       sampler's stream (hb_dsampler_stream) or ordered after it
+ *   hb_dsampler_step_end(d, it, recv, n)
+ *       imports the other ranks' logL and records, replays the iteration's
+ *       tempering swaps (identical on every rank) and the bookkeeping.
+ * Gather/download/init_logl act on the owned slots; the MAP tracker
+ * (xmap, logLmap) is meaningful on the rank owning slot 0; counters are the
+ * owned slots' (sum acc/DEacc/DEtrial/cold_acc over ranks). */
+hb_dsampler *hb_dsampler_create_shard(hb_sampler *s, struct hb_ctx *ctx, const int *chain_of_slot, int nranks,
+                                      int rank);
+long hb_dsampler_step_begin(hb_dsampler *d, long iter, double *send, long cap);
+int hb_dsampler_step_end(hb_dsampler *d, long iter, const double *recv, long n);
+/* largest n step_begin can return for this sampler (the capacity to allocate) */
+long hb_dsampler_exchange_cap(const hb_dsampler *d);
+/* the hipStream_t every kernel of the sampler runs on */
+void *hb_dsampler_stream(hb_dsampler *d);
+
 /* hb_mcmc_run with the device-resident loop; the light curve and magnitude
  * data come from ctx (t, flux: host copies for the .out file) */
 int hb_mcmc_run_device(const hb_mcmc_cfg *cfg, struct hb_ctx *ctx, const double *t, const double *flux, long n,

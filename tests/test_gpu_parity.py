@@ -273,3 +273,62 @@ def test_full_size_c2_against_oracle_and_properties(hbmi, oracle):
     roche = (a == -5e14)
     assert 0.02 < roche.mean() < 0.2
     assert np.isfinite(a[~roche]).all()
+
+
+# ------------------------------------------------- full-size (config C4)
+def test_full_size_c4_against_oracle_and_properties(hbmi, oracle):
+    """W = 65 536, N = 1024 (BASELINE config C4's whole ensemble on one GPU):
+    oracle on a 512-walker sample; on all walkers determinism, permutation
+    equivariance, the Roche fraction, and shard independence -- the eight
+    8192-walker shards a C4 rank evaluates give the full batch's values bit
+    for bit (what the sharded sampler relies on)."""
+    from hb_mcmc_amd import synth
+    from hb_mcmc_amd.dist import shard
+    from hb_mcmc_amd.likelihood import HBLikelihood
+
+    W = 65536
+    t, f, s = synth.dataset(1024, oracle.light_curve)
+    P = synth.walkers(W, seed=44)
+    with HBLikelihood(t, f, s) as L:
+        L.reserve(W)
+        a = L.loglike(P)
+        b = L.loglike(P)
+        perm = np.random.default_rng(3).permutation(W)
+        c = L.loglike(P[perm])
+        parts = [L.loglike(P[lo:hi]) for lo, hi in (shard(W, r, 8) for r in range(8))]
+    assert np.array_equal(a, b, equal_nan=True)
+    assert np.array_equal(a[perm], c, equal_nan=True)
+    assert np.array_equal(np.concatenate(parts), a, equal_nan=True)
+    idx = np.arange(0, W, 128)
+    ref = oracle.loglike_batch(t, f, s, P[idx], synth.MAG_DEFAULT, synth.MAGERR_DEFAULT, 16)
+    close_logl(a[idx], ref)
+    roche = (a == -5e14)
+    assert 0.02 < roche.mean() < 0.2
+    bad = np.nonzero(~np.isfinite(a))[0]
+    assert len(bad) <= W // 1000
+    if len(bad):  # every non-finite value is the reference's own (eclipse_area's asin domain)
+        close_logl(a[bad], oracle.loglike_batch(t, f, s, P[bad], synth.MAG_DEFAULT, synth.MAGERR_DEFAULT, 16))
+
+
+# ------------------------------------------------- full-size (config C3)
+def test_full_size_c3_against_oracle(hbmi, oracle):
+    """W = 4096, N = 20 000 (config C3, the block kernel): oracle on a
+    128-walker sample plus every walker whose logL is not finite (the bench
+    batch met one: the reference's own eclipse_area NaN), determinism."""
+    from hb_mcmc_amd import synth
+    from hb_mcmc_amd.likelihood import HBLikelihood
+
+    W, n = 4096, 20000
+    t, f, s = synth.dataset(n, oracle.light_curve)
+    P = synth.walkers(W, seed=1000)  # bench.py's first C3 batch (rank 0)
+    with HBLikelihood(t, f, s) as L:
+        assert L.eval_kernel == "hb_eval_block_kernel"
+        a = L.loglike(P)
+        b = L.loglike(P)
+    assert np.array_equal(a, b, equal_nan=True)
+    idx = np.arange(0, W, 32)
+    bad = np.nonzero(~np.isfinite(a))[0]
+    sel = np.union1d(idx, bad)
+    ref = oracle.loglike_batch(t, f, s, P[sel], synth.MAG_DEFAULT, synth.MAGERR_DEFAULT, 16)
+    close_logl(a[sel], ref)
+    assert len(bad) <= 4
