@@ -254,6 +254,41 @@ def sampler_e2e(L, w, iters, warm=20):
     return out
 
 
+def sampler_e2e_sharded(L, w, iters, rank, world, warm=20):
+    """Whole PT-MCMC iterations on `world` ranks (ShardedDeviceSampler): each
+    rank owns w slots of a w x world ladder (weak scaling, 50-rung ladder
+    repeated) and runs proposals, likelihood, Hastings test and swaps on its
+    GPU with one all-gather per iteration.  Max-over-ranks wall time."""
+    from hb_mcmc_amd.dist import shard
+    from hb_mcmc_amd.dsampler import ShardedDeviceSampler
+    from hb_mcmc_amd.sampler import SlotSampler
+
+    W = w * world
+    lo, hi = shard(W, rank, world)
+    S = SlotSampler(warm + iters, W, float(synth.THETA_STAR[2]), lo, hi, run=0, npast=500, ladder=1)
+    with ShardedDeviceSampler(S, L) as D:
+        D.init_logl()
+        for it in range(warm):
+            D.step(it)
+        D.sync()
+        dist.barrier()
+        t0 = time.perf_counter()
+        for it in range(warm, warm + iters):
+            D.step(it)
+        D.sync()
+        dist.barrier()
+        dt = time.perf_counter() - t0
+        exch = D.exchanged_doubles
+    S.close()
+    tt = torch.tensor([dt], dtype=torch.float64, device=torch.device("cuda", L.device))
+    dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+    dt = float(tt.item())
+    return {"walkers": W, "walkers_per_rank": w, "ranks": world, "iters_timed": iters,
+            "unit": "walker-steps/s (1 likelihood eval each), all ranks",
+            "device_loop_sharded": {"ms_per_iter": dt / iters * 1e3, "value": W * iters / dt,
+                                    "exchange_bytes_per_rank_per_iter": 8.0 * exch / (warm + iters)}}
+
+
 def make_event(kind):
     return _HipEvent() if kind == "hip" else torch.cuda.Event(enable_timing=True)
 
@@ -445,6 +480,10 @@ def main():
     nonfinite = int((~np.isfinite(lv)).sum())
     assert nonfinite <= max(1, w // 100), f"{nonfinite} non-finite logL of {w}"
 
+    e2e = None
+    if world > 1 and a.sampler_iters > 0:  # every rank takes part
+        e2e = sampler_e2e_sharded(L, w, a.sampler_iters, rank, world)
+
     if rank == 0:
         evals = world * w * a.steps
         value = evals / wall
@@ -495,6 +534,8 @@ def main():
         }
         if world == 1 and a.sampler_iters > 0:
             line["sampler_end_to_end"] = sampler_e2e(L, w, a.sampler_iters)
+        if world > 1 and e2e is not None:
+            line["sampler_end_to_end"] = e2e
         if world == 1 and not a.no_cpu_baseline:
             line["cpu_baseline"] = run_cpu_baseline(n, a.cpu_seconds)
         print(json.dumps(line), flush=True)
