@@ -509,9 +509,6 @@ __device__ __noinline__ double hb_cadence_flux_slow(double t, const WalkerConst*
 #ifndef HB_SPLIT_LIVE
 #define HB_SPLIT_LIVE 1
 #endif
-#ifndef HB_RCP_REUSE
-#define HB_RCP_REUSE 0
-#endif
 constexpr double kRotMaxK = 0.25;
 __device__ __forceinline__ void rotate_back_wide(double d, double z, double& s, double& c) {
   // sin d = d (1 + z S(z)), cos d = 1 + z C(z), z = d^2
@@ -544,13 +541,13 @@ __device__ __forceinline__ void rotate_back_tiny(double d, double z, double& s, 
   c = c2;
 }
 
+// Mean anomaly of K cadences: q = trunc(x / 2pi), r = x - q 2pi (exact when
+// q is the true quotient, see above); `exact` flags lanes that need
+// fmod_twopi_fast, `ok` lanes inside the fast sincos/fmod domain, plus[k] =
+// sign(sin m) > 0 (sign_sin_reduced for m in (-2pi, 2pi) \ {0}).
 template <int K>
-__device__ __forceinline__ void hb_cadence_flux_k(const double (&t)[K], const double2 (&ph)[K], bool tab,
-                                                  const WalkerConst& w, double (&v)[K], bool& bad) {
-  const double e = w.e;
-  const double aR2 = w.aR * w.aR, rsum2 = w.rsum * w.rsum;
-  double m[K], E[K], s[K], c[K];
-  bool ok = true, exact = false, plus[K];
+__device__ __forceinline__ void mean_anomaly_k(const double (&t)[K], const WalkerConst& w, double (&m)[K],
+                                               bool (&plus)[K], bool& ok, bool& exact) {
 #pragma unroll
   for (int k = 0; k < K; ++k) {
     const double x = fma(t[k], kDay, w.mB) * w.mA;
@@ -562,10 +559,20 @@ __device__ __forceinline__ void hb_cadence_flux_k(const double (&t)[K], const do
     const bool inside = same_sign & (fabs(r) < kTwoPi) & (r != 0.0);
     exact |= !inside;
     m[k] = r;
-    // sign(sin m) * 0.85 e for m in (-2pi, 2pi) \ {0} (sign_sin_reduced)
     plus[k] = (fabs(r) <= kPi) != (r < 0.0);
-    E[k] = r + (plus[k] ? w.e085 : -w.e085);
   }
+}
+
+// The reference's Kepler start E0 = M + 0.85 e sign(sin M) (likelihood3.c:
+// 155-157) and (sin, cos)(E0): rotations of the shared-period table entry
+// (tab), else the branch-free sincos.  Lanes flagged `exact` recompute M by
+// fmod_twopi_fast first (wave-uniform branch).
+template <int K>
+__device__ __forceinline__ void cold_start_k(const double (&t)[K], const double2 (&ph)[K], bool tab, bool exact,
+                                             const WalkerConst& w, double (&m)[K], const bool (&plus)[K],
+                                             double (&E)[K], double (&s)[K], double (&c)[K], bool& ok) {
+#pragma unroll
+  for (int k = 0; k < K; ++k) E[k] = m[k] + (plus[k] ? w.e085 : -w.e085);
   if (tab) {  // walker-uniform: E0 = M + sg del by rotations of the table entry
 #pragma unroll
     for (int k = 0; k < K; ++k) {
@@ -593,11 +600,23 @@ __device__ __forceinline__ void hb_cadence_flux_k(const double (&t)[K], const do
       sincos_fast(E[k], &s[k], &c[k]);
     }
   }
-  double yk[K];           // last Newton step's 1/(1 - e cos E), refined once
-  bool converged = false;
-  (void)converged;
+}
+
+// Newton on E - e sin E = M (likelihood3.c:152-160), at most 5 steps; the
+// wave leaves once every lane's predicted next correction is <= 2^-52.
+// yk: the last step's 1/(1 - e cos E).  Returns whether it converged.
+#ifdef HB_CHAIN_STATS  // experiment builds only: warm-start bookkeeping counters
+__device__ unsigned long long hb_chain_stats[8];
+#define HB_STAT(i) do { if ((threadIdx.x & 63) == 0) atomicAdd(&hb_chain_stats[i], 1ull); } while (0)
+#else
+#define HB_STAT(i) do { } while (0)
+#endif
+template <int K>
+__device__ __forceinline__ bool newton_k(double e, const double (&m)[K], double (&E)[K], double (&s)[K],
+                                         double (&c)[K], double (&yk)[K], bool& ok) {
 #pragma unroll
   for (int it = 0; it < 5; ++it) {
+    HB_STAT(5);
     bool small = true, mid = true, tiny = true, conv = true;
     double d[K], z[K];
 #pragma unroll
@@ -626,48 +645,36 @@ __device__ __forceinline__ void hb_cadence_flux_k(const double (&t)[K], const do
 #pragma unroll
       for (int k = 0; k < K; ++k) rotate_back_wide(d[k], z[k], s[k], c[k]);
     } else {
+      HB_STAT(7);
 #pragma unroll
       for (int k = 0; k < K; ++k) {
         ok &= sincos_fast_ok(E[k]);
         sincos_fast(E[k], &s[k], &c[k]);
       }
     }
-    if (__all(conv)) {
-      converged = true;
-      break;
-    }
+    if (__all(conv)) return true;
   }
-  bool need_ecl = false;
-#if HB_SPLIT_LIVE
-  // compiler barrier: the photometric constants below are (re)loaded here
-  // with scalar loads instead of being held in SGPRs across the Kepler
-  // solve, which would spill the solve's polynomial constants
-  __asm__ volatile("" ::: "memory");
-#endif
-  double dd[K], zz[K];
+  return false;
+}
+
+// The photometric polynomial of K cadences from (sin, cos) of the solved
+// eccentric anomaly, without the eclipse; dd = (projected separation / a)^2
+// and zz (sign carrier of Z1 - Z2) for the eclipse test.
+template <int K>
+__device__ __forceinline__ void flux_poly_k(const double (&s)[K], const double (&c)[K], const WalkerConst& w,
+                                            double (&v)[K], double (&dd)[K], double (&zz)[K]) {
+  const double e = w.e;
 #pragma unroll
   for (int k = 0; k < K; ++k) {
     const double den = fma(-e, c[k], 1.0);
-#if HB_RCP_REUSE
-    // converged: E moved by < 2^-26 since yk was formed, so two refinements
-    // of yk give the reciprocal to working precision without a new v_rcp
-    double inv;
-    if (converged) {
-      inv = fma(fma(-den, yk[k], 1.0), yk[k], yk[k]);
-      inv = fma(fma(-den, inv, 1.0), inv, inv);
-    } else {
-      inv = fast_rcp(den);
-    }
-#else
     const double inv = fast_rcp(den);
-#endif
     const double cnu = (c[k] - e) * inv;
     const double snu = (w.sq1me2 * s[k]) * inv;
     const double cu = fma(w.cw, cnu, -w.sw * snu);
     const double su = fma(w.sw, cnu, w.cw * snu);
     const double b = fma(e, cnu, 1.0) * w.inv1me2;
     const double sci = su * w.ci;
-    dd[k] = (den * den) * fma(cu, cu, sci * sci);  // (projected separation / a)^2; sqrt only on eclipse lanes
+    dd[k] = (den * den) * fma(cu, cu, sci * sci);  // sqrt only on eclipse lanes
     zz[k] = su * w.si;
     const double c2 = (cu - su) * (cu + su);          // cos 2u
     const double su2 = su * su;
@@ -685,17 +692,205 @@ __device__ __forceinline__ void hb_cadence_flux_k(const double (&t)[K], const do
     // values stay ~1 like the reference's Amag1 + Amag2 (one sign, one
     // exponent: the median radix-select resolves them in one digit pass)
     v[k] = fma(b2, h, fma(w.kb, cu, w.kconst));
-    // squared test: a lane within an ulp of tangency may go either way, where
-    // the overlap area (~eps^1.5) is zero to working precision
-    need_ecl |= (dd[k] * aR2 < rsum2) & (zz[k] != 0.0);
   }
-  bad = !ok;
+}
+
+// squared test: a lane within an ulp of tangency may go either way, where
+// the overlap area (~eps^1.5) is zero to working precision
+__device__ __forceinline__ bool eclipse_lane(const WalkerConst& w, double dd, double zz) {
+  return (dd * (w.aR * w.aR) < w.rsum * w.rsum) & (zz != 0.0);
+}
+
+template <int K>
+__device__ __forceinline__ void flux_from_sc_k(const double (&s)[K], const double (&c)[K], const WalkerConst& w,
+                                               double (&v)[K]) {
+  double dd[K], zz[K];
+  flux_poly_k<K>(s, c, w, v, dd, zz);
+  bool need_ecl = false;
+#pragma unroll
+  for (int k = 0; k < K; ++k) need_ecl |= eclipse_lane(w, dd[k], zz[k]);
   if (__any(need_ecl)) {
 #pragma unroll
     for (int k = 0; k < K; ++k) {
-      if ((dd[k] * aR2 < rsum2) & (zz[k] != 0.0)) v[k] -= eclipse_term(&w, sqrt(dd[k]) * w.aR, zz[k]);
+      if (eclipse_lane(w, dd[k], zz[k])) v[k] -= eclipse_term(&w, sqrt(dd[k]) * w.aR, zz[k]);
     }
   }
+}
+
+template <int K>
+__device__ __forceinline__ void hb_cadence_flux_k(const double (&t)[K], const double2 (&ph)[K], bool tab,
+                                                  const WalkerConst& w, double (&v)[K], bool& bad) {
+  double m[K], E[K], s[K], c[K], yk[K];
+  bool ok = true, exact = false, plus[K];
+  mean_anomaly_k<K>(t, w, m, plus, ok, exact);
+  cold_start_k<K>(t, ph, tab, exact, w, m, plus, E, s, c, ok);
+  (void)newton_k<K>(w.e, m, E, s, c, yk, ok);
+#if HB_SPLIT_LIVE
+  // compiler barrier: the photometric constants below are (re)loaded here
+  // with scalar loads instead of being held in SGPRs across the Kepler
+  // solve, which would spill the solve's polynomial constants
+  __asm__ volatile("" ::: "memory");
+#endif
+  flux_from_sc_k<K>(s, c, w, v);
+  bad = !ok;
+}
+
+// ------------------------------------------------------------------------
+// Warm-started Kepler solve along a lane's consecutive cadences (the wave
+// kernel, where lane l owns cadences l*VPT .. l*VPT + VPT - 1 as K chains).
+// Consecutive cadences of a light curve are close in phase, so the solved
+// anomaly of the previous cadence of the chain, advanced by the first-order
+// step dE = dM / (1 - e cos E), starts Newton within ~(dM)^2 of the root:
+// two steps (the second at the tiny rotation) instead of the reference
+// start's three or four.  The root is the one the reference's five steps
+// reach whenever those converge -- which holds for every M when e <= 0.85
+// (scripts/kepler_warm.py) -- so the warm start is taken only for e <= 0.8,
+// only when every lane's start step |dE| <= 0.25 and no lane needs the exact
+// fmod, and a warm solve that does not converge in five steps is redone from
+// the reference's start (wave-uniform decisions throughout).
+// ------------------------------------------------------------------------
+constexpr double kWarmEmax = 0.8;
+// The chain carries the previous cadence's solved E and (sin, cos)(E); its
+// mean anomaly is E - e sin E (Kepler's equation, to rounding) and its
+// 1 / (1 - e cos E) a bare v_rcp_f64 -- the start only needs dE to ~1e-8.
+template <int K>
+struct ChainState {
+  double E[K], s[K], c[K];
+};
+
+// v: the polynomial part only; the caller applies the eclipse where
+// eclipse_lane(w, dd, zz) (compacted across the wave, see model_pass_chain)
+template <int K>
+__device__ __forceinline__ void hb_cadence_flux_chain(const double (&t)[K], const double2 (&ph)[K], bool tab,
+                                                      bool first, const WalkerConst& w, ChainState<K>& st,
+                                                      double (&v)[K], double (&dd)[K], double (&zz)[K],
+                                                      bool& bad) {
+  const double e = w.e;
+  double m[K], E[K], s[K], c[K], yk[K];
+  bool ok = true, exact = false, plus[K];
+  mean_anomaly_k<K>(t, w, m, plus, ok, exact);
+#ifndef HB_WARM
+#define HB_WARM 1
+#endif
+  bool warm = HB_WARM && !first && (e <= kWarmEmax) && !__any(exact);
+  HB_STAT(0);
+#ifndef HB_WARM_FAST
+#define HB_WARM_FAST 1
+#endif
+  if (HB_WARM_FAST && warm) {
+    // the common warm step as one basic block (the K chains' solves and
+    // polynomials interleave): start rotation of degree 9 (|dE| <= 1/16),
+    // Newton step 1 with the mid rotation (|d| <= 2^-9), step 2 with the tiny
+    // one (|d| <= 2^-22) and the convergence test; any lane outside those
+    // bounds sends the whole wave through the general path below, which
+    // recomputes from the chain state
+    bool fine = true;
+    double Ef[K], sf[K], cf[K], yf[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const double D = m[k] - fma(-e, st.s[k], st.E[k]);
+      const double q = rint(D * 0.15915494309189533577);
+      const double Dc = fma(-q, kTwoPi, D);
+      const double dl = Dc * __builtin_amdgcn_rcp(fma(-e, st.c[k], 1.0));
+      double E0 = fma(q, kTwoPi, st.E[k]) + dl;
+      double s0 = st.s[k], c0 = st.c[k];
+      const double z0 = dl * dl;
+      fine &= fabs(dl) <= 0.0625;
+      {  // rotate forward by dl: sin dl = dl (1 + z S(z)), cos dl = 1 + z C(z)
+        const double sd = fma(dl * z0, fma(z0, fma(z0, fma(z0, 1.0 / 362880.0, -1.0 / 5040.0), 1.0 / 120.0),
+                                           -1.0 / 6.0), dl);
+        const double cd = fma(z0, fma(z0, fma(z0, fma(z0, 1.0 / 40320.0, -1.0 / 720.0), 1.0 / 24.0), -0.5), 1.0);
+        const double s1 = fma(s0, cd, c0 * sd);
+        const double c1 = fma(c0, cd, -(s0 * sd));
+        s0 = s1;
+        c0 = c1;
+      }
+      // Newton step 1
+      double den = fma(-e, c0, 1.0);
+      double y = __builtin_amdgcn_rcp(den);
+      y = fma(fma(-den, y, 1.0), y, y);
+      double d = ((E0 - e * s0) - m[k]) * y;
+      E0 = E0 - d;
+      fine &= fabs(d) <= 0x1p-9;
+      rotate_back_mid(d, d * d, s0, c0);
+      // Newton step 2
+      den = fma(-e, c0, 1.0);
+      y = __builtin_amdgcn_rcp(den);
+      y = fma(fma(-den, y, 1.0), y, y);
+      d = ((E0 - e * s0) - m[k]) * y;
+      E0 = E0 - d;
+      const double z = d * d;
+      fine &= (fabs(d) <= 0x1p-22) & (e * z <= 0x1p-51 * den);
+      rotate_back_tiny(d, z, s0, c0);
+      Ef[k] = E0;
+      sf[k] = s0;
+      cf[k] = c0;
+      yf[k] = y;
+    }
+    if (__all(fine)) {
+      HB_STAT(2);
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        st.E[k] = Ef[k];
+        st.s[k] = sf[k];
+        st.c[k] = cf[k];
+      }
+#if HB_SPLIT_LIVE
+      __asm__ volatile("" ::: "memory");
+#endif
+      flux_poly_k<K>(sf, cf, w, v, dd, zz);
+      bad = !ok;
+      return;
+    }
+  }
+  if (warm) {
+    HB_STAT(1);
+    bool small = true, mid = true;
+    double dl[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      // dM wrapped into [-pi, pi]; E follows M's 2pi multiple
+      const double D = m[k] - fma(-e, st.s[k], st.E[k]);
+      const double q = rint(D * 0.15915494309189533577);
+      const double Dc = fma(-q, kTwoPi, D);
+      dl[k] = Dc * __builtin_amdgcn_rcp(fma(-e, st.c[k], 1.0));
+      E[k] = fma(q, kTwoPi, st.E[k]) + dl[k];
+      s[k] = st.s[k];
+      c[k] = st.c[k];
+      const double ad = fabs(dl[k]);
+      small &= ad <= kRotMaxK;
+      mid &= ad <= 0x1p-9;
+    }
+    warm = __all(small);
+    if (warm) {  // (sin, cos) rotated forward by dl
+      HB_STAT(2);
+      if (__all(mid)) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) rotate_back_mid(-dl[k], dl[k] * dl[k], s[k], c[k]);
+      } else {
+#pragma unroll
+        for (int k = 0; k < K; ++k) rotate_back_wide(-dl[k], dl[k] * dl[k], s[k], c[k]);
+      }
+      if (!newton_k<K>(e, m, E, s, c, yk, ok)) warm = false;  // redo from the reference's start
+      if (warm) HB_STAT(3);
+    }
+  }
+  if (!warm) {
+    HB_STAT(4);
+    cold_start_k<K>(t, ph, tab, exact, w, m, plus, E, s, c, ok);
+    (void)newton_k<K>(e, m, E, s, c, yk, ok);
+  }
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    st.E[k] = E[k];
+    st.s[k] = s[k];
+    st.c[k] = c[k];
+  }
+#if HB_SPLIT_LIVE
+  __asm__ volatile("" ::: "memory");
+#endif
+  flux_poly_k<K>(s, c, w, v, dd, zz);
+  bad = !ok;
 }
 
 }  // namespace hbdev

@@ -96,6 +96,7 @@ hipError_t launch_eval_multi(int vpt, size_t slab_bytes, const double* t, const 
                              const hbdev::WalkerConst* wc, double* logl, hipStream_t s);
 int wave_vpt_for(long n);  // cadences per lane of the one-wave path, 0 if n > 2048
 size_t wave_slab_bytes(long n);
+size_t wave_lds_bytes(size_t slab);
 // acc (device sampler, one-wave path only): each wave also runs its slot's
 // Hastings test and history write (hb_accept.hpp); hipErrorNotSupported on the
 // multi-wave path

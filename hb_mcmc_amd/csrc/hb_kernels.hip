@@ -496,6 +496,101 @@ __device__ __forceinline__ void model_pass(const double* __restrict__ t, const d
   kmx_out = kmx;
 }
 
+// One-wave kernel: lane l owns the consecutive cadences l*VPT ..
+// l*VPT + VPT - 1, solved as KC chains of LC = VPT/KC cadences whose Kepler
+// starts are warm (hb_cadence_flux_chain) after each chain's first cadence.
+// Values go to the lane's row of the LDS slab, VPT doubles, position c stored
+// at c ^ (lane mod VPT) (a wave's accesses at one position then spread over
+// all banks, and the slab stays n * 8 bytes: 16 waves per CU fit the LDS);
+// the row is the lane's select keys afterwards.
+#ifndef HB_LANE_CHAIN
+#define HB_LANE_CHAIN 1
+#endif
+#ifndef HB_KC
+#define HB_KC 2  // chains per lane
+#endif
+template <int VPT>
+__device__ __forceinline__ int slab_pos(int lane, int c) {
+  return lane * VPT + (c ^ (lane & (VPT - 1)));
+}
+
+// Eclipse terms are rare and spread over the orbit, so a wave whose lanes
+// hold cadences all around it would run the out-of-line overlap area for a
+// few lanes at almost every step.  Instead the eclipsing cadences are queued
+// in LDS (slab position, separation, which star is in front) and applied 64
+// at a time, every lane busy; the value written is the same v - term.
+constexpr int kEclQ = 128;  // <= 63 carried + 64 appended (flushed after every chain's append)
+__device__ __forceinline__ void ecl_apply(const WalkerConst& w, double* vals, const double* eq_dr,
+                                          const int* eq_code, int first, int cnt, int lane) {
+  if (lane < cnt) {
+    const int code = eq_code[first + lane];
+    vals[code >> 1] -= eclipse_term(&w, eq_dr[first + lane], (code & 1) ? -1.0 : 1.0);  // out of line
+  }
+}
+
+template <int VPT>
+__device__ __forceinline__ void model_pass_chain(const double* __restrict__ t, const double2* __restrict__ ph,
+                                                 int n, const WalkerConst& w, double* vals, double* eq_dr,
+                                                 int* eq_code, int lane) {
+  constexpr int KC = VPT < HB_KC ? VPT : HB_KC;
+  constexpr int LC = VPT / KC;
+  const bool tab = (ph != nullptr) && (w.tab != 0.0);  // walker-uniform
+  const int last = n - 1;
+  const int base = lane * VPT;
+  const uint64_t lt_mask = (1ull << lane) - 1ull;
+  int qn = 0;  // queued eclipse cadences (wave-uniform)
+  ChainState<KC> st;
+  double tk[KC];
+#pragma unroll
+  for (int k = 0; k < KC; ++k) tk[k] = t[min(base + k * LC, last)];
+  for (int j = 0; j < LC; ++j) {
+    double tn[KC];
+#pragma unroll
+    for (int k = 0; k < KC; ++k) tn[k] = t[min(base + k * LC + j + 1, last)];
+    double v[KC], dd[KC], zz[KC];
+    bool bad;
+#if HB_SPLIT_LIVE
+    __asm__ volatile("" ::: "memory");
+#endif
+    if (j == 0) {  // the chains' first cadences: the reference's start (table entries)
+      double2 p0[KC];
+#pragma unroll
+      for (int k = 0; k < KC; ++k) p0[k] = tab ? ph[min(base + k * LC, last)] : make_double2(0.0, 1.0);
+      hb_cadence_flux_chain<KC>(tk, p0, tab, true, w, st, v, dd, zz, bad);
+    } else {  // warm; a cadence that falls back to the reference start evaluates sin/cos directly
+      const double2 p0[KC] = {};
+      hb_cadence_flux_chain<KC>(tk, p0, false, false, w, st, v, dd, zz, bad);
+    }
+    if (__any(bad)) {  // out-of-domain angles: reference-order ocml path (eclipse included)
+      if (bad) {
+#pragma unroll
+        for (int k = 0; k < KC; ++k) v[k] = hb_cadence_flux_slow(tk[k], &w);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < KC; ++k) {
+      const bool act = base + k * LC + j < n;
+      const int sp = slab_pos<VPT>(lane, k * LC + j);
+      if (act) vals[sp] = v[k];
+      const bool need = act && !bad && eclipse_lane(w, dd[k], zz[k]);
+      const uint64_t bal = __ballot(need);
+      if (need) {
+        const int pos = qn + __popcll(bal & lt_mask);
+        eq_dr[pos] = sqrt(dd[k]) * w.aR;
+        eq_code[pos] = 2 * sp + (zz[k] < 0.0 ? 1 : 0);
+      }
+      qn += __popcll(bal);
+      tk[k] = tn[k];
+      const bool last = (j == LC - 1) && (k == KC - 1);
+      while (qn >= 64 || (last && qn > 0)) {  // wave-uniform
+        const int cnt = qn < 64 ? qn : 64;
+        ecl_apply(w, vals, eq_dr, eq_code, qn - cnt, cnt, lane);
+        qn -= cnt;
+      }
+    }
+  }
+}
+
 // k-th smallest (0-based) of vals[0..n) by radix select; every thread of the
 // block gets the same answer.  kmin/kmax: block-wide min/max keys.
 template <int NW>
@@ -984,10 +1079,21 @@ __device__ __forceinline__ double wave_select2(const uint64_t (&key)[VPT], uint3
 // ds_read_b64 of the slab at <= 2-way bank conflicts.
 template <int VPT>
 __device__ __forceinline__ int key_index(int v, int lane) {
-#if HB_KEY_PERM
+#if HB_LANE_CHAIN
+  return lane * VPT + v;  // the lane's own cadences, in slab-row order
+#elif HB_KEY_PERM
   return lane * VPT + ((v + lane) & (VPT - 1));
 #else
   return v * 64 + lane;
+#endif
+}
+// where key v of `lane` sits in the LDS slab
+template <int VPT>
+__device__ __forceinline__ int slab_key_index(int v, int lane) {
+#if HB_LANE_CHAIN
+  return slab_pos<VPT>(lane, v);
+#else
+  return key_index<VPT>(v, lane);
 #endif
 }
 
@@ -1027,7 +1133,45 @@ __global__ __launch_bounds__(64) HB_WPE_ATTR void hb_eval_wave_kernel(
   }
 
   uint64_t kmn, kmx;
+  uint64_t key[VPT];
+#if HB_LANE_CHAIN
+  {
+    double* eq_dr = reinterpret_cast<double*>(smem + slab_bytes + 8 * kCandMax);
+    int* eq_code = reinterpret_cast<int*>(eq_dr + kEclQ);
+    model_pass_chain<VPT>(t, ph, (int)n, w, vals, eq_dr, eq_code, lane);
+  }
+  __syncthreads();
+  // keys, and the lane's min/max keys (values ~1; -0.0 / +0.0 take the outer
+  // key, NaN lanes fall back to integer key min/max)
+  {
+    double vmn = __builtin_inf(), vmx = -__builtin_inf();
+    bool nan = false;
+#pragma unroll
+    for (int v = 0; v < VPT; ++v) {
+      const bool act = key_index<VPT>(v, lane) < n;
+      const double x = act ? vals[slab_key_index<VPT>(v, lane)] : vmn;
+      key[v] = act ? dkey(x) : ~0ull;  // padding sorts last, never selected
+      vmn = fmin(vmn, x);
+      vmx = fmax(vmx, x);
+      nan |= x != x;
+    }
+    kmn = dkey(vmn == 0.0 ? -0.0 : vmn);
+    kmx = dkey(vmx == 0.0 ? 0.0 : vmx);
+    if (__any(nan)) {
+      kmn = ~0ull;
+      kmx = 0ull;
+#pragma unroll
+      for (int v = 0; v < VPT; ++v) {
+        if (key_index<VPT>(v, lane) < n) {
+          kmn = key[v] < kmn ? key[v] : kmn;
+          kmx = key[v] > kmx ? key[v] : kmx;
+        }
+      }
+    }
+  }
+#else
   model_pass<64>(t, ph, (int)n, w, vals, lane, kmn, kmx);
+#endif
 #if HB_SEL_V == 1
   kmn = wave_min_u64(kmn);
   kmx = wave_max_u64(kmx);
@@ -1035,13 +1179,14 @@ __global__ __launch_bounds__(64) HB_WPE_ATTR void hb_eval_wave_kernel(
   kmn = wave_reduce_u64(kmn, OpMinU64());
   kmx = wave_reduce_u64(kmx, OpMaxU64());
 #endif
+#if !HB_LANE_CHAIN
   __syncthreads();
-  uint64_t key[VPT];
 #pragma unroll
   for (int v = 0; v < VPT; ++v) {
     const int i = key_index<VPT>(v, lane);
-    key[v] = i < n ? dkey(vals[i]) : ~0ull;  // padding sorts last, never selected
+    key[v] = i < n ? dkey(vals[slab_key_index<VPT>(v, lane)]) : ~0ull;  // padding sorts last, never selected
   }
+#endif
   // chi^2 operands requested now so that their L2 latency overlaps the
   // median select (VPT <= 16: 4*VPT more VGPRs while the keys are live)
   constexpr int PF = (HB_PF && VPT <= 16) ? VPT : 1;
@@ -1479,7 +1624,7 @@ static hipError_t launch_multi_t(size_t slab, const double* t, const double2* ph
                                  const double* sg,
                                  const TargetDesc* tab, const int* wt, const int* list, int count,
                                  const WalkerConst* wc, double* logl, hipStream_t s) {
-  const size_t lds = slab + 8 * kCandMax;
+  const size_t lds = wave_lds_bytes(slab);
   hipLaunchKernelGGL((hb_eval_wave_kernel<VPT, true>), dim3(count), dim3(64), lds, s, t, ph, f, sg, 0L, 0L,
                      wc, logl, nullptr, 0, (int)slab, tab, wt, list, hbds::AccArgs{});
   return hipGetLastError();
@@ -1587,10 +1732,17 @@ int wave_vpt_for(long n) {
   return vpt;
 }
 
-// the template slab doubles as the 2^kSelBits-bin histogram of the select
+// the template slab (64 lane rows of VPT doubles) doubles as the
+// 2^kSelBits-bin histogram of the select
 size_t wave_slab_bytes(long n) {
-  const size_t slab = (size_t)n * 8 > (size_t)(4u << kSelBits) ? (size_t)n * 8 : (size_t)(4u << kSelBits);
+  const size_t vals = HB_LANE_CHAIN ? (size_t)64 * wave_vpt_for(n) * 8 : (size_t)n * 8;
+  const size_t slab = vals > (size_t)(4u << kSelBits) ? vals : (size_t)(4u << kSelBits);
   return (slab + 15) & ~(size_t)15;
+}
+
+// slab | select candidates | eclipse queue (lane-chain model pass)
+size_t wave_lds_bytes(size_t slab) {
+  return slab + 8 * kCandMax + (HB_LANE_CHAIN ? (size_t)kEclQ * (8 + 4) : 0);
 }
 
 EvalPlan make_plan(long n) {
@@ -1602,7 +1754,7 @@ EvalPlan make_plan(long n) {
     pl.nw = 1;
     pl.lds = true;
     pl.slab_bytes = wave_slab_bytes(n);
-    pl.lds_bytes = pl.slab_bytes + 8 * kCandMax;
+    pl.lds_bytes = wave_lds_bytes(pl.slab_bytes);
     return pl;
   }
   const size_t lds_cap = 163840;
@@ -1629,3 +1781,14 @@ EvalPlan make_plan(long n) {
 }
 
 }  // namespace hbk
+
+#ifdef HB_CHAIN_STATS
+extern "C" int hb_dbg_chain_stats(unsigned long long* out, int reset) {
+  hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(hbdev::hb_chain_stats), 8 * sizeof(unsigned long long));
+  if (e == hipSuccess && reset) {
+    unsigned long long z[8] = {0};
+    e = hipMemcpyToSymbol(HIP_SYMBOL(hbdev::hb_chain_stats), z, sizeof z);
+  }
+  return e == hipSuccess ? 0 : -1;
+}
+#endif
