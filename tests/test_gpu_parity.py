@@ -332,3 +332,34 @@ def test_full_size_c3_against_oracle(hbmi, oracle):
     ref = oracle.loglike_batch(t, f, s, P[sel], synth.MAG_DEFAULT, synth.MAGERR_DEFAULT, 16)
     close_logl(a[sel], ref)
     assert len(bad) <= 4
+
+
+@pytest.mark.parametrize("order", ["sorted", "shuffled", "reversed"])
+def test_warm_start_paths_against_oracle(hbmi, oracle, order):
+    """The one-wave kernel warm-starts Kepler from the previous cadence of a
+    lane's chain (e <= 0.8, |dE| <= 0.25; hb_device.hpp hb_cadence_flux_chain).
+    Cadence order decides whether neighbours are close in phase: sorted (the
+    warm fast path), shuffled (large phase jumps: the reference start), reversed
+    (negative steps); eccentricities straddle the 0.8 gate and reach the
+    reference's unconverged regime (e > 0.85).  Templates and logL vs the
+    oracle."""
+    from hb_mcmc_amd import synth
+    from hb_mcmc_amd.likelihood import HBLikelihood
+
+    n = 1024
+    t, f, s = synth.dataset(n, oracle.light_curve)
+    if order == "shuffled":
+        p = np.random.default_rng(5).permutation(n)
+        t, f, s = t[p], f[p], s[p]
+    elif order == "reversed":
+        t, f, s = t[::-1].copy(), f[::-1].copy(), s[::-1].copy()
+    P = synth.walkers(24, seed=77, roche_frac=0.0)
+    P[:, 3] = np.array([0.02, 0.1, 0.3, 0.5, 0.7, 0.79, 0.8, 0.81, 0.84, 0.88, 0.92, 0.97] * 2)
+    with HBLikelihood(t, f, s) as L:
+        ll = L.loglike(P)
+        tm = L.light_curve(P)
+    close_logl(ll, oracle.loglike_batch(t, f, s, P, synth.MAG_DEFAULT, synth.MAGERR_DEFAULT, 8))
+    ref = oracle.light_curve_batch(t, P, 8)
+    ok = ~np.isnan(ref).any(1)
+    tol = lc_tol(P[:, 3])[:, None]
+    assert (np.abs(tm - ref)[ok] <= tol[ok]).all()
