@@ -772,20 +772,17 @@ __device__ __forceinline__ void hb_cadence_flux_chain(const double (&t)[K], cons
 #ifndef HB_WARM
 #define HB_WARM 1
 #endif
-  bool warm = HB_WARM && !first && (e <= kWarmEmax) && !__any(exact);
+  // e <= kWarmEmax is the caller's walker-uniform gate (model_pass_chain)
+  bool warm = HB_WARM && !first && !__any(exact);
   HB_STAT(0);
-#ifndef HB_WARM_FAST
-#define HB_WARM_FAST 1
-#endif
-  if (HB_WARM_FAST && warm) {
+  if (warm) {
     // the common warm step as one basic block (the K chains' solves and
     // polynomials interleave): start rotation of degree 9 (|dE| <= 1/16),
     // Newton step 1 with the mid rotation (|d| <= 2^-9), step 2 with the tiny
-    // one (|d| <= 2^-22) and the convergence test; any lane outside those
-    // bounds sends the whole wave through the general path below, which
-    // recomputes from the chain state
+    // one (|d| <= 2^-22) and the convergence test.  A lane outside those
+    // bounds recomputes (sin, cos) of its current E directly and the wave
+    // continues with the general Newton loop from there (no restart).
     bool fine = true;
-    double Ef[K], sf[K], cf[K], yf[K];
 #pragma unroll
     for (int k = 0; k < K; ++k) {
       const double D = m[k] - fma(-e, st.s[k], st.E[k]);
@@ -822,58 +819,35 @@ __device__ __forceinline__ void hb_cadence_flux_chain(const double (&t)[K], cons
       const double z = d * d;
       fine &= (fabs(d) <= 0x1p-22) & (e * z <= 0x1p-51 * den);
       rotate_back_tiny(d, z, s0, c0);
-      Ef[k] = E0;
-      sf[k] = s0;
-      cf[k] = c0;
-      yf[k] = y;
+      E[k] = E0;
+      s[k] = s0;
+      c[k] = c0;
     }
     if (__all(fine)) {
       HB_STAT(2);
 #pragma unroll
       for (int k = 0; k < K; ++k) {
-        st.E[k] = Ef[k];
-        st.s[k] = sf[k];
-        st.c[k] = cf[k];
+        st.E[k] = E[k];
+        st.s[k] = s[k];
+        st.c[k] = c[k];
       }
 #if HB_SPLIT_LIVE
       __asm__ volatile("" ::: "memory");
 #endif
-      flux_poly_k<K>(sf, cf, w, v, dd, zz);
+      flux_poly_k<K>(s, c, w, v, dd, zz);
       bad = !ok;
       return;
     }
-  }
-  if (warm) {
     HB_STAT(1);
-    bool small = true, mid = true;
-    double dl[K];
+    if (!fine) {  // (sin, cos) of the lane's current iterate, then Newton to convergence
 #pragma unroll
-    for (int k = 0; k < K; ++k) {
-      // dM wrapped into [-pi, pi]; E follows M's 2pi multiple
-      const double D = m[k] - fma(-e, st.s[k], st.E[k]);
-      const double q = rint(D * 0.15915494309189533577);
-      const double Dc = fma(-q, kTwoPi, D);
-      dl[k] = Dc * __builtin_amdgcn_rcp(fma(-e, st.c[k], 1.0));
-      E[k] = fma(q, kTwoPi, st.E[k]) + dl[k];
-      s[k] = st.s[k];
-      c[k] = st.c[k];
-      const double ad = fabs(dl[k]);
-      small &= ad <= kRotMaxK;
-      mid &= ad <= 0x1p-9;
-    }
-    warm = __all(small);
-    if (warm) {  // (sin, cos) rotated forward by dl
-      HB_STAT(2);
-      if (__all(mid)) {
-#pragma unroll
-        for (int k = 0; k < K; ++k) rotate_back_mid(-dl[k], dl[k] * dl[k], s[k], c[k]);
-      } else {
-#pragma unroll
-        for (int k = 0; k < K; ++k) rotate_back_wide(-dl[k], dl[k] * dl[k], s[k], c[k]);
+      for (int k = 0; k < K; ++k) {
+        ok &= sincos_fast_ok(E[k]);
+        sincos_fast(E[k], &s[k], &c[k]);
       }
-      if (!newton_k<K>(e, m, E, s, c, yk, ok)) warm = false;  // redo from the reference's start
-      if (warm) HB_STAT(3);
     }
+    warm = newton_k<K>(e, m, E, s, c, yk, ok);  // else: redo from the reference's start
+    if (warm) HB_STAT(3);
   }
   if (!warm) {
     HB_STAT(4);

@@ -41,6 +41,7 @@ struct EvalPlan {
   size_t slab_bytes = 0;  // template slab / histogram bytes (one-wave path)
   bool lds = true;     // template in LDS (else HBM scratch slab)
   size_t lds_bytes = 0;
+  double gap = 0.0;    // typical cadence spacing [d] (hb_cadence_gap), warm-chain gate
 };
 
 // One light curve of a catalog (hb_catalog_*): its slice of the concatenated
@@ -53,7 +54,7 @@ struct alignas(16) TargetDesc {
   double dist;   // mag_data[0] [pc]
   double gmag;   // mag_data[1]
   double gerr;   // magerr[0]
-  double pad1;
+  double gap;    // typical cadence spacing [d] (hb_cadence_gap), warm-chain gate
 };
 
 struct TrajArgs {
@@ -78,6 +79,8 @@ enum ProbeOp {
 };
 
 EvalPlan make_plan(long n);
+// 90th percentile of |t[i+1] - t[i]| (host; the eval kernel's warm-chain gate)
+double cadence_gap(const double* t, long n);
 // forces the load of hb_kernels.hip's code object on the current device
 hipError_t preload_code_object();
 // ph (optional): the shared-period phase table of the batch, (sin, cos)(t_i
@@ -96,7 +99,7 @@ hipError_t launch_eval_multi(int vpt, size_t slab_bytes, const double* t, const 
                              const hbdev::WalkerConst* wc, double* logl, hipStream_t s);
 int wave_vpt_for(long n);  // cadences per lane of the one-wave path, 0 if n > 2048
 size_t wave_slab_bytes(long n);
-size_t wave_lds_bytes(size_t slab);
+size_t wave_lds_bytes(size_t slab, int vpt);
 // acc (device sampler, one-wave path only): each wave also runs its slot's
 // Hastings test and history write (hb_accept.hpp); hipErrorNotSupported on the
 // multi-wave path

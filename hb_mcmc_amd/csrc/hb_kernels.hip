@@ -19,6 +19,9 @@
 #include <stdint.h>
 #include <string.h>
 
+#include <algorithm>
+#include <vector>
+
 #include "hb_accept.hpp"
 #include "hb_device.hpp"
 #include "hb_internal.hpp"
@@ -496,22 +499,41 @@ __device__ __forceinline__ void model_pass(const double* __restrict__ t, const d
   kmx_out = kmx;
 }
 
-// One-wave kernel: lane l owns the consecutive cadences l*VPT ..
-// l*VPT + VPT - 1, solved as KC chains of LC = VPT/KC cadences whose Kepler
-// starts are warm (hb_cadence_flux_chain) after each chain's first cadence.
-// Values go to the lane's row of the LDS slab, VPT doubles, position c stored
-// at c ^ (lane mod VPT) (a wave's accesses at one position then spread over
-// all banks, and the slab stays n * 8 bytes: 16 waves per CU fit the LDS);
-// the row is the lane's select keys afterwards.
-#ifndef HB_LANE_CHAIN
-#define HB_LANE_CHAIN 1
-#endif
+// One-wave kernel: lane l owns the rc = ceil(n/64) consecutive cadences
+// l*rc .. l*rc + rc - 1 (its row of the LDS slab, later its select keys).
+// The chain path solves a row as KC chains whose Kepler starts are warm
+// (hb_cadence_flux_chain) after each chain's first cadence.  Row stride: rc
+// when rc is a power of two, position c stored at c ^ (lane mod rc) (a wave's
+// accesses at one position then spread over all banks); otherwise rc | 1, an
+// odd stride that is conflict-free as it stands.  The slab is ~n * 8 bytes,
+// so short light curves of a catalog class keep more waves per CU.
 #ifndef HB_KC
 #define HB_KC 2  // chains per lane
 #endif
-template <int VPT>
-__device__ __forceinline__ int slab_pos(int lane, int c) {
-  return lane * VPT + (c ^ (lane & (VPT - 1)));
+struct Rows {
+  int rc;      // cadences per lane row
+  int stride;  // row stride [doubles]
+  int swz;     // XOR swizzle mask (rc - 1 for a power-of-two rc, else 0)
+  float rcp;   // 1 / rc (row of cadence i, i < 2^11: exact after rounding)
+};
+__host__ __device__ __forceinline__ int rows_stride(int rc) { return (rc & (rc - 1)) == 0 ? rc : (rc | 1); }
+__device__ __forceinline__ Rows make_rows(int n) {
+  Rows r;
+  r.rc = (n + 63) >> 6;
+  const bool p2 = (r.rc & (r.rc - 1)) == 0;
+  r.stride = rows_stride(r.rc);
+  r.swz = p2 ? r.rc - 1 : 0;
+  r.rcp = 1.0f / (float)r.rc;
+  return r;
+}
+__device__ __forceinline__ int slab_pos(const Rows& r, int lane, int c) {
+  return lane * r.stride + (c ^ (lane & r.swz));
+}
+// slab position of cadence i: row q = i / rc by the fp32 reciprocal
+// ((i + 0.5) / rc is >= 1/(2 rc) away from an integer, far above its error)
+__device__ __forceinline__ int slab_pos_of(const Rows& r, int i) {
+  const int q = (int)(((float)i + 0.5f) * r.rcp);
+  return slab_pos(r, q, i - q * r.rc);
 }
 
 // Eclipse terms are rare and spread over the orbit, so a wave whose lanes
@@ -528,25 +550,87 @@ __device__ __forceinline__ void ecl_apply(const WalkerConst& w, double* vals, co
   }
 }
 
-template <int VPT>
-__device__ __forceinline__ void model_pass_chain(const double* __restrict__ t, const double2* __restrict__ ph,
-                                                 int n, const WalkerConst& w, double* vals, double* eq_dr,
-                                                 int* eq_code, int lane) {
-  constexpr int KC = VPT < HB_KC ? VPT : HB_KC;
-  constexpr int LC = VPT / KC;
+// Whether a walker's Kepler solves take the warm chains: e <= kWarmEmax (the
+// reference's five steps converge, so the root is the same) and the first
+// Newton correction after the first-order start, |d1| <= e dM^2 / (2 (1-e)^3)
+// for the light curve's typical phase step dM (gap = 90th percentile of the
+// cadence spacing, host-side), at most kWarmD1: the two-step fast path then
+// holds for nearly every cadence.  Otherwise (high e, sparse or shuffled
+// cadences) the cold path with four interleaved cadences per lane is faster.
+#ifndef HB_WARM_D1
+#define HB_WARM_D1 0x1p-10
+#endif
+#ifndef HB_CHAIN_VPT_MIN
+#define HB_CHAIN_VPT_MIN 8
+#endif
+#ifndef HB_CHAIN_VPT_MAX
+#define HB_CHAIN_VPT_MAX 16
+#endif
+__device__ __forceinline__ bool chain_eligible(const WalkerConst& w, double gap) {
+  const double e = w.e;
+  const double dm = gap * kDay * fabs(w.mA);
+  const double ome = 1.0 - e;
+  return (e <= kWarmEmax) && (e * dm * dm <= 2.0 * HB_WARM_D1 * ome * ome * ome);
+}
+
+// Cold path in the one-wave kernel: the wave sweeps the light curve 64*K
+// consecutive cadences at a time (cadence base + k*64 + lane), so the eclipse
+// lanes of an iteration are neighbours in phase and the inline eclipse term
+// runs only on the few iterations that cross an eclipse.  Values are stored
+// at the lane-row slab positions (slab_pos_of) that the key load reads.
+__device__ __forceinline__ void model_pass_cold(const double* __restrict__ t, const double2* __restrict__ ph,
+                                                int n, const Rows& rw, const WalkerConst& w, double* vals,
+                                                int lane) {
+  constexpr int K = HB_K;
   const bool tab = (ph != nullptr) && (w.tab != 0.0);  // walker-uniform
   const int last = n - 1;
-  const int base = lane * VPT;
+  for (int base = 0; base < n; base += K * 64) {
+    double tk[K], v[K];
+    double2 pk[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const int i = min(base + k * 64 + lane, last);
+      tk[k] = t[i];
+      pk[k] = tab ? ph[i] : make_double2(0.0, 1.0);
+    }
+    bool bad;
+#if HB_SPLIT_LIVE
+    __asm__ volatile("" ::: "memory");
+#endif
+    hb_cadence_flux_k<K>(tk, pk, tab, w, v, bad);
+    if (__any(bad)) {  // out-of-domain angles: reference-order ocml path
+      if (bad) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) v[k] = hb_cadence_flux_slow(tk[k], &w);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const int i = base + k * 64 + lane;
+      if (i < n) vals[slab_pos_of(rw, i)] = v[k];
+    }
+  }
+}
+
+template <int VPT>
+__device__ __forceinline__ void model_pass_chain(const double* __restrict__ t, const double2* __restrict__ ph,
+                                                 int n, const Rows& rw, const WalkerConst& w, double* vals,
+                                                 double* eq_dr, int* eq_code, int lane) {
+  constexpr int KC = VPT < HB_KC ? VPT : HB_KC;
+  const int lc = (rw.rc + KC - 1) / KC;  // chain length (wave-uniform)
+  const bool tab = (ph != nullptr) && (w.tab != 0.0);  // walker-uniform
+  const int last = n - 1;
+  const int base = lane * rw.rc;
   const uint64_t lt_mask = (1ull << lane) - 1ull;
   int qn = 0;  // queued eclipse cadences (wave-uniform)
   ChainState<KC> st;
   double tk[KC];
 #pragma unroll
-  for (int k = 0; k < KC; ++k) tk[k] = t[min(base + k * LC, last)];
-  for (int j = 0; j < LC; ++j) {
+  for (int k = 0; k < KC; ++k) tk[k] = t[min(base + k * lc, last)];
+  for (int j = 0; j < lc; ++j) {
     double tn[KC];
 #pragma unroll
-    for (int k = 0; k < KC; ++k) tn[k] = t[min(base + k * LC + j + 1, last)];
+    for (int k = 0; k < KC; ++k) tn[k] = t[min(base + k * lc + j + 1, last)];
     double v[KC], dd[KC], zz[KC];
     bool bad;
 #if HB_SPLIT_LIVE
@@ -555,7 +639,7 @@ __device__ __forceinline__ void model_pass_chain(const double* __restrict__ t, c
     if (j == 0) {  // the chains' first cadences: the reference's start (table entries)
       double2 p0[KC];
 #pragma unroll
-      for (int k = 0; k < KC; ++k) p0[k] = tab ? ph[min(base + k * LC, last)] : make_double2(0.0, 1.0);
+      for (int k = 0; k < KC; ++k) p0[k] = tab ? ph[min(base + k * lc, last)] : make_double2(0.0, 1.0);
       hb_cadence_flux_chain<KC>(tk, p0, tab, true, w, st, v, dd, zz, bad);
     } else {  // warm; a cadence that falls back to the reference start evaluates sin/cos directly
       const double2 p0[KC] = {};
@@ -569,8 +653,9 @@ __device__ __forceinline__ void model_pass_chain(const double* __restrict__ t, c
     }
 #pragma unroll
     for (int k = 0; k < KC; ++k) {
-      const bool act = base + k * LC + j < n;
-      const int sp = slab_pos<VPT>(lane, k * LC + j);
+      const int c = k * lc + j;
+      const bool act = (c < rw.rc) & (base + c < n);
+      const int sp = slab_pos(rw, lane, c);
       if (act) vals[sp] = v[k];
       const bool need = act && !bad && eclipse_lane(w, dd[k], zz[k]);
       const uint64_t bal = __ballot(need);
@@ -581,7 +666,7 @@ __device__ __forceinline__ void model_pass_chain(const double* __restrict__ t, c
       }
       qn += __popcll(bal);
       tk[k] = tn[k];
-      const bool last = (j == LC - 1) && (k == KC - 1);
+      const bool last = (j == lc - 1) && (k == KC - 1);
       while (qn >= 64 || (last && qn > 0)) {  // wave-uniform
         const int cnt = qn < 64 ? qn : 64;
         ecl_apply(w, vals, eq_dr, eq_code, qn - cnt, cnt, lane);
@@ -1068,33 +1153,14 @@ __device__ __forceinline__ double wave_select2(const uint64_t (&key)[VPT], uint3
 #ifndef HB_PF
 #define HB_PF 0  // 1: request the chi^2 operands before the select (costs VGPR spills)
 #endif
-#ifndef HB_KEY_PERM
-#define HB_KEY_PERM 1
-#endif
-// Cadence held in key slot v of `lane`.  A light curve is smooth, so 64
-// consecutive cadences mostly share one histogram bin and a wave's LDS atomic
-// would serialise on one address; the skewed transpose (lane owns cadences
-// lane*VPT .. lane*VPT+VPT-1, visited in rotated order) gives each atomic
-// instruction 64 cadences spread over the whole light curve, and keeps the
-// ds_read_b64 of the slab at <= 2-way bank conflicts.
-template <int VPT>
-__device__ __forceinline__ int key_index(int v, int lane) {
-#if HB_LANE_CHAIN
-  return lane * VPT + v;  // the lane's own cadences, in slab-row order
-#elif HB_KEY_PERM
-  return lane * VPT + ((v + lane) & (VPT - 1));
-#else
-  return v * 64 + lane;
-#endif
-}
-// where key v of `lane` sits in the LDS slab
-template <int VPT>
-__device__ __forceinline__ int slab_key_index(int v, int lane) {
-#if HB_LANE_CHAIN
-  return slab_pos<VPT>(lane, v);
-#else
-  return key_index<VPT>(v, lane);
-#endif
+// Key slot v of `lane` holds cadence lane*rc + v (its own row; v >= rc is
+// padding).  A light curve is smooth, so 64 consecutive cadences mostly share
+// one histogram bin and a wave's LDS atomic would serialise on one address;
+// lane-owned rows give each atomic instruction 64 cadences spread over the
+// whole light curve.
+__device__ __forceinline__ int key_index(const Rows& r, int v, int lane) { return lane * r.rc + v; }
+__device__ __forceinline__ bool key_live(const Rows& r, int v, int lane, long n) {
+  return (v < r.rc) & (lane * r.rc + v < n);
 }
 
 // MULTI (catalog mode): the walker is list[blockIdx.x] and its light curve is
@@ -1107,7 +1173,7 @@ __global__ __launch_bounds__(64) HB_WPE_ATTR void hb_eval_wave_kernel(
     const double* __restrict__ t, const double2* __restrict__ ph, const double* __restrict__ f,
     const double* __restrict__ isg,
     long n, long kth, const WalkerConst* __restrict__ wcs, double* __restrict__ logl,
-    double* __restrict__ tmpl_out, int mode, int slab_bytes, const TargetDesc* __restrict__ tab,
+    double* __restrict__ tmpl_out, int mode, int slab_bytes, double gap, const TargetDesc* __restrict__ tab,
     const int* __restrict__ wt, const int* __restrict__ list, hbds::AccArgs hst) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int lane = threadIdx.x;
@@ -1134,11 +1200,15 @@ __global__ __launch_bounds__(64) HB_WPE_ATTR void hb_eval_wave_kernel(
 
   uint64_t kmn, kmx;
   uint64_t key[VPT];
-#if HB_LANE_CHAIN
+  const Rows rw = make_rows((int)n);
   {
-    double* eq_dr = reinterpret_cast<double*>(smem + slab_bytes + 8 * kCandMax);
-    int* eq_code = reinterpret_cast<int*>(eq_dr + kEclQ);
-    model_pass_chain<VPT>(t, ph, (int)n, w, vals, eq_dr, eq_code, lane);
+    if (VPT >= HB_CHAIN_VPT_MIN && VPT <= HB_CHAIN_VPT_MAX && chain_eligible(w, MULTI ? tab[wt[wv]].gap : gap)) {
+      double* eq_dr = reinterpret_cast<double*>(smem + slab_bytes + 8 * kCandMax);
+      int* eq_code = reinterpret_cast<int*>(eq_dr + kEclQ);
+      model_pass_chain<VPT>(t, ph, (int)n, rw, w, vals, eq_dr, eq_code, lane);
+    } else {
+      model_pass_cold(t, ph, (int)n, rw, w, vals, lane);
+    }
   }
   __syncthreads();
   // keys, and the lane's min/max keys (values ~1; -0.0 / +0.0 take the outer
@@ -1148,8 +1218,8 @@ __global__ __launch_bounds__(64) HB_WPE_ATTR void hb_eval_wave_kernel(
     bool nan = false;
 #pragma unroll
     for (int v = 0; v < VPT; ++v) {
-      const bool act = key_index<VPT>(v, lane) < n;
-      const double x = act ? vals[slab_key_index<VPT>(v, lane)] : vmn;
+      const bool act = key_live(rw, v, lane, n);
+      const double x = act ? vals[slab_pos(rw, lane, v)] : vmn;
       key[v] = act ? dkey(x) : ~0ull;  // padding sorts last, never selected
       vmn = fmin(vmn, x);
       vmx = fmax(vmx, x);
@@ -1162,30 +1232,19 @@ __global__ __launch_bounds__(64) HB_WPE_ATTR void hb_eval_wave_kernel(
       kmx = 0ull;
 #pragma unroll
       for (int v = 0; v < VPT; ++v) {
-        if (key_index<VPT>(v, lane) < n) {
+        if (key_live(rw, v, lane, n)) {
           kmn = key[v] < kmn ? key[v] : kmn;
           kmx = key[v] > kmx ? key[v] : kmx;
         }
       }
     }
   }
-#else
-  model_pass<64>(t, ph, (int)n, w, vals, lane, kmn, kmx);
-#endif
 #if HB_SEL_V == 1
   kmn = wave_min_u64(kmn);
   kmx = wave_max_u64(kmx);
 #else
   kmn = wave_reduce_u64(kmn, OpMinU64());
   kmx = wave_reduce_u64(kmx, OpMaxU64());
-#endif
-#if !HB_LANE_CHAIN
-  __syncthreads();
-#pragma unroll
-  for (int v = 0; v < VPT; ++v) {
-    const int i = key_index<VPT>(v, lane);
-    key[v] = i < n ? dkey(vals[slab_key_index<VPT>(v, lane)]) : ~0ull;  // padding sorts last, never selected
-  }
 #endif
   // chi^2 operands requested now so that their L2 latency overlaps the
   // median select (VPT <= 16: 4*VPT more VGPRs while the keys are live)
@@ -1194,7 +1253,7 @@ __global__ __launch_bounds__(64) HB_WPE_ATTR void hb_eval_wave_kernel(
   if (HB_PF && VPT <= 16 && mode == 0) {
 #pragma unroll
     for (int v = 0; v < PF; ++v) {
-      const int i = min(key_index<VPT>(v, lane), (int)n - 1);
+      const int i = min(key_index(rw, v, lane), (int)n - 1);
       fv[v] = f[i];
       iv[v] = isg[i];
     }
@@ -1215,8 +1274,8 @@ __global__ __launch_bounds__(64) HB_WPE_ATTR void hb_eval_wave_kernel(
     double* o = tmpl_out + (size_t)wv * (size_t)n;
 #pragma unroll
     for (int v = 0; v < VPT; ++v) {
-      const int i = key_index<VPT>(v, lane);
-      if (i < n) {
+      const int i = key_index(rw, v, lane);
+      if (key_live(rw, v, lane, n)) {
         const double m = (dval(key[v]) - med) + 1.0;
         o[i] = (blend + m * one_m_blend) * tune;
       }
@@ -1226,8 +1285,8 @@ __global__ __launch_bounds__(64) HB_WPE_ATTR void hb_eval_wave_kernel(
   double acc = 0.0;
 #pragma unroll
   for (int v = 0; v < VPT; ++v) {
-    const int i = key_index<VPT>(v, lane);
-    if (i < n) {
+    const int i = key_index(rw, v, lane);
+    if (key_live(rw, v, lane, n)) {
       double m = (dval(key[v]) - med) + 1.0;
       m = (blend + m * one_m_blend) * tune;
       const double r = (HB_PF && VPT <= 16) ? (m - fv[v < PF ? v : 0]) * iv[v < PF ? v : 0] : (m - f[i]) * isg[i];
@@ -1605,7 +1664,7 @@ static hipError_t launch_wave_t(const EvalPlan& pl, const double* t, const doubl
                                 const WalkerConst* wc, int nwalk, double* logl, double* tmpl, int mode,
                                 hipStream_t s) {
   hipLaunchKernelGGL((hb_eval_wave_kernel<VPT, false>), dim3(nwalk), dim3(64), pl.lds_bytes, s, t, ph, f, sg,
-                     pl.n, pl.kth, wc, logl, tmpl, mode, (int)pl.slab_bytes, nullptr, nullptr, nullptr,
+                     pl.n, pl.kth, wc, logl, tmpl, mode, (int)pl.slab_bytes, pl.gap, nullptr, nullptr, nullptr,
                      hbds::AccArgs{});
   return hipGetLastError();
 }
@@ -1615,7 +1674,7 @@ static hipError_t launch_wave_acc_t(const EvalPlan& pl, const double* t, const d
                                     const double* sg, const WalkerConst* wc, int nwalk, double* logl,
                                     hipStream_t s, const hbds::AccArgs& acc) {
   hipLaunchKernelGGL((hb_eval_wave_kernel<VPT, false, true>), dim3(nwalk), dim3(64), pl.lds_bytes, s, t, ph, f,
-                     sg, pl.n, pl.kth, wc, logl, nullptr, 0, (int)pl.slab_bytes, nullptr, nullptr, nullptr, acc);
+                     sg, pl.n, pl.kth, wc, logl, nullptr, 0, (int)pl.slab_bytes, pl.gap, nullptr, nullptr, nullptr, acc);
   return hipGetLastError();
 }
 
@@ -1624,9 +1683,9 @@ static hipError_t launch_multi_t(size_t slab, const double* t, const double2* ph
                                  const double* sg,
                                  const TargetDesc* tab, const int* wt, const int* list, int count,
                                  const WalkerConst* wc, double* logl, hipStream_t s) {
-  const size_t lds = wave_lds_bytes(slab);
+  const size_t lds = wave_lds_bytes(slab, VPT);
   hipLaunchKernelGGL((hb_eval_wave_kernel<VPT, true>), dim3(count), dim3(64), lds, s, t, ph, f, sg, 0L, 0L,
-                     wc, logl, nullptr, 0, (int)slab, tab, wt, list, hbds::AccArgs{});
+                     wc, logl, nullptr, 0, (int)slab, 0.0, tab, wt, list, hbds::AccArgs{});
   return hipGetLastError();
 }
 
@@ -1735,14 +1794,25 @@ int wave_vpt_for(long n) {
 // the template slab (64 lane rows of VPT doubles) doubles as the
 // 2^kSelBits-bin histogram of the select
 size_t wave_slab_bytes(long n) {
-  const size_t vals = HB_LANE_CHAIN ? (size_t)64 * wave_vpt_for(n) * 8 : (size_t)n * 8;
+  const size_t vals = (size_t)64 * rows_stride((int)((n + 63) / 64)) * 8;
   const size_t slab = vals > (size_t)(4u << kSelBits) ? vals : (size_t)(4u << kSelBits);
   return (slab + 15) & ~(size_t)15;
 }
 
-// slab | select candidates | eclipse queue (lane-chain model pass)
-size_t wave_lds_bytes(size_t slab) {
-  return slab + 8 * kCandMax + (HB_LANE_CHAIN ? (size_t)kEclQ * (8 + 4) : 0);
+// slab | select candidates | eclipse queue (chain model pass only)
+size_t wave_lds_bytes(size_t slab, int vpt) {
+  const bool chain = vpt >= HB_CHAIN_VPT_MIN && vpt <= HB_CHAIN_VPT_MAX;
+  return slab + 8 * kCandMax + (chain ? (size_t)kEclQ * (8 + 4) : 0);
+}
+
+double cadence_gap(const double* t, long n) {
+  if (n < 2) return 0.0;
+  std::vector<double> g((size_t)(n - 1));
+  for (long i = 0; i + 1 < n; ++i) g[(size_t)i] = fabs(t[i + 1] - t[i]);
+  const size_t q = (size_t)((n - 1) * 9 / 10);
+  std::nth_element(g.begin(), g.begin() + q, g.end());
+  const double v = g[q];
+  return v == v ? v : __builtin_inf();  // NaN spacing: never warm
 }
 
 EvalPlan make_plan(long n) {
@@ -1754,7 +1824,7 @@ EvalPlan make_plan(long n) {
     pl.nw = 1;
     pl.lds = true;
     pl.slab_bytes = wave_slab_bytes(n);
-    pl.lds_bytes = wave_lds_bytes(pl.slab_bytes);
+    pl.lds_bytes = wave_lds_bytes(pl.slab_bytes, pl.vpt);
     return pl;
   }
   const size_t lds_cap = 163840;

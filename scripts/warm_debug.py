@@ -28,12 +28,13 @@ for order in ["sorted", "shuffled", "reversed"]:
         tm = L.light_curve(P)
     ref = orc.light_curve_batch(t, P, 8)
     e = P[:, 3]
-    tol = 1e-12 * np.maximum(1.0, (0.2 / (1 - e)) ** 3)
+    tol = 1e-12 * np.maximum(1.0, (0.2 / (1 - e)) ** 3)[:, None]
+    tol = np.maximum(tol, 1e-11 * np.abs(ref))
     for r in range(len(P)):
         d = np.abs(tm[r] - ref[r])
         bad = ~(d <= tol[r]) & ~np.isnan(ref[r])
         if bad.any():
             i = int(np.nanargmax(np.where(np.isnan(d), np.inf, d)))
             print(f"{order} row {r} e={e[r]} nbad={bad.sum()} worst i={i} t={t[i]:.9g} got={tm[r, i]!r} "
-                  f"ref={ref[r, i]!r} tol={tol[r]:.2e} bad idx={np.nonzero(bad)[0][:12].tolist()} P={P[r].tolist()}")
+                  f"ref={ref[r, i]!r} tol={tol[r, i]:.2e} bad idx={np.nonzero(bad)[0][:12].tolist()} P={P[r].tolist()}")
 print("done")
