@@ -300,23 +300,40 @@ def run_c5(a, rank, world, local, dev):
     no data-path collective (independent targets)."""
     from hb_mcmc_amd.catalog import Catalog, deal_targets
 
+    from hb_mcmc_amd.hbio import load_folded_catalog
+
+    # targets 0..110: the reference's folded light curves (data/folded_catalog.npz)
+    # with cp_data magnitudes; the rest: synthetic fill, N ~ U[82, 1861]
+    real = load_folded_catalog()[:a.targets]
     rng = np.random.default_rng(20260105)
-    ncad = rng.integers(82, 1862, a.targets)  # the folded files' empirical range (SURVEY.md 8(d))
+    nsyn = a.targets - len(real)
+    ncad = np.concatenate([[len(r["t"]) for r in real], rng.integers(82, 1862, nsyn)]).astype(np.int64)
     owner = deal_targets(ncad, world)
     mine = [k for k in range(a.targets) if owner[k] == rank]
-    targets = []
+    targets, thetas = [], []
     for k in mine:
         n = int(ncad[k])
+        if k < len(real):
+            r = real[k]
+            targets.append((r["t"], r["flux"], r["sigma"], r["mag"], r["magerr"]))
+            th = synth.THETA_STAR.copy()
+            th[2] = np.log10(r["period"])
+            th[6] = np.fmod(th[6], r["period"])
+            thetas.append(th)
+            continue
         t = synth.cadences(n)
         with HBLikelihood(t, np.ones(n), np.ones(n), device=local) as tmp:
             truth = tmp.light_curve(synth.THETA_STAR[None, :])[0]
         s_ = np.full(n, 1e-3)
         targets.append((t, truth + s_ * synth.noise(n), s_))
+        thetas.append(synth.THETA_STAR)
     cat = Catalog(targets, device=local)
     wpt = np.full(len(mine), a.walkers_per_target, dtype=np.int32)
     wtot = int(wpt.sum())
     nb = 4
-    P = [torch.from_numpy(synth.walkers(wtot, seed=2000 + 97 * rank + k)).to(dev) for k in range(nb)]
+    P = [torch.from_numpy(np.concatenate([synth.walkers(a.walkers_per_target, seed=2000 + 97 * rank + 7919 * k + j,
+                                                        theta=th) for j, th in enumerate(thetas)])).to(dev)
+         for k in range(nb)]
     out = torch.empty(wtot, dtype=torch.float64, device=dev)
     stream = torch.cuda.current_stream()
     for k in range(a.warmup):
@@ -352,8 +369,10 @@ def run_c5(a, rank, world, local, dev):
         line = {"metric": METRIC, "value": evals / wall, "unit": "evals/s", "n_gpus": world, "steps": a.steps,
                 "warmup": a.warmup, "ms_per_step": wall / a.steps * 1e3, "higher_is_better": True,
                 "scaling": "strong", "vs_baseline": None, "dtype": "f64",
-                "data": "synthetic catalog: N ~ U[82, 1861] per target (rng 20260105), truth = "
-                        "test_likelihoods.c:33-36, sigma 1e-3",
+                "data": f"{len(real)} folded light curves of the reference (data/lightcurves/folded_lightcurves, "
+                        "periods.txt; magnitudes from data/color_mag/cp_data_4-21-2022.csv) + "
+                        f"{nsyn} synthetic (N ~ U[82, 1861], rng 20260105, truth = test_likelihoods.c:33-36, "
+                        "sigma 1e-3); walkers around the truth at each target's period",
                 "config": {"workload": f"C5: catalog sweep, {a.targets} targets x {a.walkers_per_target} walkers",
                            "targets": a.targets, "walkers_per_target": a.walkers_per_target,
                            "global_walkers": a.targets * a.walkers_per_target,

@@ -777,6 +777,25 @@ extern "C" void calc_light_curve(double* times, long Nt, double* pars, double* t
   if (hb_light_curve_batch(c, pars, 1, tmpl, nullptr) != 0) hb_fatal("hb_light_curve_batch failed");
 }
 
+// likelihood3.c:880-941 (SAVECOMP = 0, likelihood3.h:30): the model light
+// curve on 10 000 times spaced (30 d + P) / 10 000 apart, accumulated the way
+// the reference does (t[i] = t[i-1] + dt), evaluated on the GPU, written as
+// "%12.5e\t%12.5e\n" lines.
+extern "C" void write_lc_to_file(double* pars, char* fname) {
+  require_device();
+  constexpr long kN = 10000;
+  const double span = 30. + pow(10., pars[2]);
+  const double dt = span / (double)kN;
+  std::vector<double> times((size_t)kN), lc((size_t)kN);
+  times[0] = 0.;
+  for (long i = 1; i < kN; ++i) times[(size_t)i] = times[(size_t)i - 1] + dt;
+  calc_light_curve(times.data(), kN, pars, lc.data());
+  FILE* fp = fopen(fname, "w");
+  if (!fp) return;  // the reference would crash in fprintf; here nothing is written
+  for (long i = 0; i < kN; ++i) fprintf(fp, "%12.5e\t%12.5e\n", times[(size_t)i], lc[(size_t)i]);
+  fclose(fp);
+}
+
 extern "C" void traj(double* times, double* tp, double* d_arr, double* Z1_arr, double* Z2_arr,
                      double* rr_arr, double* ff_arr, int Nt) {
   require_device();

@@ -114,6 +114,10 @@ double envelope_Temp(double logM);
 double envelope_Radius(double logM);
 /* likelihood3.c:945-948 */
 double Eggleton_RL(double q);
+/* likelihood3.c:880-941 (SAVECOMP = 0): the model light curve at 10 000
+ * times spanning 30 d + one period, written to `fname` as "%12.5e\t%12.5e"
+ * lines (time [d], flux).  The light curve is computed on the GPU. */
+void write_lc_to_file(double pars[], char fname[]);
 
 /* ===================== Part 2: batched MI355X interface ===================== */
 

@@ -31,12 +31,14 @@
  *   orc_stellar           <- calc_radii_and_Teffs                likelihood3.c:693-717
  *   orc_photometry        <- calc_mags                           likelihood3.c:725-795
  *   orc_loglike           <- loglikelihood                       likelihood3.c:809-873
+ *   orc_write_lc_file     <- write_lc_to_file                    likelihood3.c:880-941
  *   orc_lobe_fraction     <- Eggleton_RL                         likelihood3.c:945-948
  *   orc_roche_flag        <- RocheOverflow                       likelihood3.c:953-974
  * Compile-time configuration mirrored: USE_GMAG=1, USE_COLOR_INFO=0,
  * ALPHA_FREE=ALPHA_MORE=BLENDING=1 => 21 parameters (likelihood3.h:11-29).
  */
 #include <math.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -501,4 +503,26 @@ void orc_light_curve_batch(const double *tt, long n, const double *pw, long w, d
 #pragma omp parallel for schedule(static)
 #endif
     for (long j = 0; j < w; ++j) orc_light_curve(tt, n, pw + 21 * j, out + n * j);
+}
+
+/* ------------------------------------------------------------------ */
+/* model light curve over 30 d + one period, to a text file             */
+/* (likelihood3.c:880-941, SAVECOMP = 0 as configured in likelihood3.h:30)*/
+/* ------------------------------------------------------------------ */
+void orc_write_lc_file(const double *p, const char *path)
+{
+    enum { NT = 10000 };
+    double span = 30. + pow(10., p[2]);
+    double step = span / (double)NT;
+    double *tt = (double *)malloc(2 * NT * sizeof(double));
+    double *lc = tt + NT;
+    tt[0] = 0.;
+    for (int i = 1; i < NT; ++i) tt[i] = tt[i - 1] + step; /* running sum, as written */
+    orc_light_curve(tt, NT, p, lc);
+    FILE *fp = fopen(path, "w");
+    if (fp) {
+        for (int i = 0; i < NT; ++i) fprintf(fp, "%12.5e\t%12.5e\n", tt[i], lc[i]);
+        fclose(fp);
+    }
+    free(tt);
 }

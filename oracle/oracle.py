@@ -71,6 +71,7 @@ class _Base:
         s("quickSort").argtypes = [_PD, _I, _I]
         s("partition").restype = _D
         s("partition").argtypes = [_PD, _I, _I]
+        s("write_lc_to_file").argtypes = [_PD, C.c_char_p]
 
     def _sym(self, name):
         return getattr(self.lib, self.SYM.get(name, name))
@@ -163,6 +164,10 @@ class _Base:
         k = self._sym("partition")(_ptr(a), 0, len(a) - 1)
         return int(k), a
 
+    def write_lc_to_file(self, p, path):
+        p = np.ascontiguousarray(p, dtype=np.float64)
+        self._sym("write_lc_to_file")(_ptr(p), os.fsencode(path))
+
 
 class Oracle(_Base):
     SYM = {
@@ -185,6 +190,7 @@ class Oracle(_Base):
         "remove_median": "orc_median_shift",
         "quickSort": "orc_quicksort",
         "partition": "orc_partition",
+        "write_lc_to_file": "orc_write_lc_file",
     }
 
     def __init__(self, path: str | None = None):

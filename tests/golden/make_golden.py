@@ -304,6 +304,24 @@ def sampler_fixture():
         shutil.rmtree(tmp, ignore_errors=True)
 
 
+def writelc_fixture(ref: Reference, g):
+    """write_lc_to_file (likelihood3.c:880-941): the reference's file bytes for
+    THETA_STAR and seeded draws around it (periods 0.9-12 d)."""
+    pv = np.vstack([synth.THETA_STAR[None, :], random_params(g, 5, scale=1.0)])
+    pv[1:, 2] = np.log10(np.array([0.9, 2.0, 3.3, 7.5, 12.0]))
+    pv[1:, 6] = np.fmod(pv[1:, 6], 10 ** pv[1:, 2])
+    tmp = tempfile.mkdtemp()
+    try:
+        files = {}
+        for k, p in enumerate(pv):
+            path = os.path.join(tmp, f"lc{k}.txt")
+            ref.write_lc_to_file(p, path)
+            files[f"file{k}"] = np.frombuffer(open(path, "rb").read(), dtype=np.uint8)
+        save("writelc.npz", params=pv, **files)
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+
+
 def main():
     if not os.path.isdir(REF):
         sys.exit("reference tree not found; goldens can only be generated in the development container")
@@ -317,6 +335,7 @@ def main():
     limits_fixture(ref)
     pyhb_fixture(g)
     sampler_fixture()
+    writelc_fixture(ref, np.random.Generator(np.random.PCG64(20261016)))
 
 
 def sampler_only():
@@ -327,5 +346,7 @@ def sampler_only():
 if __name__ == "__main__":
     if len(sys.argv) > 1 and sys.argv[1] == "sampler":
         sampler_only()
+    elif len(sys.argv) > 1 and sys.argv[1] == "writelc":
+        writelc_fixture(Reference(), np.random.Generator(np.random.PCG64(20261016)))
     else:
         main()

@@ -202,3 +202,86 @@ def test_catalog_cli_two_ranks_equals_hb_mcmc_cli(hbmi, oracle, tmp_path):
         assert len(files) == 12 + 7
         for rel in files:
             assert filecmp.cmp(os.path.join(root, rel), os.path.join(ours, rel), shallow=False), (tic, rel)
+
+
+# ---------------------------------------------- the reference's own targets
+def test_cp_data_reader_and_folded_catalog():
+    """cp_data CSV reader (hbio.read_cp_data / cp_mag_data) and the packed
+    folded light curves (data/folded_catalog.npz): 111 targets, N in
+    [82, 1861], every one with a cp_data row and a period; the mag block takes
+    the columns dist, Gmag0, BmV0, VmG0, GmT0 (+ errors) and the reference's
+    mag-file fallbacks for missing values (helpful_functions.py:377-420)."""
+    from hb_mcmc_amd.hbio import DATA_DIR, cp_mag_data, load_folded_catalog, read_cp_data
+
+    cp = read_cp_data(os.path.join(DATA_DIR, "cp_data_4-21-2022.csv"))
+    assert len(cp) == 360
+    r = cp["390661644"]  # first row of the CSV
+    mag, err = cp_mag_data(r)
+    assert np.array_equal(mag, [1063.35, 7.474916800000001, -0.1333100000000002, -0.0528777999999998,
+                                -0.0545445999999998])
+    assert np.array_equal(err, [0.2794518397133617, 0.24556637711065, 0.2780135623688168, 0.0595220802711405])
+    mag, err = cp_mag_data(cp["440546714"])  # no Gaia: G, V-G and G-T missing
+    assert mag[0] == 944.364 and (mag[1], err[0]) == (10.0, 10000.0)
+    assert (mag[3], err[2]) == (0.0, 1000.0) and (mag[4], err[3]) == (0.0, 1000.0)
+    assert mag[2] == -0.8790000000000013 and err[1] == 1.1352114340509436
+    m0, e0 = cp_mag_data(None)
+    assert np.array_equal(m0, [1000.0, 1, 1, 1, 1]) and np.array_equal(e0, np.full(4, 1e15))
+    cat = load_folded_catalog()
+    assert len(cat) == 111
+    ns = [len(c["t"]) for c in cat]
+    assert min(ns) == 82 and max(ns) == 1861
+    assert all(c["tic"] in cp and c["period"] > 0 for c in cat)
+
+
+def test_folded_catalog_matches_reference_files():
+    """The packed arrays equal the reference's files as its reader parses
+    them (mcmc_wrapper2.c:257-298 via hbio.read_folded_lc)."""
+    from hb_mcmc_amd.hbio import load_folded_catalog, read_folded_lc, read_periods
+
+    d = "/root/reference/data/lightcurves/folded_lightcurves"
+    if not os.path.isdir(d):
+        pytest.skip("reference tree not present (GPU box)")
+    per = read_periods("/root/reference/data/lightcurves/periods.txt")
+    for c in load_folded_catalog():
+        t, f, e = read_folded_lc(os.path.join(d, c["name"]))
+        assert np.array_equal(t, c["t"]) and np.array_equal(f, c["flux"]) and np.array_equal(e, c["sigma"])
+        assert per[c["tic"]] == c["period"]
+
+
+def test_mag_file_round_trip(tmp_path):
+    from hb_mcmc_amd.hbio import read_mag_file, write_mag_file
+
+    mag, err = np.array([812.5, 9.75, 0.125, -0.25, 0.0625]), np.array([0.01, 0.2, 0.3, 0.04])
+    write_mag_file(str(tmp_path / "m.txt"), mag, err)
+    m2, e2 = read_mag_file(str(tmp_path / "m.txt"))
+    assert np.array_equal(m2, mag) and np.array_equal(e2, err)
+
+
+@pytest.mark.gpu
+def test_catalog_on_reference_targets_against_oracle(hbmi, oracle):
+    """The 111 folded light curves with their cp_data magnitude blocks in one
+    catalog (every size class N = 82..1861): logL of 8 walkers per target at
+    the target's period vs the oracle (1e-10 relative; sentinel/NaN exact)."""
+    from hb_mcmc_amd import synth
+    from hb_mcmc_amd.catalog import Catalog
+    from hb_mcmc_amd.hbio import load_folded_catalog
+
+    cat = load_folded_catalog()
+    W = 8
+    P = []
+    for k, c in enumerate(cat):
+        th = synth.THETA_STAR.copy()
+        th[2] = np.log10(c["period"])
+        th[6] = np.fmod(th[6], c["period"])
+        P.append(synth.walkers(W, seed=300 + k, theta=th))
+    P = np.concatenate(P)
+    with Catalog([(c["t"], c["flux"], c["sigma"], c["mag"], c["magerr"]) for c in cat]) as C_:
+        got = C_.loglike(P, np.full(len(cat), W, dtype=np.int32))
+    for k, c in enumerate(cat):
+        ref = oracle.loglike_batch(c["t"], c["flux"], c["sigma"], P[k * W:(k + 1) * W], c["mag"], c["magerr"], 8)
+        g = got[k * W:(k + 1) * W]
+        assert np.array_equal(np.isnan(g), np.isnan(ref)), c["name"]
+        ok = ~np.isnan(ref)
+        assert np.array_equal(g[ref == -5e14], ref[ref == -5e14]), c["name"]
+        err = np.abs(g[ok] - ref[ok]) / np.maximum(1.0, np.abs(ref[ok]))
+        assert err.max(initial=0.0) <= LOGL_RTOL, (c["name"], err.max())

@@ -370,3 +370,19 @@ def test_warm_start_paths_against_oracle(hbmi, oracle, order):
     ok = ~np.isnan(ref).any(1)
     tol = lc_tol(P[:, 3], ref)
     assert (np.abs(tm - ref)[ok] <= tol[ok]).all()
+
+
+# ------------------------------------------------- write_lc_to_file
+def test_write_lc_to_file_bytes(hbmi, tmp_path):
+    """write_lc_to_file (likelihood3.c:880-941) through libhbmi.so: the light
+    curve (N = 10 000 > 2048: the block kernel) computed on the GPU and printed
+    with %12.5e is the reference's file byte for byte.  (A template within
+    1e-12 of the reference can only print differently when a value lies within
+    1e-12 of a 5-digit rounding boundary; none of these fixtures has one.)"""
+    g = golden("writelc.npz")
+    hbmi.write_lc_to_file.argtypes = [PD, C.c_char_p]
+    for k, pv in enumerate(g["params"]):
+        path = tmp_path / f"lc{k}.txt"
+        pv = np.ascontiguousarray(pv)
+        hbmi.write_lc_to_file(p(pv), str(path).encode())
+        assert path.read_bytes() == g[f"file{k}"].tobytes(), f"fixture {k}"

@@ -92,3 +92,13 @@ def test_20k_and_real1861(oracle):
     assert same(tm.sum(1), g["tsum"]) and same(tm[:, :16], g["thead"]) and same(tm[:, -16:], g["ttail"])
     g = golden("lc_real237957506.npz")
     assert same(oracle.loglike_batch(g["t"], g["f"], g["s"], g["params"], g["mag"], g["magerr"], 8), g["logl"])
+
+
+def test_write_lc_to_file_bytes(oracle, tmp_path):
+    """write_lc_to_file (likelihood3.c:880-941): the oracle's file equals the
+    reference's byte for byte (10 000 '%12.5e\\t%12.5e' lines)."""
+    g = golden("writelc.npz")
+    for k, p in enumerate(g["params"]):
+        path = tmp_path / f"lc{k}.txt"
+        oracle.write_lc_to_file(p, str(path))
+        assert path.read_bytes() == g[f"file{k}"].tobytes()
