@@ -6,7 +6,6 @@
 // error channel); the batched API returns a negative code instead.
 // Part 2: the batched context API (hb_create / hb_loglik_batch...).
 #include <hip/hip_runtime.h>
-#include <hipcub/hipcub.hpp>
 
 #include <math.h>
 #include <stdint.h>
@@ -911,17 +910,14 @@ extern "C" void remove_median(double* arr, long begin, long end) {
 extern "C" void quickSort(double arr[], int low, int high) {
   require_device();
   if (low >= high) return;
-  const int n = high - low + 1;
+  const long n = (long)high - low + 1;
+  long npad = 1;
+  while (npad < n) npad <<= 1;
   double* d_in = t_buf_a.get((size_t)n);
-  double* d_out = t_buf_b.get((size_t)n);
+  uint64_t* d_keys = reinterpret_cast<uint64_t*>(t_buf_b.get((size_t)npad));
   if (hipMemcpy(d_in, arr + low, (size_t)n * 8, hipMemcpyHostToDevice) != hipSuccess) hb_fatal("upload");
-  size_t tmp_bytes = 0;
-  (void)hipcub::DeviceRadixSort::SortKeys(nullptr, tmp_bytes, d_in, d_out, n);
-  void* d_tmp = nullptr;
-  if (hipMalloc(&d_tmp, tmp_bytes > 0 ? tmp_bytes : 16) != hipSuccess) hb_fatal("hipMalloc(sort tmp)");
-  if (hipcub::DeviceRadixSort::SortKeys(d_tmp, tmp_bytes, d_in, d_out, n) != hipSuccess) hb_fatal("sort");
-  if (hipMemcpy(arr + low, d_out, (size_t)n * 8, hipMemcpyDeviceToHost) != hipSuccess) hb_fatal("download");
-  (void)hipFree(d_tmp);
+  if (hbk::launch_sort(d_in, d_in, d_keys, n, nullptr) != hipSuccess) hb_fatal("sort launch");
+  if (hipMemcpy(arr + low, d_in, (size_t)n * 8, hipMemcpyDeviceToHost) != hipSuccess) hb_fatal("download");
 }
 
 extern "C" double partition(double arr[], int low, int high) {

@@ -111,5 +111,8 @@ hipError_t launch_traj(const double* d_times, int nt, const TrajArgs& ta, double
 hipError_t launch_probe(int op, const double* d_in, double* d_out, hipStream_t s);
 hipError_t launch_partition(double* d_a, int lo, int hi, int* d_res, hipStream_t s);
 hipError_t launch_median(double* d_a, long n, long kth, hipStream_t s);
+// ascending sort of d_in[0..n) into d_out (bitonic over order-preserving keys;
+// d_keys: room for n rounded up to a power of two)
+hipError_t launch_sort(const double* d_in, double* d_out, uint64_t* d_keys, long n, hipStream_t s);
 
 }  // namespace hbk

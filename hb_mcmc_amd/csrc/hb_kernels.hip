@@ -1610,6 +1610,60 @@ __global__ __launch_bounds__(1024) void hb_median_kernel(double* __restrict__ a,
 }
 
 // ---------------------------------------------------------------------------
+// quickSort drop-in (likelihood3.c:70-83): bitonic sort of order-preserving
+// 64-bit keys (dkey), padded to a power of two with ~0 (sorts last).  Up to
+// kSortLds keys the whole network runs in one workgroup's LDS; beyond it the
+// merge steps with a stride >= kSortLds/2 are one global launch each and the
+// smaller strides of every stage finish in LDS per kSortLds-key tile.  Off the
+// batched hot path (drop-in completeness); equal keys are equal values, so
+// stability does not matter.
+// ---------------------------------------------------------------------------
+constexpr int kSortLds = 8192;  // keys per LDS tile (64 KiB)
+__global__ __launch_bounds__(1024) void hb_sort_keys_kernel(const double* __restrict__ in, long n, long npad,
+                                                            uint64_t* __restrict__ keys) {
+  for (long i = blockIdx.x * 1024L + threadIdx.x; i < npad; i += (long)gridDim.x * 1024L)
+    keys[i] = i < n ? dkey(in[i]) : ~0ull;
+}
+__global__ __launch_bounds__(1024) void hb_sort_vals_kernel(const uint64_t* __restrict__ keys, long n,
+                                                            double* __restrict__ out) {
+  for (long i = blockIdx.x * 1024L + threadIdx.x; i < n; i += (long)gridDim.x * 1024L) out[i] = dval(keys[i]);
+}
+__device__ __forceinline__ void cmp_swap(uint64_t& a, uint64_t& b, bool up) {
+  const uint64_t lo = a < b ? a : b, hi = a < b ? b : a;
+  a = up ? lo : hi;
+  b = up ? hi : lo;
+}
+// stages k = kfrom .. kto (doubling), strides j < min(k, tile) of each, on
+// one LDS tile of `tile` keys (tile = npad when the whole sort fits); the
+// direction of a pair is that of its k-block in the global index
+__global__ __launch_bounds__(1024) void hb_sort_tile_kernel(uint64_t* __restrict__ keys, int tile, long kfrom,
+                                                            long kto) {
+  __shared__ uint64_t sk[kSortLds];
+  const long base = (long)blockIdx.x * tile;
+  for (int i = threadIdx.x; i < tile; i += 1024) sk[i] = keys[base + i];
+  __syncthreads();
+  for (long k = kfrom; k <= kto; k <<= 1) {
+    for (long j = (k < tile ? k : tile) >> 1; j > 0; j >>= 1) {
+      for (int q = threadIdx.x; q < tile / 2; q += 1024) {
+        const int i = (int)(2 * j * (q / j) + (q % j));  // lower index of the pair
+        const bool up = ((base + i) & k) == 0;
+        cmp_swap(sk[i], sk[i + j], up);
+      }
+      __syncthreads();
+    }
+  }
+  for (int i = threadIdx.x; i < tile; i += 1024) keys[base + i] = sk[i];
+}
+// one global merge step (stage k, stride j >= tile / 2)
+__global__ __launch_bounds__(1024) void hb_sort_step_kernel(uint64_t* __restrict__ keys, long npad, long k,
+                                                            long j) {
+  for (long q = blockIdx.x * 1024L + threadIdx.x; q < npad / 2; q += (long)gridDim.x * 1024L) {
+    const long i = 2 * j * (q / j) + (q % j);
+    cmp_swap(keys[i], keys[i + j], (i & k) == 0);
+  }
+}
+
+// ---------------------------------------------------------------------------
 // host launchers
 // ---------------------------------------------------------------------------
 hipError_t launch_prep(const double* d_params, int nwalk, const MagArgs& ma, WalkerConst* d_wc,
@@ -1770,6 +1824,28 @@ hipError_t launch_probe(int op, const double* d_in, double* d_out, hipStream_t s
 
 hipError_t launch_partition(double* d_a, int lo, int hi, int* d_res, hipStream_t s) {
   hipLaunchKernelGGL(hb_partition_kernel, dim3(1), dim3(64), 0, s, d_a, lo, hi, d_res);
+  return hipGetLastError();
+}
+
+hipError_t launch_sort(const double* d_in, double* d_out, uint64_t* d_keys, long n, hipStream_t s) {
+  if (n <= 1) {
+    if (n == 1) return hipMemcpyAsync(d_out, d_in, 8, hipMemcpyDeviceToDevice, s);
+    return hipSuccess;
+  }
+  long npad = 1;
+  while (npad < n) npad <<= 1;
+  const int grid = (int)std::min<long>((npad + 1023) / 1024, 4096);
+  hipLaunchKernelGGL(hb_sort_keys_kernel, dim3(grid), dim3(1024), 0, s, d_in, n, npad, d_keys);
+  const int tile = (int)std::min<long>(npad, kSortLds);
+  const int ntile = (int)(npad / tile);
+  // stages up to the tile size entirely in LDS
+  hipLaunchKernelGGL(hb_sort_tile_kernel, dim3(ntile), dim3(1024), 0, s, d_keys, tile, 2L, (long)tile);
+  for (long k = 2L * tile; k <= npad; k <<= 1) {
+    for (long j = k >> 1; j >= tile; j >>= 1)
+      hipLaunchKernelGGL(hb_sort_step_kernel, dim3(grid), dim3(1024), 0, s, d_keys, npad, k, j);
+    hipLaunchKernelGGL(hb_sort_tile_kernel, dim3(ntile), dim3(1024), 0, s, d_keys, tile, k, k);
+  }
+  hipLaunchKernelGGL(hb_sort_vals_kernel, dim3(grid), dim3(1024), 0, s, d_keys, n, d_out);
   return hipGetLastError();
 }
 

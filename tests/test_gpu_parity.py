@@ -386,3 +386,28 @@ def test_write_lc_to_file_bytes(hbmi, tmp_path):
         pv = np.ascontiguousarray(pv)
         hbmi.write_lc_to_file(p(pv), str(path).encode())
         assert path.read_bytes() == g[f"file{k}"].tobytes(), f"fixture {k}"
+
+
+@pytest.mark.parametrize("n", [2, 3, 100, 8191, 8192, 8193, 40000, 200003])
+def test_quicksort_sizes(hbmi, n):
+    """quickSort drop-in (likelihood3.c:70-83) across the bitonic sorter's
+    regimes: one LDS tile (n <= 8192), tiles + global merge steps beyond;
+    with duplicates, +-0.0, +-inf and subnormals.  Same multiset, ascending
+    (np.sort); +-0.0 may trade places as in the reference's comparisons."""
+    rng = np.random.default_rng(n)
+    a = rng.standard_normal(n) * 10.0 ** rng.integers(-300, 300, n)
+    a[rng.integers(0, n, max(1, n // 10))] = 1.5  # duplicates
+    if n > 8:
+        a[:6] = [0.0, -0.0, np.inf, -np.inf, 5e-324, -5e-324]
+        rng.shuffle(a)
+    b = a.copy()
+    hbmi.quickSort(p(b), 0, n - 1)
+    ref = np.sort(a)
+    assert np.array_equal(b, ref)
+    # a sub-range sort leaves the rest untouched
+    c = a.copy()
+    lo, hi = n // 4, n - 1 - n // 4
+    if hi > lo:
+        hbmi.quickSort(p(c), lo, hi)
+        assert np.array_equal(c[lo:hi + 1], np.sort(a[lo:hi + 1]))
+        assert np.array_equal(c[:lo], a[:lo]) and np.array_equal(c[hi + 1:], a[hi + 1:])
