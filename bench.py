@@ -81,6 +81,8 @@ def parse():
     ap.add_argument("--sampler-iters", type=int, default=100,
                     help="also time the whole PT-MCMC iteration (mcmc_wrapper2.c loop) at the workload's W and N: "
                          "device-resident sampler vs the host sampler + GPU likelihood (0 = skip)")
+    ap.add_argument("--dropin-iters", type=int, default=200,
+                    help="iterations of the reference sampler relinked against libhbmi.so (dropin field; 0 = skip)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
                     help="per-launch HBM bytes measured by rocprofv3 --pmc (see profiles/README.md)")
     a = ap.parse_args()
@@ -287,6 +289,50 @@ def sampler_e2e_sharded(L, w, iters, rank, world, warm=20):
             "unit": "walker-steps/s (1 likelihood eval each), all ranks",
             "device_loop_sharded": {"ms_per_iter": dt / iters * 1e3, "value": W * iters / dt,
                                     "exchange_bytes_per_rank_per_iter": 8.0 * exch / (warm + iters)}}
+
+
+def dropin_rate(niter):
+    """The literal north_star drop-in: the reference's OWN sampler
+    (src/mcmc_wrapper2.c, unmodified, 25 OpenMP threads) relinked against
+    libhbmi.so (`make -C oracle dropin` -> oracle/_ref/hb_mcmc_ref_hbmi), so
+    every scalar loglikelihood() call (2 per chain per iteration,
+    mcmc_wrapper2.c:488-489) runs through the likelihood3.h entry point on the
+    GPU.  Timed on TIC 127079833's folded light curve (the trace test's input),
+    next to the same sampler built with likelihood3.c (oracle/_ref/hb_mcmc_ref)
+    on the host cores.  Child processes; nothing here touches HIP."""
+    import subprocess
+    import tempfile
+
+    exe = os.path.join(ROOT, "oracle", "_ref", "hb_mcmc_ref_hbmi")
+    if not os.path.exists(exe):
+        return {"error": "oracle/_ref/hb_mcmc_ref_hbmi not built (make -C oracle dropin)"}
+    from hb_mcmc_amd.hbio import write_folded_lc
+
+    g = np.load(os.path.join(ROOT, "tests", "golden", "sampler_127079833.npz"))
+    out = {"niter": niter, "chains": 50, "light_curve": f"TIC 127079833 folded, N = {len(g['lc_t'])}",
+           "unit": "sampler iterations/s (100 scalar loglikelihood() calls each)"}
+    for key, name in (("dropin", "hb_mcmc_ref_hbmi"), ("reference_cpu", "hb_mcmc_ref")):
+        path = os.path.join(ROOT, "oracle", "_ref", name)
+        if not os.path.exists(path):
+            continue
+        with tempfile.TemporaryDirectory() as tmp:
+            d = os.path.join(tmp, "data", "lightcurves", "folded_lightcurves")
+            os.makedirs(d)
+            write_folded_lc(os.path.join(d, "127079833_new.txt"), g["lc_t"], g["lc_f"], g["lc_e"])
+            for sub in ("subpars", "pars", "chains", "logL", "log", "lightcurves/mcmc_lightcurves"):
+                os.makedirs(os.path.join(tmp, "data", sub), exist_ok=True)
+            os.makedirs(os.path.join(tmp, "debug"))
+            t0 = time.perf_counter()
+            r = subprocess.run([path, str(niter), "127079833", "0.5021", "0"], cwd=tmp, capture_output=True,
+                               text=True, timeout=600, env=dict(os.environ, HBREF_ROOT=tmp))
+            dt = time.perf_counter() - t0
+        if r.returncode != 0:
+            out[key] = {"error": r.stderr[-300:]}
+            continue
+        out[key] = {"iters_per_s": niter / dt, "loglik_calls_per_s": 100.0 * niter / dt, "wall_s": dt}
+    if "iters_per_s" in out.get("dropin", {}) and "iters_per_s" in out.get("reference_cpu", {}):
+        out["speedup_vs_reference_cpu"] = out["dropin"]["iters_per_s"] / out["reference_cpu"]["iters_per_s"]
+    return out
 
 
 def make_event(kind):
@@ -557,6 +603,10 @@ def main():
             line["sampler_end_to_end"] = e2e
         if world == 1 and not a.no_cpu_baseline:
             line["cpu_baseline"] = run_cpu_baseline(n, a.cpu_seconds)
+        if world == 1 and a.dropin_iters > 0:
+            line["dropin"] = dropin_rate(a.dropin_iters)
+            if "iters_per_s" in line["dropin"].get("dropin", {}):
+                line["dropin_iters_per_s"] = line["dropin"]["dropin"]["iters_per_s"]
         print(json.dumps(line), flush=True)
     L.close()
     if world > 1:

@@ -155,6 +155,7 @@ struct hb_ctx {
   double* d_f = nullptr;
   double* d_s = nullptr;          // 1 / max(sigma, 1e-5)
   double2* d_ph = nullptr;        // shared-period phase table, written by every prep launch
+  double* d_rows = nullptr;       // t, f, 1/sigma in lane-row order (hbk::build_rows; one-wave path)
   // per-walker workspace
   int cap = 0;
   WalkerConst* d_wc = nullptr;
@@ -259,6 +260,16 @@ extern "C" hb_ctx* hb_create(const double* t, const double* f, const double* sig
     hb_destroy(c.release());
     return nullptr;
   }
+  if (c->plan.vpt > 0) {
+    std::vector<double> rows((size_t)hbk::wave_rows_doubles(n));
+    hbk::build_rows(t, f, s.data(), n, rows.data());
+    if (hipMalloc(&c->d_rows, sizeof(double) * rows.size()) != hipSuccess ||
+        hipMemcpy(c->d_rows, rows.data(), sizeof(double) * rows.size(), hipMemcpyHostToDevice) != hipSuccess) {
+      set_err_msg("hb_create: lane-row arrays: hipMalloc/upload failed");
+      hb_destroy(c.release());
+      return nullptr;
+    }
+  }
   return c.release();
 }
 
@@ -272,6 +283,7 @@ extern "C" void hb_destroy(hb_ctx* c) {
   if (c->d_f) (void)hipFree(c->d_f);
   if (c->d_s) (void)hipFree(c->d_s);
   if (c->d_ph) (void)hipFree(c->d_ph);
+  if (c->d_rows) (void)hipFree(c->d_rows);
   delete c;
 }
 
@@ -296,7 +308,7 @@ static int run_batch(hb_ctx* c, const double* d_params, int w, double* d_logl, d
   }
   HB_TRY(hbk::launch_prep(d_params, w, c->mags, c->d_wc, s, nullptr, nullptr, c->d_t, c->plan.n, c->d_ph),
          "hb_prep_kernel");
-  HB_TRY(hbk::launch_eval(c->plan, c->d_t, c->d_ph, c->d_f, c->d_s, c->d_wc, w, d_logl, d_tmpl, c->d_scratch,
+  HB_TRY(hbk::launch_eval(c->plan, c->d_t, c->d_ph, c->d_f, c->d_s, c->d_rows, c->d_wc, w, d_logl, d_tmpl, c->d_scratch,
                           d_tmpl ? 1 : 0, s, acc),
          "hb_eval_kernel");
   return 0;
@@ -333,7 +345,7 @@ extern "C" int hb_evaluate_dev(hb_ctx* c, int w, double* d_out, int mode, void* 
   if (w > c->cap) return set_err_msg("hb_evaluate_dev: W exceeds the prepared workspace");
   if (mode != 0 && mode != 1) return set_err_msg("hb_evaluate_dev: mode must be 0 or 1");
   HB_TRY(hipSetDevice(c->device), "hipSetDevice");
-  HB_TRY(hbk::launch_eval(c->plan, c->d_t, c->d_ph, c->d_f, c->d_s, c->d_wc, w, mode == 0 ? d_out : nullptr,
+  HB_TRY(hbk::launch_eval(c->plan, c->d_t, c->d_ph, c->d_f, c->d_s, c->d_rows, c->d_wc, w, mode == 0 ? d_out : nullptr,
                           mode == 1 ? d_out : nullptr, c->d_scratch, mode, (hipStream_t)stream),
          "hb_eval_kernel");
   return 0;
@@ -401,6 +413,7 @@ struct hb_catalog {
   double* d_f = nullptr;
   double* d_s = nullptr;         // 1 / max(sigma, 1e-5)
   double2* d_ph = nullptr;       // per-target phase tables (concatenated like d_t)
+  double* d_rows = nullptr;      // per-target lane-row t, f, 1/sigma (TargetDesc::roff)
   int* d_w0 = nullptr;           // first walker of each target in the current layout, -1 if none
   hbk::TargetDesc* d_tab = nullptr;
   // walker layout cache (walkers per target as last seen)
@@ -424,7 +437,8 @@ struct hb_catalog {
 extern "C" void hb_catalog_destroy(hb_catalog* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
-  for (void* p : {(void*)c->d_t, (void*)c->d_f, (void*)c->d_s, (void*)c->d_ph, (void*)c->d_w0, (void*)c->d_tab,
+  for (void* p : {(void*)c->d_t, (void*)c->d_f, (void*)c->d_s, (void*)c->d_ph, (void*)c->d_rows, (void*)c->d_w0,
+                  (void*)c->d_tab,
                   (void*)c->d_wt, (void*)c->d_list,
                   (void*)c->d_wc, (void*)c->d_params, (void*)c->d_out})
     if (p) (void)hipFree(p);
@@ -457,7 +471,7 @@ extern "C" hb_catalog* hb_catalog_create(int ntargets, const double* const* t, c
   c->ntargets = ntargets;
   c->tab.resize(ntargets);
   c->cls.resize(ntargets);
-  long total = 0;
+  long total = 0, rtotal = 0;
   for (int k = 0; k < ntargets; ++k) {
     if (n[k] < 2 || n[k] > 64 * 32 || !t[k] || !f[k] || !sigma[k]) {
       set_err_msg("hb_catalog_create: target " + std::to_string(k) +
@@ -467,6 +481,8 @@ extern "C" hb_catalog* hb_catalog_create(int ntargets, const double* const* t, c
     hbk::TargetDesc& d = c->tab[k];
     memset(&d, 0, sizeof d);
     d.off = total;
+    d.roff = rtotal;
+    rtotal += hbk::wave_rows_doubles(n[k]);
     d.n = n[k];
     d.kth = (n[k] % 2 == 0) ? n[k] / 2 : n[k] / 2 + 1;  // likelihood3.c:97-99
     d.dist = mag5 ? mag5[5 * k + 0] : 1000.;             // mcmc_wrapper2.c:321-327 fallback
@@ -486,8 +502,18 @@ extern "C" hb_catalog* hb_catalog_create(int ntargets, const double* const* t, c
       hs[o + i] = 1.0 / sg;
     }
   }
+  std::vector<double> hr((size_t)rtotal);
+  for (int k = 0; k < ntargets; ++k) {
+    const long o = c->tab[k].off;
+    hbk::build_rows(&ht[o], &hf[o], &hs[o], n[k], &hr[(size_t)c->tab[k].roff]);
+  }
   if (hipSetDevice(device) != hipSuccess) { set_err_msg("hb_catalog_create: hipSetDevice failed"); return nullptr; }
   const size_t b = sizeof(double) * (size_t)total;
+  if (hipMalloc(&c->d_rows, sizeof(double) * hr.size()) != hipSuccess ||
+      hipMemcpy(c->d_rows, hr.data(), sizeof(double) * hr.size(), hipMemcpyHostToDevice) != hipSuccess) {
+    set_err_msg("hb_catalog_create: lane-row arrays: hipMalloc/upload failed");
+    return nullptr;
+  }
   if (hipMalloc(&c->d_t, b) != hipSuccess || hipMalloc(&c->d_f, b) != hipSuccess ||
       hipMalloc(&c->d_s, b) != hipSuccess || hipMalloc(&c->d_ph, 2 * b) != hipSuccess ||
       hipMalloc(&c->d_w0, sizeof(int) * ntargets) != hipSuccess ||
@@ -603,7 +629,7 @@ static int catalog_run(hb_catalog* c, const double* d_params, double* d_logl, hi
     int vpt = 1;
     while (vpt < kCatRcHi[cl]) vpt <<= 1;
     hipStream_t sj = (j % ns == 0) ? s : c->aux[j % ns - 1];
-    HB_TRY(hbk::launch_eval_multi(vpt, c->class_slab[cl], c->d_t, c->d_ph, c->d_f, c->d_s, c->d_tab, c->d_wt,
+    HB_TRY(hbk::launch_eval_multi(vpt, c->class_slab[cl], c->d_t, c->d_ph, c->d_f, c->d_s, c->d_rows, c->d_tab, c->d_wt,
                                   c->d_list + c->class_off[cl], cnt, c->d_wc, d_logl, sj),
            "eval launch");
   }

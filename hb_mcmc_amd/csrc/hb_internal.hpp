@@ -50,7 +50,7 @@ struct alignas(16) TargetDesc {
   long off;      // first cadence in the concatenated arrays
   long n;        // cadences (2..2048 in the batched path)
   long kth;      // 0-based median rank (likelihood3.c:97-99)
-  long pad0;
+  long roff;     // first double of the target's lane-row arrays (build_rows)
   double dist;   // mag_data[0] [pc]
   double gmag;   // mag_data[1]
   double gerr;   // magerr[0]
@@ -94,17 +94,20 @@ hipError_t launch_prep(const double* d_params, int nwalk, const MagArgs& ma, hbd
 // catalog mode: walkers list[0..count) of one size class (cadences per lane
 // vpt), each reading its target's slice through tab[wt[walker]]
 hipError_t launch_eval_multi(int vpt, size_t slab_bytes, const double* t, const double2* ph, const double* f,
-                             const double* sg,
+                             const double* sg, const double* rows,
                              const TargetDesc* tab, const int* wt, const int* list, int count,
                              const hbdev::WalkerConst* wc, double* logl, hipStream_t s);
 int wave_vpt_for(long n);  // cadences per lane of the one-wave path, 0 if n > 2048
 size_t wave_slab_bytes(long n);
 size_t wave_lds_bytes(size_t slab, int vpt);
+// t, f, 1/sigma in the one-wave kernel's lane-row order (3 x 64 x ceil(n/64) doubles)
+long wave_rows_doubles(long n);
+void build_rows(const double* t, const double* f, const double* isg, long n, double* out);
 // acc (device sampler, one-wave path only): each wave also runs its slot's
 // Hastings test and history write (hb_accept.hpp); hipErrorNotSupported on the
 // multi-wave path
 hipError_t launch_eval(const EvalPlan& pl, const double* t, const double2* ph, const double* f, const double* sg,
-                       const hbdev::WalkerConst* wc, int nwalk, double* logl, double* tmpl,
+                       const double* rows, const hbdev::WalkerConst* wc, int nwalk, double* logl, double* tmpl,
                        double* scratch, int mode, hipStream_t s, const hbds::AccArgs* acc = nullptr);
 hipError_t launch_traj(const double* d_times, int nt, const TrajArgs& ta, double* d, double* z1,
                        double* z2, double* rr, double* ff, hipStream_t s);

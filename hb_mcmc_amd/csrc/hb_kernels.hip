@@ -54,6 +54,36 @@ using namespace hbdev;
 #ifndef HB_ABLATE_SELECT
 #define HB_ABLATE_SELECT 0
 #endif
+#ifndef HB_PRIO
+#define HB_PRIO 1  // wave pacing (Pacer): 0 off, 1 by own quartile, 2 by lead over the SIMD's slowest wave
+#endif
+// LDS ordering among the lanes of ONE wave (the one-wave-per-walker kernel may
+// share its workgroup with other walkers' waves, which must not be waited for)
+#define HB_WSYNC()                                        \
+  do {                                                    \
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront"); \
+    __builtin_amdgcn_wave_barrier();                      \
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront"); \
+  } while (0)
+// Experiment builds only (HB_WAVE_CLOCKS): per-wave shader clock at entry and
+// exit plus HW_ID / XCC_ID, read back by hb_debug_wave_clocks().
+#ifdef HB_WAVE_CLOCKS
+__device__ unsigned long long hb_wave_clk[4 * 65536];
+#define HB_CLK_BEGIN() const unsigned long long clk0_ = __builtin_amdgcn_s_memtime()
+#define HB_CLK_END(wv)                                                                  \
+  do {                                                                                  \
+    const unsigned long long clk1_ = __builtin_amdgcn_s_memtime();                      \
+    if ((threadIdx.x & 63) == 0 && (wv) < 65536) {                                      \
+      hb_wave_clk[4 * (wv) + 0] = clk0_;                                                \
+      hb_wave_clk[4 * (wv) + 1] = clk1_;                                                \
+      hb_wave_clk[4 * (wv) + 2] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);  \
+      hb_wave_clk[4 * (wv) + 3] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 20); \
+    }                                                                                   \
+  } while (0)
+#else
+#define HB_CLK_BEGIN() do { } while (0)
+#define HB_CLK_END(wv) do { } while (0)
+#endif
 
 namespace hbk {
 
@@ -573,6 +603,56 @@ __device__ __forceinline__ bool chain_eligible(const WalkerConst& w, double gap)
   return (e <= kWarmEmax) && (e * dm * dm <= 2.0 * HB_WARM_D1 * ome * ome * ome);
 }
 
+// Wave pacing.  The waves sharing a SIMD are issued by priority, then age:
+// with equal priorities the oldest wave runs nearly unimpeded and finishes
+// first, and the youngest runs its last stretch alone, latency-bound
+// (scripts/wave_clocks.py: finish times 46k/69k/89k/107k cycles for the four
+// waves of a SIMD at C2).  A Pacer lowers a wave's priority as it gets ahead:
+//   HB_PRIO == 1: by quartile of its own model pass (3 -> 0);
+//   HB_PRIO == 2: by its lead over the slowest wave of its workgroup on the
+//                 same SIMD (progress words in LDS, multi-walker workgroups).
+struct Pacer {
+  uint32_t* prog;  // WPB progress words (simd << 16 | progress/16), nullptr: none
+  uint32_t tag;    // this wave's simd << 16
+  int wib;         // wave in block
+  int wpb;         // waves per block
+  int lane;
+  uint32_t inc;    // (16 << 8) / steps
+  __device__ __forceinline__ void begin(int steps) {
+    inc = (16u << 8) / (uint32_t)(steps > 0 ? steps : 1);
+  }
+  __device__ __forceinline__ void step(int j, int n) const {
+#if HB_PRIO == 1
+    if (4 * j == n || 4 * j == n + 1 || 4 * j == n + 2 || 4 * j == n + 3) __builtin_amdgcn_s_setprio(2);
+    if (2 * j == n || 2 * j == n + 1) __builtin_amdgcn_s_setprio(1);
+    if (4 * j == 3 * n || 4 * j == 3 * n + 1 || 4 * j == 3 * n + 2 || 4 * j == 3 * n + 3)
+      __builtin_amdgcn_s_setprio(0);
+#elif HB_PRIO == 2
+    (void)n;
+    if (prog == nullptr) return;
+    const uint32_t p = ((uint32_t)j * inc) >> 8;
+    if (lane == 0) prog[wib] = tag | p;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const uint32_t v = lane < wpb ? prog[lane] : 0xffffffffu;
+    uint32_t q = ((v & 0xffff0000u) == tag) ? (v & 0xffffu) : 0xffffu;
+    q = min(q, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)q, 0xB1, 0xf, 0xf, false));
+    q = min(q, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)q, 0x4E, 0xf, 0xf, false));
+    q = min(q, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)q, 0x141, 0xf, 0xf, false));
+    q = min(q, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)q, 0x140, 0xf, 0xf, false));
+    const uint32_t lead = p - (uint32_t)__builtin_amdgcn_readfirstlane((int)q);  // row 0 holds the min
+    if (lead == 0) __builtin_amdgcn_s_setprio(3);
+    else if (lead <= 2) __builtin_amdgcn_s_setprio(2);
+    else if (lead <= 4) __builtin_amdgcn_s_setprio(1);
+    else __builtin_amdgcn_s_setprio(0);
+#else
+    (void)j;
+    (void)n;
+#endif
+  }
+};
+
 // Cold path in the one-wave kernel: the wave sweeps the light curve 64*K
 // consecutive cadences at a time (cadence base + k*64 + lane), so the eclipse
 // lanes of an iteration are neighbours in phase and the inline eclipse term
@@ -580,11 +660,14 @@ __device__ __forceinline__ bool chain_eligible(const WalkerConst& w, double gap)
 // at the lane-row slab positions (slab_pos_of) that the key load reads.
 __device__ __forceinline__ void model_pass_cold(const double* __restrict__ t, const double2* __restrict__ ph,
                                                 int n, const Rows& rw, const WalkerConst& w, double* vals,
-                                                int lane) {
+                                                int lane, Pacer pc) {
   constexpr int K = HB_K;
   const bool tab = (ph != nullptr) && (w.tab != 0.0);  // walker-uniform
   const int last = n - 1;
-  for (int base = 0; base < n; base += K * 64) {
+  const int nit = (n + K * 64 - 1) / (K * 64);
+  pc.begin(nit);
+  for (int base = 0, it = 0; base < n; base += K * 64, ++it) {
+    pc.step(it, nit);
     double tk[K], v[K];
     double2 pk[K];
 #pragma unroll
@@ -612,10 +695,13 @@ __device__ __forceinline__ void model_pass_cold(const double* __restrict__ t, co
   }
 }
 
+// tT: the light curve's times in lane-row order (tT[c * 64 + l] = t[l * rc + c],
+// build_rows), so the step-c loads of the 64 lanes are one coalesced 512-B
+// request instead of 64 strided ones
 template <int VPT>
-__device__ __forceinline__ void model_pass_chain(const double* __restrict__ t, const double2* __restrict__ ph,
+__device__ __forceinline__ void model_pass_chain(const double* __restrict__ tT, const double2* __restrict__ ph,
                                                  int n, const Rows& rw, const WalkerConst& w, double* vals,
-                                                 double* eq_dr, int* eq_code, int lane) {
+                                                 double* eq_dr, int* eq_code, int lane, Pacer pc) {
   constexpr int KC = VPT < HB_KC ? VPT : HB_KC;
   const int lc = (rw.rc + KC - 1) / KC;  // chain length (wave-uniform)
   const bool tab = (ph != nullptr) && (w.tab != 0.0);  // walker-uniform
@@ -626,16 +712,40 @@ __device__ __forceinline__ void model_pass_chain(const double* __restrict__ t, c
   ChainState<KC> st;
   double tk[KC];
 #pragma unroll
-  for (int k = 0; k < KC; ++k) tk[k] = t[min(base + k * lc, last)];
+  for (int k = 0; k < KC; ++k) tk[k] = tT[min(k * lc, rw.rc - 1) * 64 + lane];
+  pc.begin(lc);
   for (int j = 0; j < lc; ++j) {
+    pc.step(j, lc);
+#if defined(HB_PAD_V) || defined(HB_PAD_S)  // experiment builds only: issue-cost probes
+    {
+      int x = j;
+#ifdef HB_PAD_V
+#pragma unroll
+      for (int q = 0; q < HB_PAD_V; ++q) __asm__ volatile("v_add_u32 %0, 1, %0" : "+v"(x));
+#endif
+#ifdef HB_PAD_S
+#pragma unroll
+      for (int q = 0; q < HB_PAD_S; ++q) __asm__ volatile("s_add_u32 %0, %0, 1" : "+s"(x) :: "scc");
+#endif
+    }
+#endif
     double tn[KC];
 #pragma unroll
-    for (int k = 0; k < KC; ++k) tn[k] = t[min(base + k * lc + j + 1, last)];
+    for (int k = 0; k < KC; ++k) tn[k] = tT[min(k * lc + j + 1, rw.rc - 1) * 64 + lane];
     double v[KC], dd[KC], zz[KC];
     bool bad;
 #if HB_SPLIT_LIVE
     __asm__ volatile("" ::: "memory");
 #endif
+#if HB_ABLATE_MODEL  // experiment builds only: trivial model, same data flow
+#pragma unroll
+    for (int k = 0; k < KC; ++k) {
+      v[k] = tk[k] * w.kb + w.kr0;
+      dd[k] = 1.0;
+      zz[k] = 0.0;
+    }
+    bad = false;
+#else
     if (j == 0) {  // the chains' first cadences: the reference's start (table entries)
       double2 p0[KC];
 #pragma unroll
@@ -645,6 +755,7 @@ __device__ __forceinline__ void model_pass_chain(const double* __restrict__ t, c
       const double2 p0[KC] = {};
       hb_cadence_flux_chain<KC>(tk, p0, false, false, w, st, v, dd, zz, bad);
     }
+#endif
     if (__any(bad)) {  // out-of-domain angles: reference-order ocml path (eclipse included)
       if (bad) {
 #pragma unroll
@@ -1094,24 +1205,24 @@ __device__ __forceinline__ void select_pass(const uint64_t (&key)[VPT], uint32_t
   uint4* h4 = reinterpret_cast<uint4*>(hist);
 #pragma unroll
   for (int q = 0; q < Q; ++q) h4[lane * Q + q] = make_uint4(0u, 0u, 0u, 0u);
-  __syncthreads();
+  HB_WSYNC();
 #pragma unroll
   for (int v = 0; v < VPT; ++v)
     if ((key[v] & mask) == prefix) atomicAdd(&hist[(uint32_t)(key[v] >> shift) & dm], 1u);
-  __syncthreads();
+  HB_WSYNC();
   uint32_t bin, before;
   wave_pick_bin<B>(hist, lane, kk, bin, before, cnt);
   kk -= before;
   prefix |= (uint64_t)bin << shift;
   mask |= (uint64_t)dm << shift;
   hi = shift - 1;
-  __syncthreads();  // histogram reads done before the next clear
+  HB_WSYNC();  // histogram reads done before the next clear
 }
 
 template <int VPT>
 __device__ __forceinline__ double wave_select2(const uint64_t (&key)[VPT], uint32_t kth, uint64_t kmin,
                                                uint64_t kmax, uint32_t* hist, uint64_t* cand) {
-  const int lane = threadIdx.x;
+  const int lane = threadIdx.x & 63;
   if (kmin == kmax) return dval(kmin);
   int hi = 63 - __builtin_clzll(kmin ^ kmax);
   uint64_t mask = (hi == 63) ? 0ull : ~((2ull << hi) - 1ull);
@@ -1129,7 +1240,7 @@ __device__ __forceinline__ double wave_select2(const uint64_t (&key)[VPT], uint3
     if (m) cand[basec + __popcll(bal & ((1ull << lane) - 1ull))] = key[v];
     basec += (uint32_t)__popcll(bal);
   }
-  __syncthreads();
+  HB_WSYNC();
   const uint64_t mine = (uint32_t)lane < cnt ? cand[lane] : ~0ull;
   uint32_t r = 0;
   for (uint32_t j = 0; j < cnt; ++j) {
@@ -1150,9 +1261,6 @@ __device__ __forceinline__ double wave_select2(const uint64_t (&key)[VPT], uint3
 #ifndef HB_BLOCK_KEYS
 #define HB_BLOCK_KEYS 1  // 0: N > 2048 uses the LDS-walking block select (previous version)
 #endif
-#ifndef HB_PF
-#define HB_PF 0  // 1: request the chi^2 operands before the select (costs VGPR spills)
-#endif
 // Key slot v of `lane` holds cadence lane*rc + v (its own row; v >= rc is
 // padding).  A light curve is smooth, so 64 consecutive cadences mostly share
 // one histogram bin and a wave's LDS atomic would serialise on one address;
@@ -1168,49 +1276,85 @@ __device__ __forceinline__ bool key_live(const Rows& r, int v, int lane, long n)
 // ACC (device sampler): the wave then runs the Hastings test and history write
 // of its slot (hb_accept.hpp) on the logL it just computed, in place of a
 // separate ds_accept launch.
-template <int VPT, bool MULTI, bool ACC = false>
-__global__ __launch_bounds__(64) HB_WPE_ATTR void hb_eval_wave_kernel(
+// WPB > 1: WPB walkers (one wave each) per workgroup; a wave's LDS is its
+// lds_per-byte slice.  The waves only meet at the progress-word barrier of
+// the pacer (HB_PRIO == 2); everything else syncs per wave (HB_WSYNC).
+template <int VPT, bool MULTI, bool ACC = false, int WPB = 1>
+__global__ __launch_bounds__(64 * WPB) HB_WPE_ATTR void hb_eval_wave_kernel(
     const double* __restrict__ t, const double2* __restrict__ ph, const double* __restrict__ f,
-    const double* __restrict__ isg,
+    const double* __restrict__ isg, const double* __restrict__ rows,
     long n, long kth, const WalkerConst* __restrict__ wcs, double* __restrict__ logl,
     double* __restrict__ tmpl_out, int mode, int slab_bytes, double gap, const TargetDesc* __restrict__ tab,
-    const int* __restrict__ wt, const int* __restrict__ list, hbds::AccArgs hst) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int lane = threadIdx.x;
-  int wv = blockIdx.x;
-  if (MULTI) {
-    wv = list[blockIdx.x];
+    const int* __restrict__ wt, const int* __restrict__ list, hbds::AccArgs hst, int count, int lds_per) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_all[];
+  const int lane = threadIdx.x & 63;
+  const int wib = WPB > 1 ? __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) : 0;
+  const int slot = (int)blockIdx.x * WPB + wib;
+  const bool valid = WPB == 1 || slot < count;
+  unsigned char* smem = smem_all + (size_t)wib * (size_t)lds_per;
+  int wv = slot;
+  if (MULTI && valid) {
+    wv = list[slot];
     const TargetDesc& td = tab[wt[wv]];
     t += td.off;
     if (ph) ph += td.off;
     f += td.off;
     isg += td.off;
+    rows += td.roff;
     n = td.n;
     kth = td.kth;
   }
+  HB_CLK_BEGIN();
+#if HB_PRIO
+  __builtin_amdgcn_s_setprio(3);
+#endif
   double* vals = reinterpret_cast<double*>(smem);
   uint32_t* hist = reinterpret_cast<uint32_t*>(smem);
   uint64_t* cand = reinterpret_cast<uint64_t*>(smem + slab_bytes);
-  const WalkerConst& w = wcs[wv];
-  if (mode == 0 && w.roche != 0.0) {  // likelihood3.c:866-869, see hb_eval_kernel
+  const WalkerConst& w = wcs[valid ? wv : 0];
+  const bool roche_exit = mode == 0 && w.roche != 0.0;
+  Pacer pc{nullptr, 0u, wib, WPB, lane, 0u};
+#if HB_PRIO == 2
+  if (WPB > 1) {
+    // progress words: simd << 16 | progress; finished or idle waves report 0xffff
+    uint32_t* prog = reinterpret_cast<uint32_t*>(smem_all + (size_t)WPB * (size_t)lds_per);
+    const uint32_t simd = ((uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 4) >> 4) & 3u;  // HW_ID.simd_id
+    pc.prog = prog;
+    pc.tag = simd << 16;
+    if (lane == 0) prog[wib] = pc.tag | ((valid && !roche_exit) ? 0u : 0xffffu);
+    __syncthreads();  // the workgroup's only barrier
+  }
+#endif
+  if (!valid) return;
+  if (roche_exit) {  // likelihood3.c:866-869, see hb_eval_kernel
     if (lane == 0) logl[wv] = -kBig / 2.0;
     if (ACC) hbds::accept_slot_wave(hst, wv, -kBig / 2.0, lane);
+    HB_CLK_END(wv);
     return;
   }
 
   uint64_t kmn, kmx;
   uint64_t key[VPT];
   const Rows rw = make_rows((int)n);
+  const double* __restrict__ fT = rows + 64 * rw.rc;   // f and 1/sigma in lane-row order
+  const double* __restrict__ iT = rows + 128 * rw.rc;
   {
     if (VPT >= HB_CHAIN_VPT_MIN && VPT <= HB_CHAIN_VPT_MAX && chain_eligible(w, MULTI ? tab[wt[wv]].gap : gap)) {
-      double* eq_dr = reinterpret_cast<double*>(smem + slab_bytes + 8 * kCandMax);
+      // the eclipse queue shares the select's candidate area (dead until the select)
+      double* eq_dr = reinterpret_cast<double*>(smem + slab_bytes);
       int* eq_code = reinterpret_cast<int*>(eq_dr + kEclQ);
-      model_pass_chain<VPT>(t, ph, (int)n, rw, w, vals, eq_dr, eq_code, lane);
+      model_pass_chain<VPT>(rows, ph, (int)n, rw, w, vals, eq_dr, eq_code, lane, pc);
     } else {
-      model_pass_cold(t, ph, (int)n, rw, w, vals, lane);
+      model_pass_cold(t, ph, (int)n, rw, w, vals, lane, pc);
     }
   }
-  __syncthreads();
+#if HB_PRIO == 2
+  if (pc.prog != nullptr) {
+    if (lane == 0) pc.prog[wib] = pc.tag | 0xffffu;  // model pass done: stop holding the others back
+    __builtin_amdgcn_s_setprio(0);
+  }
+#endif
+  HB_WSYNC();
   // keys, and the lane's min/max keys (values ~1; -0.0 / +0.0 take the outer
   // key, NaN lanes fall back to integer key min/max)
   {
@@ -1246,19 +1390,7 @@ __global__ __launch_bounds__(64) HB_WPE_ATTR void hb_eval_wave_kernel(
   kmn = wave_reduce_u64(kmn, OpMinU64());
   kmx = wave_reduce_u64(kmx, OpMaxU64());
 #endif
-  // chi^2 operands requested now so that their L2 latency overlaps the
-  // median select (VPT <= 16: 4*VPT more VGPRs while the keys are live)
-  constexpr int PF = (HB_PF && VPT <= 16) ? VPT : 1;
-  double fv[PF], iv[PF];
-  if (HB_PF && VPT <= 16 && mode == 0) {
-#pragma unroll
-    for (int v = 0; v < PF; ++v) {
-      const int i = min(key_index(rw, v, lane), (int)n - 1);
-      fv[v] = f[i];
-      iv[v] = isg[i];
-    }
-  }
-  __syncthreads();  // the slab becomes the histogram
+  HB_WSYNC();  // the slab becomes the histogram
 #if HB_ABLATE_SELECT
   const double med = dval(kmn);
 #else
@@ -1280,16 +1412,16 @@ __global__ __launch_bounds__(64) HB_WPE_ATTR void hb_eval_wave_kernel(
         o[i] = (blend + m * one_m_blend) * tune;
       }
     }
+    HB_CLK_END(wv);
     return;
   }
   double acc = 0.0;
 #pragma unroll
   for (int v = 0; v < VPT; ++v) {
-    const int i = key_index(rw, v, lane);
     if (key_live(rw, v, lane, n)) {
       double m = (dval(key[v]) - med) + 1.0;
       m = (blend + m * one_m_blend) * tune;
-      const double r = (HB_PF && VPT <= 16) ? (m - fv[v < PF ? v : 0]) * iv[v < PF ? v : 0] : (m - f[i]) * isg[i];
+      const double r = (m - fT[v * 64 + lane]) * iT[v * 64 + lane];  // lane-row order: coalesced
       acc += r * r;
     }
   }
@@ -1308,6 +1440,7 @@ __global__ __launch_bounds__(64) HB_WPE_ATTR void hb_eval_wave_kernel(
     if (w.roche != 0.0) c = kBig;
     hbds::accept_slot_wave(hst, wv, __shfl(-c / 2.0, 0), lane);
   }
+  HB_CLK_END(wv);
 }
 
 // ---------------------------------------------------------------------------
@@ -1712,77 +1845,128 @@ static hipError_t launch_eval_t(const EvalPlan& pl, const double* t, const doubl
   return hipGetLastError();
 }
 
+// Walkers per workgroup of the one-wave kernel: 16 fills a CU (4 waves per
+// SIMD) with one workgroup, so the pacer (HB_PRIO == 2) sees every wave of a
+// SIMD; fewer when the batch would leave CUs idle or the LDS does not fit.
+#ifndef HB_WPB_MAX
+#define HB_WPB_MAX 1
+#endif
+constexpr size_t kLdsCap = 163840;
+int wave_wpb(int count, size_t lds_per) {
+  int wpb = HB_WPB_MAX;
+  while (wpb > 1 && ((long)count < 256L * wpb || (size_t)wpb * lds_per + 64 > kLdsCap)) wpb >>= 2;
+  return wpb < 1 ? 1 : wpb;
+}
+
+template <int VPT, bool MULTI, bool ACC, int WPB>
+static hipError_t launch_wave_g(size_t lds_per, int count, hipStream_t s, const double* t, const double2* ph,
+                                const double* f, const double* sg, const double* rows, long n, long kth, const WalkerConst* wc,
+                                double* logl, double* tmpl, int mode, size_t slab, double gap,
+                                const TargetDesc* tab, const int* wt, const int* list,
+                                const hbds::AccArgs& acc) {
+  auto kern = hb_eval_wave_kernel<VPT, MULTI, ACC, WPB>;
+  const size_t lds = (size_t)WPB * lds_per + (WPB > 1 ? 64 : 0);
+  static bool attr_set = false;  // per instantiation; benign race (idempotent)
+  if (!attr_set && lds > 65536) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsCap);
+    if (e != hipSuccess) return e;
+    attr_set = true;
+  }
+  hipLaunchKernelGGL(kern, dim3((count + WPB - 1) / WPB), dim3(64 * WPB), lds, s, t, ph, f, sg, rows, n, kth, wc, logl,
+                     tmpl, mode, (int)slab, gap, tab, wt, list, acc, count, (int)lds_per);
+  return hipGetLastError();
+}
+
+template <int VPT, bool MULTI, bool ACC>
+static hipError_t launch_wave_w(size_t slab, int count, hipStream_t s, const double* t, const double2* ph,
+                                const double* f, const double* sg, const double* rows, long n, long kth, const WalkerConst* wc,
+                                double* logl, double* tmpl, int mode, double gap, const TargetDesc* tab,
+                                const int* wt, const int* list, const hbds::AccArgs& acc) {
+  const size_t per = wave_lds_bytes(slab, VPT);
+  switch (wave_wpb(count, per)) {
+#if HB_WPB_MAX >= 16
+    case 16:
+      return launch_wave_g<VPT, MULTI, ACC, 16>(per, count, s, t, ph, f, sg, rows, n, kth, wc, logl, tmpl, mode, slab,
+                                                gap, tab, wt, list, acc);
+#endif
+#if HB_WPB_MAX >= 4
+    case 4:
+      return launch_wave_g<VPT, MULTI, ACC, 4>(per, count, s, t, ph, f, sg, rows, n, kth, wc, logl, tmpl, mode, slab,
+                                               gap, tab, wt, list, acc);
+#endif
+    default:
+      return launch_wave_g<VPT, MULTI, ACC, 1>(per, count, s, t, ph, f, sg, rows, n, kth, wc, logl, tmpl, mode, slab,
+                                               gap, tab, wt, list, acc);
+  }
+}
+
 template <int VPT>
 static hipError_t launch_wave_t(const EvalPlan& pl, const double* t, const double2* ph, const double* f,
-                                const double* sg,
+                                const double* sg, const double* rows,
                                 const WalkerConst* wc, int nwalk, double* logl, double* tmpl, int mode,
                                 hipStream_t s) {
-  hipLaunchKernelGGL((hb_eval_wave_kernel<VPT, false>), dim3(nwalk), dim3(64), pl.lds_bytes, s, t, ph, f, sg,
-                     pl.n, pl.kth, wc, logl, tmpl, mode, (int)pl.slab_bytes, pl.gap, nullptr, nullptr, nullptr,
-                     hbds::AccArgs{});
-  return hipGetLastError();
+  return launch_wave_w<VPT, false, false>(pl.slab_bytes, nwalk, s, t, ph, f, sg, rows, pl.n, pl.kth, wc, logl, tmpl,
+                                          mode, pl.gap, nullptr, nullptr, nullptr, hbds::AccArgs{});
 }
 
 template <int VPT>
 static hipError_t launch_wave_acc_t(const EvalPlan& pl, const double* t, const double2* ph, const double* f,
-                                    const double* sg, const WalkerConst* wc, int nwalk, double* logl,
-                                    hipStream_t s, const hbds::AccArgs& acc) {
-  hipLaunchKernelGGL((hb_eval_wave_kernel<VPT, false, true>), dim3(nwalk), dim3(64), pl.lds_bytes, s, t, ph, f,
-                     sg, pl.n, pl.kth, wc, logl, nullptr, 0, (int)pl.slab_bytes, pl.gap, nullptr, nullptr, nullptr, acc);
-  return hipGetLastError();
+                                    const double* sg, const double* rows, const WalkerConst* wc, int nwalk,
+                                    double* logl, hipStream_t s, const hbds::AccArgs& acc) {
+  return launch_wave_w<VPT, false, true>(pl.slab_bytes, nwalk, s, t, ph, f, sg, rows, pl.n, pl.kth, wc, logl, nullptr,
+                                         0, pl.gap, nullptr, nullptr, nullptr, acc);
 }
 
 template <int VPT>
 static hipError_t launch_multi_t(size_t slab, const double* t, const double2* ph, const double* f,
-                                 const double* sg,
+                                 const double* sg, const double* rows,
                                  const TargetDesc* tab, const int* wt, const int* list, int count,
                                  const WalkerConst* wc, double* logl, hipStream_t s) {
-  const size_t lds = wave_lds_bytes(slab, VPT);
-  hipLaunchKernelGGL((hb_eval_wave_kernel<VPT, true>), dim3(count), dim3(64), lds, s, t, ph, f, sg, 0L, 0L,
-                     wc, logl, nullptr, 0, (int)slab, 0.0, tab, wt, list, hbds::AccArgs{});
-  return hipGetLastError();
+  return launch_wave_w<VPT, true, false>(slab, count, s, t, ph, f, sg, rows, 0L, 0L, wc, logl, nullptr, 0, 0.0, tab, wt,
+                                         list, hbds::AccArgs{});
 }
 
 hipError_t launch_eval_multi(int vpt, size_t slab, const double* t, const double2* ph, const double* f,
-                             const double* sg,
+                             const double* sg, const double* rows,
                              const TargetDesc* tab, const int* wt, const int* list, int count,
                              const WalkerConst* wc, double* logl, hipStream_t s) {
   if (count <= 0) return hipSuccess;
   switch (vpt) {
-    case 1: return launch_multi_t<1>(slab, t, ph, f, sg, tab, wt, list, count, wc, logl, s);
-    case 2: return launch_multi_t<2>(slab, t, ph, f, sg, tab, wt, list, count, wc, logl, s);
-    case 4: return launch_multi_t<4>(slab, t, ph, f, sg, tab, wt, list, count, wc, logl, s);
-    case 8: return launch_multi_t<8>(slab, t, ph, f, sg, tab, wt, list, count, wc, logl, s);
-    case 16: return launch_multi_t<16>(slab, t, ph, f, sg, tab, wt, list, count, wc, logl, s);
-    case 32: return launch_multi_t<32>(slab, t, ph, f, sg, tab, wt, list, count, wc, logl, s);
+    case 1: return launch_multi_t<1>(slab, t, ph, f, sg, rows, tab, wt, list, count, wc, logl, s);
+    case 2: return launch_multi_t<2>(slab, t, ph, f, sg, rows, tab, wt, list, count, wc, logl, s);
+    case 4: return launch_multi_t<4>(slab, t, ph, f, sg, rows, tab, wt, list, count, wc, logl, s);
+    case 8: return launch_multi_t<8>(slab, t, ph, f, sg, rows, tab, wt, list, count, wc, logl, s);
+    case 16: return launch_multi_t<16>(slab, t, ph, f, sg, rows, tab, wt, list, count, wc, logl, s);
+    case 32: return launch_multi_t<32>(slab, t, ph, f, sg, rows, tab, wt, list, count, wc, logl, s);
     default: return hipErrorInvalidValue;
   }
 }
 
 hipError_t launch_eval(const EvalPlan& pl, const double* t, const double2* ph, const double* f, const double* sg,
-                       const WalkerConst* wc, int nwalk, double* logl, double* tmpl, double* scratch,
+                       const double* rows, const WalkerConst* wc, int nwalk, double* logl, double* tmpl, double* scratch,
                        int mode, hipStream_t s, const hbds::AccArgs* acc) {
   if (nwalk <= 0) return hipSuccess;
   if (acc != nullptr) {  // fused Hastings epilogue: one-wave path only
     if (mode != 0) return hipErrorInvalidValue;
     switch (pl.vpt) {
-      case 1: return launch_wave_acc_t<1>(pl, t, ph, f, sg, wc, nwalk, logl, s, *acc);
-      case 2: return launch_wave_acc_t<2>(pl, t, ph, f, sg, wc, nwalk, logl, s, *acc);
-      case 4: return launch_wave_acc_t<4>(pl, t, ph, f, sg, wc, nwalk, logl, s, *acc);
-      case 8: return launch_wave_acc_t<8>(pl, t, ph, f, sg, wc, nwalk, logl, s, *acc);
-      case 16: return launch_wave_acc_t<16>(pl, t, ph, f, sg, wc, nwalk, logl, s, *acc);
-      case 32: return launch_wave_acc_t<32>(pl, t, ph, f, sg, wc, nwalk, logl, s, *acc);
+      case 1: return launch_wave_acc_t<1>(pl, t, ph, f, sg, rows, wc, nwalk, logl, s, *acc);
+      case 2: return launch_wave_acc_t<2>(pl, t, ph, f, sg, rows, wc, nwalk, logl, s, *acc);
+      case 4: return launch_wave_acc_t<4>(pl, t, ph, f, sg, rows, wc, nwalk, logl, s, *acc);
+      case 8: return launch_wave_acc_t<8>(pl, t, ph, f, sg, rows, wc, nwalk, logl, s, *acc);
+      case 16: return launch_wave_acc_t<16>(pl, t, ph, f, sg, rows, wc, nwalk, logl, s, *acc);
+      case 32: return launch_wave_acc_t<32>(pl, t, ph, f, sg, rows, wc, nwalk, logl, s, *acc);
       default: return hipErrorNotSupported;
     }
   }
   switch (pl.vpt) {
     case 0: break;
-    case 1: return launch_wave_t<1>(pl, t, ph, f, sg, wc, nwalk, logl, tmpl, mode, s);
-    case 2: return launch_wave_t<2>(pl, t, ph, f, sg, wc, nwalk, logl, tmpl, mode, s);
-    case 4: return launch_wave_t<4>(pl, t, ph, f, sg, wc, nwalk, logl, tmpl, mode, s);
-    case 8: return launch_wave_t<8>(pl, t, ph, f, sg, wc, nwalk, logl, tmpl, mode, s);
-    case 16: return launch_wave_t<16>(pl, t, ph, f, sg, wc, nwalk, logl, tmpl, mode, s);
-    case 32: return launch_wave_t<32>(pl, t, ph, f, sg, wc, nwalk, logl, tmpl, mode, s);
+    case 1: return launch_wave_t<1>(pl, t, ph, f, sg, rows, wc, nwalk, logl, tmpl, mode, s);
+    case 2: return launch_wave_t<2>(pl, t, ph, f, sg, rows, wc, nwalk, logl, tmpl, mode, s);
+    case 4: return launch_wave_t<4>(pl, t, ph, f, sg, rows, wc, nwalk, logl, tmpl, mode, s);
+    case 8: return launch_wave_t<8>(pl, t, ph, f, sg, rows, wc, nwalk, logl, tmpl, mode, s);
+    case 16: return launch_wave_t<16>(pl, t, ph, f, sg, rows, wc, nwalk, logl, tmpl, mode, s);
+    case 32: return launch_wave_t<32>(pl, t, ph, f, sg, rows, wc, nwalk, logl, tmpl, mode, s);
     default: return hipErrorInvalidValue;
   }
   if (pl.bvpt > 0) {
@@ -1878,7 +2062,23 @@ size_t wave_slab_bytes(long n) {
 // slab | select candidates | eclipse queue (chain model pass only)
 size_t wave_lds_bytes(size_t slab, int vpt) {
   const bool chain = vpt >= HB_CHAIN_VPT_MIN && vpt <= HB_CHAIN_VPT_MAX;
-  return slab + 8 * kCandMax + (chain ? (size_t)kEclQ * (8 + 4) : 0);
+  const size_t q = chain ? (size_t)kEclQ * (8 + 4) : 0;  // eclipse queue aliases the candidates
+  return (slab + (q > 8 * kCandMax ? q : 8 * kCandMax) + 15) & ~(size_t)15;
+}
+
+// t, f and 1/sigma in the one-wave kernel's lane-row order: row block c holds
+// cadence l * rc + c for lanes l = 0..63 (rc = ceil(n / 64); cadences past the
+// end repeat the last one and are never used)
+long wave_rows_doubles(long n) { return 3L * 64L * ((n + 63) / 64); }
+void build_rows(const double* t, const double* f, const double* isg, long n, double* out) {
+  const long rc = (n + 63) / 64;
+  for (long c = 0; c < rc; ++c)
+    for (long l = 0; l < 64; ++l) {
+      const long i = std::min(l * rc + c, n - 1);
+      out[c * 64 + l] = t[i];
+      out[64 * rc + c * 64 + l] = f[i];
+      out[128 * rc + c * 64 + l] = isg[i];
+    }
 }
 
 double cadence_gap(const double* t, long n) {
@@ -1935,6 +2135,14 @@ extern "C" int hb_dbg_chain_stats(unsigned long long* out, int reset) {
     unsigned long long z[8] = {0};
     e = hipMemcpyToSymbol(HIP_SYMBOL(hbdev::hb_chain_stats), z, sizeof z);
   }
+  return e == hipSuccess ? 0 : -1;
+}
+#endif
+
+#ifdef HB_WAVE_CLOCKS
+extern "C" int hb_debug_wave_clocks(unsigned long long* out, int nwaves) {
+  if (nwaves > 65536) nwaves = 65536;
+  hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(hb_wave_clk), 4 * sizeof(unsigned long long) * nwaves);
   return e == hipSuccess ? 0 : -1;
 }
 #endif

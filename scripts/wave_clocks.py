@@ -1,0 +1,70 @@
+"""Per-wave lifetimes of the C2 eval kernel (experiment build with
+-DHB_WAVE_CLOCKS, loaded through HBMI_LIB): start/end shader clocks, SIMD and
+CU of every wave, then per-SIMD occupancy over the kernel's span.
+
+    HBMI_LIB=.../libhbmi_clk.so python scripts/wave_clocks.py [--ncad 1024] [--walkers 4096]
+"""
+import argparse, ctypes as C, json, os, sys
+import numpy as np
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import torch  # noqa: E402
+from hb_mcmc_amd import _lib, synth  # noqa: E402
+from hb_mcmc_amd.likelihood import HBLikelihood  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--ncad", type=int, default=1024)
+ap.add_argument("--walkers", type=int, default=4096)
+ap.add_argument("--reps", type=int, default=20)
+a = ap.parse_args()
+n, w = a.ncad, a.walkers
+t = synth.cadences(n)
+with HBLikelihood(t, np.ones(n), np.ones(n), device=0) as tmp:
+    truth = tmp.light_curve(synth.THETA_STAR[None, :])[0]
+s = np.full(n, 1e-3)
+f = truth + s * synth.noise(n)
+L = HBLikelihood(t, f, s, device=0)
+L.reserve(w)
+P = torch.from_numpy(synth.walkers(w, seed=1000)).cuda()
+out = torch.empty(w, dtype=torch.float64, device="cuda")
+st = torch.cuda.current_stream()
+for _ in range(a.reps):
+    L.prepare_dev(P, st)
+    L.evaluate_dev(w, out, 0, st)
+torch.cuda.synchronize()
+lib = _lib.lib()
+buf = (C.c_ulonglong * (4 * w))()
+assert lib.hb_debug_wave_clocks(buf, w) == 0
+c = np.frombuffer(buf, dtype=np.uint64).reshape(w, 4).astype(np.int64)
+t0, t1, hw, xcc = c[:, 0], c[:, 1], c[:, 2], c[:, 3]
+simd = (hw >> 4) & 3
+cu = (hw >> 8) & 15
+se = (hw >> 13) & 7
+xid = xcc & 15
+key = ((xid * 8 + se) * 16 + cu) * 4 + simd
+life = t1 - t0
+res = {"waves": int(w), "life_mean": float(life.mean()), "life_min": int(life.min()), "life_max": int(life.max()),
+       "life_pct": [float(x) for x in np.percentile(life, [5, 25, 50, 75, 95])]}
+spans, occ, order = [], [], []
+for k in np.unique(key):
+    m = key == k
+    a0, a1 = t0[m].min(), t1[m].max()
+    spans.append(a1 - a0)
+    occ.append(life[m].sum() / max(1, (a1 - a0)))
+    srt = np.argsort(t0[m])
+    order.append(list((t1[m][srt] - a0)))
+res["simds"] = len(spans)
+res["waves_per_simd"] = float(w / len(spans))
+res["simd_span_mean"] = float(np.mean(spans))
+res["simd_span_max"] = int(np.max(spans))
+res["simd_mean_resident_waves"] = float(np.mean(occ))
+ends = [sorted(o) for o in order if len(o) == 4]
+if ends:
+    res["finish_order_mean_of_4"] = [float(np.mean([e[i] for e in ends])) for i in range(4)]
+starts = []
+for k in np.unique(key):
+    m = key == k
+    starts.append(np.sort(t0[m] - t0[m].min()))
+res["start_stagger_mean"] = [float(np.mean([s[i] for s in starts if len(s) > i])) for i in range(4)]
+print(json.dumps(res, indent=1))
+L.close()
