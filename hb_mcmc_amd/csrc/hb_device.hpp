@@ -76,9 +76,13 @@ struct alignas(16) WalkerConst {
   double cpsi, spsi;             // cos/sin psi
   double cdel, sdel;             // cos/sin del, del = 0.85 e
   double tab;                    // 1.0: use the table, 0.0: direct sincos
-  double pad[2];
+  // cos/sin u numerators: cos u (1 - e cos E) = cw (cos E - e) - swq sin E,
+  // sin u (1 - e cos E) = sw (cos E - e) + cwq sin E
+  double swq, cwq;               // sin/cos omega0 x sqrt(1 - e^2)
+  double ci2;                    // cos^2 inc
+  double pad0;
 };
-static_assert(sizeof(WalkerConst) == 44 * 8, "WalkerConst layout");
+static_assert(sizeof(WalkerConst) == 46 * 8, "WalkerConst layout");
 
 // ------------------------------------------------------------------------
 // small helpers
@@ -379,7 +383,10 @@ __device__ inline void hb_prepare_walker(const double* __restrict__ p, const dou
   w.cdel = 1.0;
   w.sdel = 0.0;
   w.tab = 0.0;  // the scalar drop-in paths evaluate sin/cos directly
-  for (int k = 0; k < 2; ++k) w.pad[k] = 0.0;
+  w.swq = w.sw * w.sq1me2;
+  w.cwq = w.cw * w.sq1me2;
+  w.ci2 = w.ci * w.ci;
+  w.pad0 = 0.0;
 }
 
 // ------------------------------------------------------------------------
@@ -660,6 +667,9 @@ __device__ __forceinline__ bool newton_k(double e, const double (&m)[K], double 
 // The photometric polynomial of K cadences from (sin, cos) of the solved
 // eccentric anomaly, without the eclipse; dd = (projected separation / a)^2
 // and zz (sign carrier of Z1 - Z2) for the eclipse test.
+#ifndef HB_FLUX_V
+#define HB_FLUX_V 2  // 2: numerator form (beta = 1 / den); 1: through cos/sin nu
+#endif
 template <int K>
 __device__ __forceinline__ void flux_poly_k(const double (&s)[K], const double (&c)[K], const WalkerConst& w,
                                             double (&v)[K], double (&dd)[K], double (&zz)[K]) {
@@ -668,6 +678,19 @@ __device__ __forceinline__ void flux_poly_k(const double (&s)[K], const double (
   for (int k = 0; k < K; ++k) {
     const double den = fma(-e, c[k], 1.0);
     const double inv = fast_rcp(den);
+#if HB_FLUX_V == 2
+    // u = omega0 + nu from the numerators of cos/sin nu (den > 0): beta =
+    // (1 + e cos nu) / (1 - e^2) = 1 / (1 - e cos E) identically, and the
+    // squared projected separation / a^2 is CU^2 + cos^2 i SU^2
+    const double P = c[k] - e;
+    const double CU = fma(w.cw, P, -(w.swq * s[k]));
+    const double SU = fma(w.sw, P, w.cwq * s[k]);
+    const double cu = CU * inv;
+    const double su = SU * inv;
+    const double b = inv;
+    dd[k] = fma(CU, CU, w.ci2 * (SU * SU));  // sqrt only on eclipse lanes
+    zz[k] = SU * w.si;
+#else
     const double cnu = (c[k] - e) * inv;
     const double snu = (w.sq1me2 * s[k]) * inv;
     const double cu = fma(w.cw, cnu, -w.sw * snu);
@@ -676,6 +699,7 @@ __device__ __forceinline__ void flux_poly_k(const double (&s)[K], const double (
     const double sci = su * w.ci;
     dd[k] = (den * den) * fma(cu, cu, sci * sci);  // sqrt only on eclipse lanes
     zz[k] = su * w.si;
+#endif
     const double c2 = (cu - su) * (cu + su);          // cos 2u
     const double su2 = su * su;
     const double s3 = su * fma(-4.0, su2, 3.0);       // sin 3u
@@ -772,6 +796,9 @@ __device__ __forceinline__ void hb_cadence_flux_chain(const double (&t)[K], cons
 #ifndef HB_WARM
 #define HB_WARM 1
 #endif
+#ifndef HB_WARM_V
+#define HB_WARM_V 2  // 2: third-order start + one Newton step; 1: first-order start + two steps
+#endif
   // e <= kWarmEmax is the caller's walker-uniform gate (model_pass_chain)
   bool warm = HB_WARM && !first && !__any(exact);
   HB_STAT(0);
@@ -783,6 +810,53 @@ __device__ __forceinline__ void hb_cadence_flux_chain(const double (&t)[K], cons
     // bounds recomputes (sin, cos) of its current E directly and the wave
     // continues with the general Newton loop from there (no restart).
     bool fine = true;
+#if HB_WARM_V == 2
+    // Third-order start: series reversion of Kepler's equation about the
+    // previous cadence's root, E0 = E_p + x - A x^2 + (2 A^2 - B) x^3 with
+    // x = dM / f1, A = f2 / (2 f1), B = f3 / (6 f1) at E_p (derivatives of
+    // E - e sin E: f1 = 1 - e cos, f2 = e sin, f3 = e cos), error O(x^4);
+    // then (sin, cos)(E0) by the degree-9 rotation and ONE Newton step.
+    // |d| <= 2^-22 with e d^2 <= 2^-51 (1 - e cos E) means the next correction
+    // is below 2^-52 (converged, like the two-step path below).
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const double D = m[k] - fma(-e, st.s[k], st.E[k]);
+      const double q = rint(D * 0.15915494309189533577);
+      const double Dc = fma(-q, kTwoPi, D);
+      const double g = fma(-e, st.c[k], 1.0);
+      double r = __builtin_amdgcn_rcp(g);
+      r = fma(fma(-g, r, 1.0), r, r);
+      const double x = Dc * r;
+      const double A = (e * st.s[k]) * (0.5 * r);
+      const double B = (e * st.c[k]) * (r * (1.0 / 6.0));
+      const double C = fma(2.0 * A, A, -B);
+      const double dl = fma(x * x, fma(C, x, -A), x);
+      double E0 = fma(q, kTwoPi, st.E[k]) + dl;
+      double s0 = st.s[k], c0 = st.c[k];
+      const double z0 = dl * dl;
+      fine &= fabs(dl) <= 0.0625;
+      {  // rotate forward by dl: sin dl = dl (1 + z S(z)), cos dl = 1 + z C(z)
+        const double sd = fma(dl * z0, fma(z0, fma(z0, fma(z0, 1.0 / 362880.0, -1.0 / 5040.0), 1.0 / 120.0),
+                                           -1.0 / 6.0), dl);
+        const double cd = fma(z0, fma(z0, fma(z0, fma(z0, 1.0 / 40320.0, -1.0 / 720.0), 1.0 / 24.0), -0.5), 1.0);
+        const double s1 = fma(s0, cd, c0 * sd);
+        const double c1 = fma(c0, cd, -(s0 * sd));
+        s0 = s1;
+        c0 = c1;
+      }
+      const double den = fma(-e, c0, 1.0);
+      double y = __builtin_amdgcn_rcp(den);
+      y = fma(fma(-den, y, 1.0), y, y);
+      const double d = ((E0 - e * s0) - m[k]) * y;
+      E0 = E0 - d;
+      const double z = d * d;
+      fine &= (fabs(d) <= 0x1p-22) & (e * z <= 0x1p-51 * den);
+      rotate_back_tiny(d, z, s0, c0);
+      E[k] = E0;
+      s[k] = s0;
+      c[k] = c0;
+    }
+#else
 #pragma unroll
     for (int k = 0; k < K; ++k) {
       const double D = m[k] - fma(-e, st.s[k], st.E[k]);
@@ -823,6 +897,7 @@ __device__ __forceinline__ void hb_cadence_flux_chain(const double (&t)[K], cons
       s[k] = s0;
       c[k] = c0;
     }
+#endif
     if (__all(fine)) {
       HB_STAT(2);
 #pragma unroll

@@ -283,7 +283,7 @@ __global__ __launch_bounds__(kPrepThreads) void hb_prep_kernel(const double* __r
       sincos_table(0.85 * e, sv, cv);
       wc->sdel = sv;
       wc->cdel = cv;
-      wc->pad[0] = wc->pad[1] = 0.0;
+      wc->pad0 = 0.0;
     }
   } else {
     // Gaia G term (loglikelihood :834-848)
@@ -339,6 +339,9 @@ __global__ __launch_bounds__(kPrepThreads) void hb_prep_kernel(const double* __r
     wc->cw = gs[2][j];
     wc->ci = ci;
     wc->si = si;
+    wc->ci2 = ci * ci;
+    wc->swq = gs[1][j] * sq1me2;
+    wc->cwq = gs[2][j] * sq1me2;
     wc->aR = aR;
     wc->mA = mA;
     wc->mB = -wc->T0c;
@@ -571,12 +574,15 @@ __device__ __forceinline__ int slab_pos_of(const Rows& r, int i) {
 // few lanes at almost every step.  Instead the eclipsing cadences are queued
 // in LDS (slab position, separation, which star is in front) and applied 64
 // at a time, every lane busy; the value written is the same v - term.
+// Entries hold (dd, code); entry kEclQ is the write target of the lanes that
+// queue nothing (every lane stores, no exec-mask branch per cadence).
 constexpr int kEclQ = 128;  // <= 63 carried + 64 appended (flushed after every chain's append)
-__device__ __forceinline__ void ecl_apply(const WalkerConst& w, double* vals, const double* eq_dr,
+__device__ __forceinline__ void ecl_apply(const WalkerConst& w, double* vals, const double* eq_dd,
                                           const int* eq_code, int first, int cnt, int lane) {
   if (lane < cnt) {
     const int code = eq_code[first + lane];
-    vals[code >> 1] -= eclipse_term(&w, eq_dr[first + lane], (code & 1) ? -1.0 : 1.0);  // out of line
+    const double dR = sqrt(eq_dd[first + lane]) * w.aR;  // projected separation [Rsun]
+    vals[code >> 1] -= eclipse_term(&w, dR, (code & 1) ? -1.0 : 1.0);  // out of line
   }
 }
 
@@ -768,13 +774,15 @@ __device__ __forceinline__ void model_pass_chain(const double* __restrict__ tT, 
       const bool act = (c < rw.rc) & (base + c < n);
       const int sp = slab_pos(rw, lane, c);
       if (act) vals[sp] = v[k];
+#ifdef HB_ABLATE_ECL  // experiment builds only: no eclipse test
+      const bool need = false;
+#else
       const bool need = act && !bad && eclipse_lane(w, dd[k], zz[k]);
+#endif
       const uint64_t bal = __ballot(need);
-      if (need) {
-        const int pos = qn + __popcll(bal & lt_mask);
-        eq_dr[pos] = sqrt(dd[k]) * w.aR;
-        eq_code[pos] = 2 * sp + (zz[k] < 0.0 ? 1 : 0);
-      }
+      const int pos = need ? qn + __popcll(bal & lt_mask) : kEclQ;
+      eq_dr[pos] = dd[k];
+      eq_code[pos] = 2 * sp + (zz[k] < 0.0 ? 1 : 0);
       qn += __popcll(bal);
       tk[k] = tn[k];
       const bool last = (j == lc - 1) && (k == KC - 1);
@@ -1342,7 +1350,7 @@ __global__ __launch_bounds__(64 * WPB) HB_WPE_ATTR void hb_eval_wave_kernel(
     if (VPT >= HB_CHAIN_VPT_MIN && VPT <= HB_CHAIN_VPT_MAX && chain_eligible(w, MULTI ? tab[wt[wv]].gap : gap)) {
       // the eclipse queue shares the select's candidate area (dead until the select)
       double* eq_dr = reinterpret_cast<double*>(smem + slab_bytes);
-      int* eq_code = reinterpret_cast<int*>(eq_dr + kEclQ);
+      int* eq_code = reinterpret_cast<int*>(eq_dr + kEclQ + 1);
       model_pass_chain<VPT>(rows, ph, (int)n, rw, w, vals, eq_dr, eq_code, lane, pc);
     } else {
       model_pass_cold(t, ph, (int)n, rw, w, vals, lane, pc);
@@ -2062,7 +2070,7 @@ size_t wave_slab_bytes(long n) {
 // slab | select candidates | eclipse queue (chain model pass only)
 size_t wave_lds_bytes(size_t slab, int vpt) {
   const bool chain = vpt >= HB_CHAIN_VPT_MIN && vpt <= HB_CHAIN_VPT_MAX;
-  const size_t q = chain ? (size_t)kEclQ * (8 + 4) : 0;  // eclipse queue aliases the candidates
+  const size_t q = chain ? (size_t)(kEclQ + 1) * (8 + 4) : 0;  // eclipse queue aliases the candidates
   return (slab + (q > 8 * kCandMax ? q : 8 * kCandMax) + 15) & ~(size_t)15;
 }
 
