@@ -1363,32 +1363,26 @@ __global__ __launch_bounds__(64 * WPB) HB_WPE_ATTR void hb_eval_wave_kernel(
   }
 #endif
   HB_WSYNC();
-  // keys, and the lane's min/max keys (values ~1; -0.0 / +0.0 take the outer
-  // key, NaN lanes fall back to integer key min/max)
-  {
-    double vmn = __builtin_inf(), vmx = -__builtin_inf();
-    bool nan = false;
+  // keys, and the lane's min/max keys.  Every slot is loaded unconditionally
+  // (slot v >= rc reads row position rc - 1) so the VPT LDS reads are in
+  // flight together, then masked; min/max run on the order keys (exact
+  // bracket, NaN keys included, no IEEE min/max canonicalisation).
+  constexpr int kCh = VPT < 8 ? VPT : 8;  // slots per batch of loads in flight
+  kmn = ~0ull;
+  kmx = 0ull;
 #pragma unroll
-    for (int v = 0; v < VPT; ++v) {
+  for (int v0 = 0; v0 < VPT; v0 += kCh) {
+    double x[kCh];
+#pragma unroll
+    for (int u = 0; u < kCh; ++u) x[u] = vals[slab_pos(rw, lane, v0 + u < rw.rc ? v0 + u : rw.rc - 1)];
+#pragma unroll
+    for (int u = 0; u < kCh; ++u) {
+      const int v = v0 + u;
       const bool act = key_live(rw, v, lane, n);
-      const double x = act ? vals[slab_pos(rw, lane, v)] : vmn;
-      key[v] = act ? dkey(x) : ~0ull;  // padding sorts last, never selected
-      vmn = fmin(vmn, x);
-      vmx = fmax(vmx, x);
-      nan |= x != x;
-    }
-    kmn = dkey(vmn == 0.0 ? -0.0 : vmn);
-    kmx = dkey(vmx == 0.0 ? 0.0 : vmx);
-    if (__any(nan)) {
-      kmn = ~0ull;
-      kmx = 0ull;
-#pragma unroll
-      for (int v = 0; v < VPT; ++v) {
-        if (key_live(rw, v, lane, n)) {
-          kmn = key[v] < kmn ? key[v] : kmn;
-          kmx = key[v] > kmx ? key[v] : kmx;
-        }
-      }
+      const uint64_t kv = dkey(x[u]);
+      key[v] = act ? kv : ~0ull;  // padding sorts last, never selected
+      kmn = key[v] < kmn ? key[v] : kmn;
+      kmx = (act && kv > kmx) ? kv : kmx;
     }
   }
 #if HB_SEL_V == 1
@@ -1423,14 +1417,25 @@ __global__ __launch_bounds__(64 * WPB) HB_WPE_ATTR void hb_eval_wave_kernel(
     HB_CLK_END(wv);
     return;
   }
+  // chi^2 operands in lane-row order (coalesced), loaded unconditionally
+  // (slot v >= rc re-reads row rc - 1) so the loads are in flight together
   double acc = 0.0;
 #pragma unroll
-  for (int v = 0; v < VPT; ++v) {
-    if (key_live(rw, v, lane, n)) {
+  for (int v0 = 0; v0 < VPT; v0 += kCh) {
+    double fv[kCh], iv[kCh];
+#pragma unroll
+    for (int u = 0; u < kCh; ++u) {
+      const int vc = v0 + u < rw.rc ? v0 + u : rw.rc - 1;
+      fv[u] = fT[vc * 64 + lane];
+      iv[u] = iT[vc * 64 + lane];
+    }
+#pragma unroll
+    for (int u = 0; u < kCh; ++u) {
+      const int v = v0 + u;
       double m = (dval(key[v]) - med) + 1.0;
       m = (blend + m * one_m_blend) * tune;
-      const double r = (m - fT[v * 64 + lane]) * iT[v * 64 + lane];  // lane-row order: coalesced
-      acc += r * r;
+      const double r = (m - fv[u]) * iv[u];
+      acc += key_live(rw, v, lane, n) ? r * r : 0.0;
     }
   }
 #if HB_SEL_V == 1
