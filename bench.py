@@ -83,8 +83,6 @@ def parse():
                          "device-resident sampler vs the host sampler + GPU likelihood (0 = skip)")
     ap.add_argument("--dropin-iters", type=int, default=200,
                     help="iterations of the reference sampler relinked against libhbmi.so (dropin field; 0 = skip)")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
-                    help="per-launch HBM bytes measured by rocprofv3 --pmc (see profiles/README.md)")
     a = ap.parse_args()
     if a.walkers is None:
         a.walkers = 8192 if a.config == "C4" else 4096
@@ -335,6 +333,58 @@ def dropin_rate(niter):
     return out
 
 
+SIMDS = 1024               # 256 CUs x 4 SIMDs (MI355X_MICROARCH.md chip table)
+CLOCK_HZ = 2.4e9           # max engine clock (chip table)
+
+
+def counters_for(config):
+    """Per-call PMC counters of this workload measured on the kernels this
+    tree builds (profiles/pmc_counters.json keyed by _lib.kernel_build_id(),
+    written by scripts/pmc_summary.py), or None."""
+    from hb_mcmc_amd._lib import kernel_build_id
+    bid = kernel_build_id()
+    path = os.path.join(ROOT, "profiles", "pmc_counters.json")
+    try:
+        c = json.load(open(path)).get(bid, {}).get(config)
+    except (OSError, ValueError):
+        c = None
+    return bid, c
+
+
+def roofline(config, kernel_ms, evals_per_call, hbm_bytes_per_call, extra):
+    """The dominant kernel's roofline.  Bound: the fp64 VALU (the path is
+    elementwise fp64 transcendental work + a select; measured
+    HBM traffic is a few % of the algorithmic bytes because t/f/sigma stay
+    L2-resident).  achieved = counted fp64 flops per call (PMC) / the call's
+    HIP-event duration; the VALU-issue fraction prices the counted fp64 (4
+    clk per wave64 instruction) and other VALU instructions (2 clk) against
+    1024 SIMDs at 2.4 GHz.  The SURVEY 8(d) algorithmic-bytes figure is kept
+    as roofline.hbm.  Without counters for this kernel build the HBM figure
+    is the primary one."""
+    bid, c = counters_for(config)
+    sec = kernel_ms * 1e-3
+    hbm = {"achieved": hbm_bytes_per_call / sec / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "frac": hbm_bytes_per_call / sec / 1e9 / HBM_PEAK_GBS,
+           "algorithmic_bytes_per_call": hbm_bytes_per_call}
+    out = {}
+    if c and "fp64_flop_per_call" in c:
+        tf = c["fp64_flop_per_call"] / sec / 1e12
+        out = {"bound": "valu", "achieved": tf, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+               "frac": tf / FP64_PEAK_TFLOPS, "traffic": c.get("hbm_bytes_per_call"),
+               "fp64_flop_per_eval_counted": c["fp64_flop_per_call"] / evals_per_call}
+        if "valu_issue_cycles_per_call" in c:
+            out["valu_issue_frac"] = c["valu_issue_cycles_per_call"] / (SIMDS * CLOCK_HZ * sec)
+        out["hbm"] = hbm
+        out["counters"] = {"build": bid, "source": c.get("source")}
+    else:
+        out = {"bound": "hbm", "achieved": hbm["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+               "frac": hbm["frac"], "traffic": None,
+               "counters": {"build": bid, "source": None,
+                            "note": "no PMC pass recorded for this kernel build (scripts/pmc_summary.py)"}}
+    out.update(extra)
+    return out
+
+
 def make_event(kind):
     return _HipEvent() if kind == "hip" else torch.cuda.Event(enable_timing=True)
 
@@ -411,7 +461,6 @@ def run_c5(a, rank, world, local, dev):
     cat.close()
     if rank == 0:
         evals = a.targets * a.walkers_per_target * a.steps
-        achieved = bytes_step / (call_ms * 1e-3) / 1e9
         line = {"metric": METRIC, "value": evals / wall, "unit": "evals/s", "n_gpus": world, "steps": a.steps,
                 "warmup": a.warmup, "ms_per_step": wall / a.steps * 1e3, "higher_is_better": True,
                 "scaling": "strong", "vs_baseline": None, "dtype": "f64",
@@ -423,11 +472,10 @@ def run_c5(a, rank, world, local, dev):
                            "targets": a.targets, "walkers_per_target": a.walkers_per_target,
                            "global_walkers": a.targets * a.walkers_per_target,
                            "parallelism": f"targets dealt over {world} GPU(s) by cadence count, no collective"},
-                "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                             "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                             "kernel": "hb_catalog call (prep + hb_eval_wave_kernel<VPT,true> per size class), "
-                                       "rank 0", "kernel_ms": call_ms, "kernel_event_samples": ks,
-                             "kernel_timer": a.timer, "bytes_per_step_rank0": bytes_step}}
+                "roofline": roofline("C5", call_ms, float(wtot), bytes_step,
+                                     {"kernel": "hb_catalog call (prep + hb_eval_wave_kernel<VPT,true> per size "
+                                                "class), rank 0", "kernel_ms": call_ms, "kernel_event_samples": ks,
+                                      "kernel_timer": a.timer})}
         print(json.dumps(line), flush=True)
 
 
@@ -553,18 +601,6 @@ def main():
         evals = world * w * a.steps
         value = evals / wall
         bytes_per_eval = 24 * n + 176
-        achieved = bytes_per_eval * w / (eval_ms * 1e-3) / 1e9
-        traffic = None
-        if os.path.exists(a.traffic_json):
-            try:
-                tj = json.load(open(a.traffic_json))
-                key = f"N{n}_W{w}"
-                traffic = tj.get(key, {}).get("hbm_bytes_per_launch")
-            except Exception:
-                traffic = None
-        flops_conv = 600.0 * n  # SURVEY.md 8(d) counting convention
-        # the eval plan (hb_kernels.hip make_plan): one wave per walker up to 2048 cadences,
-        # NW waves with register keys above
         kernel_name = L.eval_kernel
         line = {
             "metric": METRIC,
@@ -586,14 +622,11 @@ def main():
                                        f"with the next step's kernels") if world > 1 else "single GPU",
                        "evals_per_walker_step": 1,
                        "note": "reference sampler spends 2 evals per walker-step (mcmc_wrapper2.c:488-489)"},
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": kernel_name, "kernel_ms": eval_ms, "prep_kernel_ms": prep_ms,
-                         "kernel_event_samples": len(timed), "kernel_timer": a.timer,
-                         "bytes_per_eval": bytes_per_eval},
-            "fp64": {"achieved_tflops": flops_conv * w / (eval_ms * 1e-3) / 1e12, "peak_tflops": FP64_PEAK_TFLOPS,
-                     "frac": flops_conv * w / (eval_ms * 1e-3) / 1e12 / FP64_PEAK_TFLOPS,
-                     "convention": "600*N flop per eval (SURVEY.md 8(d)); fp64 VALU is the binding roof"},
+            "roofline": roofline(a.config if a.config != "C2" or n <= 2048 else "C3", eval_ms, float(w),
+                                 float(bytes_per_eval * w),
+                                 {"kernel": kernel_name, "kernel_ms": eval_ms, "prep_kernel_ms": prep_ms,
+                                  "kernel_event_samples": len(timed), "kernel_timer": a.timer,
+                                  "bytes_per_eval": bytes_per_eval}),
             "kernel_only_evals_per_s": w / ((eval_ms + prep_ms) * 1e-3),
             "nonfinite_logl_last_batch": nonfinite,
         }

@@ -28,6 +28,22 @@ class HBMIError(RuntimeError):
     pass
 
 
+# sources that determine the likelihood kernels' machine code: the PMC counter
+# file (profiles/pmc_counters.json) is keyed by this id, so bench.py only
+# quotes counters that were measured on the kernels it runs
+KERNEL_SOURCES = ("hb_kernels.hip", "hb_device.hpp", "hb_math.hpp", "hb_internal.hpp", "hb_accept.hpp",
+                  "hb_glibc_math.hpp", "hb_glibc_tables.inc", "Makefile")
+
+
+def kernel_build_id() -> str:
+    import hashlib
+    h = hashlib.sha256()
+    for name in KERNEL_SOURCES:
+        with open(os.path.join(CSRC, name), "rb") as fh:
+            h.update(name.encode() + b"\0" + fh.read())
+    return h.hexdigest()[:16]
+
+
 def build(jobs: int = 4) -> str:
     """Compile libhbmi.so for gfx950 in-tree (hipcc cross-compiles without a GPU)."""
     subprocess.run(["make", "-s", f"-j{jobs}", "-C", CSRC], check=True)

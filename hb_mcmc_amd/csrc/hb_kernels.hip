@@ -1320,7 +1320,11 @@ __global__ __launch_bounds__(64 * WPB) HB_WPE_ATTR void hb_eval_wave_kernel(
   uint32_t* hist = reinterpret_cast<uint32_t*>(smem);
   uint64_t* cand = reinterpret_cast<uint64_t*>(smem + slab_bytes);
   const WalkerConst& w = wcs[valid ? wv : 0];
+#ifdef HB_ABLATE_EXIT  // experiment builds only: every wave takes the early exit (launch floor)
+  const bool roche_exit = mode == 0;
+#else
   const bool roche_exit = mode == 0 && w.roche != 0.0;
+#endif
   Pacer pc{nullptr, 0u, wib, WPB, lane, 0u};
 #if HB_PRIO == 2
   if (WPB > 1) {

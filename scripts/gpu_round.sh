@@ -15,6 +15,6 @@ step() {  # name, timeout, cmd...
 step pytest_gpu 900 python -u -m pytest tests -x -v -m gpu -p no:cacheprovider --timeout 300 --timeout-method thread
 step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 step bench_c2 600 python bench.py
-step bench_c3 600 python bench.py --ncad 20000 --steps 20 --warmup 3 --no-cpu-baseline --sampler-iters 0
-step bench_c5 600 python bench.py --config C5 --steps 100 --warmup 10 --no-cpu-baseline --sampler-iters 0
+step bench_c3 600 python bench.py --config C3 --steps 20 --warmup 3 --no-cpu-baseline --sampler-iters 0 --dropin-iters 0
+step bench_c5 600 python bench.py --config C5 --steps 100 --warmup 10 --no-cpu-baseline --sampler-iters 0 --dropin-iters 0
 bash scripts/profile.sh $TAG
