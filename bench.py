@@ -81,7 +81,7 @@ def parse():
     ap.add_argument("--sampler-iters", type=int, default=100,
                     help="also time the whole PT-MCMC iteration (mcmc_wrapper2.c loop) at the workload's W and N: "
                          "device-resident sampler vs the host sampler + GPU likelihood (0 = skip)")
-    ap.add_argument("--dropin-iters", type=int, default=200,
+    ap.add_argument("--dropin-iters", type=int, default=1000,
                     help="iterations of the reference sampler relinked against libhbmi.so (dropin field; 0 = skip)")
     a = ap.parse_args()
     if a.walkers is None:

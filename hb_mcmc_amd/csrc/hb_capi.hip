@@ -14,6 +14,7 @@
 #include <string.h>
 
 #include <memory>
+#include <condition_variable>
 #include <mutex>
 #include <string>
 #include <algorithm>
@@ -693,45 +694,124 @@ uint64_t mix64(uint64_t h, uint64_t v) {
   h *= 0xbf58476d1ce4e5b9ull;
   return h ^ (h >> 31);
 }
+// four independent lanes (the multiply chains overlap), folded at the end
 uint64_t hash_doubles(uint64_t h, const double* a, long n) {
-  for (long i = 0; i < n; ++i) {
+  uint64_t l[4] = {h, h ^ 0x1111, h ^ 0x2222, h ^ 0x3333};
+  long i = 0;
+  for (; i + 4 <= n; i += 4)
+    for (int k = 0; k < 4; ++k) {
+      uint64_t v;
+      memcpy(&v, a + i + k, 8);
+      l[k] = mix64(l[k], v);
+    }
+  for (; i < n; ++i) {
     uint64_t v;
     memcpy(&v, a + i, 8);
-    h = mix64(h, v);
+    l[0] = mix64(l[0], v);
   }
-  return mix64(h, (uint64_t)n);
+  return mix64(mix64(mix64(mix64(l[0], l[1]), l[2]), l[3]), (uint64_t)n);
 }
 
-// Per-thread cache of resident light curves: the reference sampler calls
-// loglikelihood() with the same arrays every step from each OpenMP thread.
-struct CacheEnt {
-  uint64_t key;
-  hb_ctx* ctx;
+// Resident light curves of the likelihood3.h drop-in, shared by every caller
+// thread: the reference sampler calls loglikelihood() with the same arrays
+// from its 25 OpenMP threads (mcmc_wrapper2.c:383-489).
+//
+// Call combiner: concurrent loglikelihood() calls on one light curve are
+// evaluated together.  A caller queues its parameter vector; if no launch is
+// in flight it becomes the leader, takes every queued request and evaluates
+// them as one batch (one H2D copy, one prep + eval launch pair, one D2H copy);
+// the others sleep until their result is written.  Requests that arrive while
+// a batch runs form the next batch.  Each walker's logL does not depend on the
+// batch it rides in (the kernels evaluate walkers independently).
+struct DropReq {
+  const double* p;
+  double out;
+  bool done;
 };
-struct ThreadCache {
-  std::vector<CacheEnt> ents;
-  ~ThreadCache() {
-    for (auto& e : ents) hb_destroy(e.ctx);
-  }
-  hb_ctx* get(uint64_t key) {
-    for (size_t i = 0; i < ents.size(); ++i)
-      if (ents[i].key == key) {
-        CacheEnt e = ents[i];
-        ents.erase(ents.begin() + i);
-        ents.push_back(e);
-        return e.ctx;
-      }
-    return nullptr;
-  }
-  void put(uint64_t key, hb_ctx* c) {
-    if (ents.size() >= 4) {
-      hb_destroy(ents.front().ctx);
-      ents.erase(ents.begin());
+struct DropinCtx {
+  uint64_t key = 0;
+  hb_ctx* ctx = nullptr;
+  std::mutex mu;
+  std::condition_variable cv;
+  std::vector<DropReq*> pending;
+  bool busy = false;
+  std::vector<double> params, out;  // the leader's staging
+  uint64_t last_use = 0;
+};
+struct DropinCache {
+  std::mutex mu;
+  std::vector<std::shared_ptr<DropinCtx>> ents;
+  uint64_t tick = 0;
+};
+// never destroyed: contexts outlive static destruction (the HIP runtime may
+// already be gone then); at most kDropinMax light curves stay resident
+DropinCache& dropin_cache() {
+  static DropinCache* c = new DropinCache;
+  return *c;
+}
+constexpr size_t kDropinMax = 8;
+
+std::shared_ptr<DropinCtx> dropin_ctx(const double* t, const double* f, const double* s, long n,
+                                      const double* mag, const double* err) {
+  uint64_t key = hash_doubles(0x5eed, t, n);
+  key = hash_doubles(key, f, n);
+  key = hash_doubles(key, s, n);
+  key = hash_doubles(key, mag, 5);
+  key = hash_doubles(key, err, 4);
+  DropinCache& dc = dropin_cache();
+  std::lock_guard<std::mutex> lk(dc.mu);
+  for (auto& e : dc.ents)
+    if (e->key == key) {
+      e->last_use = ++dc.tick;
+      return e;
     }
-    ents.push_back({key, c});
+  if (dc.ents.size() >= kDropinMax) {  // evict the least recently used idle entry
+    size_t victim = dc.ents.size();
+    for (size_t i = 0; i < dc.ents.size(); ++i)
+      if (dc.ents[i].use_count() == 1 && (victim == dc.ents.size() || dc.ents[i]->last_use < dc.ents[victim]->last_use))
+        victim = i;
+    if (victim < dc.ents.size()) {
+      hb_destroy(dc.ents[victim]->ctx);
+      dc.ents.erase(dc.ents.begin() + (long)victim);
+    }
   }
-};
-thread_local ThreadCache t_cache;
+  auto e = std::make_shared<DropinCtx>();
+  e->key = key;
+  e->ctx = hb_create(t, f, s, n, mag, err, 0);
+  if (!e->ctx) hb_fatal("hb_create failed");
+  e->last_use = ++dc.tick;
+  dc.ents.push_back(e);
+  return e;
+}
+
+double dropin_loglik(DropinCtx& d, const double* params) {
+  DropReq r{params, 0.0, false};
+  std::unique_lock<std::mutex> lk(d.mu);
+  d.pending.push_back(&r);
+  for (;;) {
+    if (r.done) return r.out;
+    if (!d.busy) {  // lead: evaluate every queued request (this one included)
+      d.busy = true;
+      std::vector<DropReq*> batch;
+      batch.swap(d.pending);
+      lk.unlock();
+      const int w = (int)batch.size();
+      d.params.resize((size_t)w * 21);
+      d.out.resize((size_t)w);
+      for (int i = 0; i < w; ++i) memcpy(&d.params[(size_t)i * 21], batch[(size_t)i]->p, 21 * sizeof(double));
+      if (hb_loglik_batch(d.ctx, d.params.data(), w, d.out.data(), nullptr) != 0) hb_fatal("hb_loglik_batch failed");
+      lk.lock();
+      for (int i = 0; i < w; ++i) {
+        batch[(size_t)i]->out = d.out[(size_t)i];
+        batch[(size_t)i]->done = true;
+      }
+      d.busy = false;
+      d.cv.notify_all();
+      continue;
+    }
+    d.cv.wait(lk);
+  }
+}
 
 struct DevBuf {
   double* p = nullptr;
@@ -765,19 +845,9 @@ double probe(int op, const double* in, int nin, double* out, int nout) {
 }
 
 hb_ctx* cached_ctx(const double* t, const double* f, const double* s, long n, const double* mag,
-                   const double* err) {
-  uint64_t key = hash_doubles(0x5eed, t, n);
-  key = hash_doubles(key, f, n);
-  key = hash_doubles(key, s, n);
-  key = hash_doubles(key, mag, 5);
-  key = hash_doubles(key, err, 4);
-  hb_ctx* c = t_cache.get(key);
-  if (!c) {
-    c = hb_create(t, f, s, n, mag, err, 0);
-    if (!c) hb_fatal("hb_create failed");
-    t_cache.put(key, c);
-  }
-  return c;
+                   const double* err, std::shared_ptr<DropinCtx>& hold) {
+  hold = dropin_ctx(t, f, s, n, mag, err);
+  return hold->ctx;
 }
 
 }  // namespace
@@ -788,17 +858,16 @@ extern "C" double loglikelihood(double time[], double lightcurve[], double noise
   // caller-visible side effect of the reference (likelihood3.c:824-827)
   for (long i = 0; i < N; ++i)
     if (noise[i] < 1.e-5) noise[i] = 1.e-5;
-  hb_ctx* c = cached_ctx(time, lightcurve, noise, N, mag_data, magerr);
-  double out = 0.0;
-  if (hb_loglik_batch(c, params, 1, &out, nullptr) != 0) hb_fatal("hb_loglik_batch failed");
-  return out;
+  std::shared_ptr<DropinCtx> d = dropin_ctx(time, lightcurve, noise, N, mag_data, magerr);
+  return dropin_loglik(*d, params);
 }
 
 extern "C" void calc_light_curve(double* times, long Nt, double* pars, double* tmpl) {
   require_device();
   std::vector<double> zeros((size_t)Nt, 0.0), ones((size_t)Nt, 1.0);
   const double mag[5] = {1000., 1., 1., 1., 1.}, err[4] = {1e15, 1e15, 1e15, 1e15};
-  hb_ctx* c = cached_ctx(times, zeros.data(), ones.data(), Nt, mag, err);
+  std::shared_ptr<DropinCtx> hold;
+  hb_ctx* c = cached_ctx(times, zeros.data(), ones.data(), Nt, mag, err, hold);
   if (hb_light_curve_batch(c, pars, 1, tmpl, nullptr) != 0) hb_fatal("hb_light_curve_batch failed");
 }
 
