@@ -792,15 +792,34 @@ __device__ __forceinline__ void hb_cadence_flux_chain(const double (&t)[K], cons
   const double e = w.e;
   double m[K], E[K], s[K], c[K], yk[K];
   bool ok = true, exact = false, plus[K];
-  mean_anomaly_k<K>(t, w, m, plus, ok, exact);
 #ifndef HB_WARM
 #define HB_WARM 1
 #endif
 #ifndef HB_WARM_V
 #define HB_WARM_V 2  // 2: third-order start + one Newton step; 1: first-order start + two steps
 #endif
+#if HB_WARM_V == 2
+  // The warm step only needs M up to a multiple of 2pi (D is reduced by
+  // rint below), so the exactness flags and sign(sin M) of the reference's
+  // start are computed only when a cold start is taken.
+  bool have_flags = false;
+  if (first) {
+    mean_anomaly_k<K>(t, w, m, plus, ok, exact);
+    have_flags = true;
+  } else {
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const double x = fma(t[k], kDay, w.mB) * w.mA;
+      ok &= sincos_fast_ok(x);
+      m[k] = fma(-trunc(x * 0.15915494309189533577), kTwoPi, x);
+    }
+  }
+  bool warm = HB_WARM && !first;
+#else
+  mean_anomaly_k<K>(t, w, m, plus, ok, exact);
   // e <= kWarmEmax is the caller's walker-uniform gate (model_pass_chain)
   bool warm = HB_WARM && !first && !__any(exact);
+#endif
   HB_STAT(0);
   if (warm) {
     // the common warm step as one basic block (the K chains' solves and
@@ -926,6 +945,12 @@ __device__ __forceinline__ void hb_cadence_flux_chain(const double (&t)[K], cons
   }
   if (!warm) {
     HB_STAT(4);
+#if HB_WARM_V == 2
+    if (!have_flags) {  // rare: the warm chain did not converge
+      ok = true;
+      mean_anomaly_k<K>(t, w, m, plus, ok, exact);
+    }
+#endif
     cold_start_k<K>(t, ph, tab, exact, w, m, plus, E, s, c, ok);
     (void)newton_k<K>(e, m, E, s, c, yk, ok);
   }

@@ -574,15 +574,16 @@ __device__ __forceinline__ int slab_pos_of(const Rows& r, int i) {
 // few lanes at almost every step.  Instead the eclipsing cadences are queued
 // in LDS (slab position, separation, which star is in front) and applied 64
 // at a time, every lane busy; the value written is the same v - term.
-// Entries hold (dd, code); entry kEclQ is the write target of the lanes that
-// queue nothing (every lane stores, no exec-mask branch per cadence).
+// Entries hold (dd with the sign of zz, slab position); entry kEclQ is the
+// write target of the lanes that queue nothing (every lane stores, no
+// exec-mask branch per cadence).
 constexpr int kEclQ = 128;  // <= 63 carried + 64 appended (flushed after every chain's append)
 __device__ __forceinline__ void ecl_apply(const WalkerConst& w, double* vals, const double* eq_dd,
                                           const int* eq_code, int first, int cnt, int lane) {
   if (lane < cnt) {
-    const int code = eq_code[first + lane];
-    const double dR = sqrt(eq_dd[first + lane]) * w.aR;  // projected separation [Rsun]
-    vals[code >> 1] -= eclipse_term(&w, dR, (code & 1) ? -1.0 : 1.0);  // out of line
+    const double q = eq_dd[first + lane];
+    const double dR = sqrt(fabs(q)) * w.aR;  // projected separation [Rsun]
+    vals[eq_code[first + lane]] -= eclipse_term(&w, dR, signbit(q) ? -1.0 : 1.0);  // out of line
   }
 }
 
@@ -624,15 +625,19 @@ struct Pacer {
   int wpb;         // waves per block
   int lane;
   uint32_t inc;    // (16 << 8) / steps
+  int q1, q2, q3;  // first steps of the 2nd, 3rd and 4th quarter
   __device__ __forceinline__ void begin(int steps) {
     inc = (16u << 8) / (uint32_t)(steps > 0 ? steps : 1);
+    q1 = (steps + 3) >> 2;
+    q2 = (steps + 1) >> 1;
+    q3 = (3 * steps + 3) >> 2;
   }
   __device__ __forceinline__ void step(int j, int n) const {
 #if HB_PRIO == 1
-    if (4 * j == n || 4 * j == n + 1 || 4 * j == n + 2 || 4 * j == n + 3) __builtin_amdgcn_s_setprio(2);
-    if (2 * j == n || 2 * j == n + 1) __builtin_amdgcn_s_setprio(1);
-    if (4 * j == 3 * n || 4 * j == 3 * n + 1 || 4 * j == 3 * n + 2 || 4 * j == 3 * n + 3)
-      __builtin_amdgcn_s_setprio(0);
+    (void)n;
+    if (j == q1) __builtin_amdgcn_s_setprio(2);
+    if (j == q2) __builtin_amdgcn_s_setprio(1);
+    if (j == q3) __builtin_amdgcn_s_setprio(0);
 #elif HB_PRIO == 2
     (void)n;
     if (prog == nullptr) return;
@@ -713,6 +718,7 @@ __device__ __forceinline__ void model_pass_chain(const double* __restrict__ tT, 
   const bool tab = (ph != nullptr) && (w.tab != 0.0);  // walker-uniform
   const int last = n - 1;
   const int base = lane * rw.rc;
+  const int rs = lane * rw.stride, lsw = lane & rw.swz;  // slab_pos(rw, lane, c) = rs + (c ^ lsw)
   const uint64_t lt_mask = (1ull << lane) - 1ull;
   int qn = 0;  // queued eclipse cadences (wave-uniform)
   ChainState<KC> st;
@@ -771,19 +777,21 @@ __device__ __forceinline__ void model_pass_chain(const double* __restrict__ tT, 
 #pragma unroll
     for (int k = 0; k < KC; ++k) {
       const int c = k * lc + j;
-      const bool act = (c < rw.rc) & (base + c < n);
-      const int sp = slab_pos(rw, lane, c);
-      if (act) vals[sp] = v[k];
+      if (c < rw.rc) {  // wave-uniform: the last chain may run past the row end
+        // cadences past n (the last row's padding) store harmless values: their keys are masked
+        const int sp = rs + (c ^ lsw);
+        vals[sp] = v[k];
 #ifdef HB_ABLATE_ECL  // experiment builds only: no eclipse test
-      const bool need = false;
+        const bool need = false;
 #else
-      const bool need = act && !bad && eclipse_lane(w, dd[k], zz[k]);
+        const bool need = !bad && eclipse_lane(w, dd[k], zz[k]);
 #endif
-      const uint64_t bal = __ballot(need);
-      const int pos = need ? qn + __popcll(bal & lt_mask) : kEclQ;
-      eq_dr[pos] = dd[k];
-      eq_code[pos] = 2 * sp + (zz[k] < 0.0 ? 1 : 0);
-      qn += __popcll(bal);
+        const uint64_t bal = __ballot(need);
+        const int pos = need ? qn + __popcll(bal & lt_mask) : kEclQ;
+        eq_dr[pos] = copysign(dd[k], zz[k]);  // sign bit: which star is in front
+        eq_code[pos] = sp;
+        qn += __popcll(bal);
+      }
       tk[k] = tn[k];
       const bool last = (j == lc - 1) && (k == KC - 1);
       while (qn >= 64 || (last && qn > 0)) {  // wave-uniform
@@ -1325,7 +1333,7 @@ __global__ __launch_bounds__(64 * WPB) HB_WPE_ATTR void hb_eval_wave_kernel(
 #else
   const bool roche_exit = mode == 0 && w.roche != 0.0;
 #endif
-  Pacer pc{nullptr, 0u, wib, WPB, lane, 0u};
+  Pacer pc{nullptr, 0u, wib, WPB, lane, 0u, 0, 0, 0};
 #if HB_PRIO == 2
   if (WPB > 1) {
     // progress words: simd << 16 | progress; finished or idle waves report 0xffff
