@@ -1,5 +1,6 @@
 """Copy rocprofv3 outputs from gpurun_out/ into profiles/ (tracked) and derive
-per-launch HBM traffic for bench.py's roofline.traffic.
+per-dispatch PMC averages (round 1 format; bench.py reads profiles/pmc_counters.json,
+written by scripts/pmc_summary.py).
 
     python scripts/summarize_prof.py TAG NCAD WALKERS
 
@@ -27,13 +28,7 @@ summary = {kern: {c: sum(v) / len(v) for c, v in d.items()} for kern, d in vals.
 out = {"tag": tag, "ncad": ncad, "walkers": walkers, "per_dispatch_mean": summary}
 ev = summary.get("eval", {})
 if "FETCH_SIZE" in ev and "WRITE_SIZE" in ev:
-    hbm = (2 * ev["FETCH_SIZE"] + ev["WRITE_SIZE"]) * 1024
-    out["eval_hbm_bytes_per_launch"] = hbm
-    tj_path = os.path.join(prof, "pmc_traffic.json")
-    tj = json.load(open(tj_path)) if os.path.exists(tj_path) else {}
-    tj[f"N{ncad}_W{walkers}"] = {"hbm_bytes_per_launch": hbm, "source": f"profiles/{tag}_pmc_summary.json",
-                                 "formula": "(2*FETCH_SIZE + WRITE_SIZE)*1024, separate --pmc passes"}
-    json.dump(tj, open(tj_path, "w"), indent=1)
+    out["eval_hbm_bytes_per_launch"] = (2 * ev["FETCH_SIZE"] + ev["WRITE_SIZE"]) * 1024
 if summary:
     json.dump(out, open(os.path.join(prof, f"{tag}_pmc_summary.json"), "w"), indent=1)
 print(json.dumps(out, indent=1)[:3000])
