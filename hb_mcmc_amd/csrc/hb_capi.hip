@@ -566,13 +566,46 @@ static int catalog_layout(hb_catalog* c, const int* walkers, hipStream_t s) {
     c->class_off[cl] = (int)list.size();
     long nmax = 0, work = 0;
     w = 0;
+    // XCD-aware order: workgroup b of a launch runs on XCD b mod 8, so the
+    // class list puts all walkers of one target at positions of one residue
+    // mod 8 -- that target's light curve then fills one XCD's L2 instead of
+    // all eight.  Targets go to the least-loaded residue, largest work first;
+    // a residue whose queue runs dry takes from the longest one.
+    constexpr int kXcd = 8;
+    std::vector<std::pair<long, int>> tw;  // (work, target)
     for (int k = 0; k < c->ntargets; ++k) {
       if (c->cls[k] == cl) {
-        for (int i = 0; i < walkers[k]; ++i) list.push_back((int)(w + i));
         if (walkers[k] > 0 && c->tab[k].n > nmax) nmax = c->tab[k].n;
         work += (long)walkers[k] * c->tab[k].n;
+        if (walkers[k] > 0) tw.push_back({(long)walkers[k] * c->tab[k].n, k});
       }
-      w += walkers[k];
+    }
+    std::vector<long> first((size_t)c->ntargets + 1, 0);
+    for (int k = 0; k < c->ntargets; ++k) first[(size_t)k + 1] = first[(size_t)k] + walkers[k];
+    std::stable_sort(tw.begin(), tw.end(), [](const std::pair<long, int>& a, const std::pair<long, int>& b) {
+      return a.first > b.first;
+    });
+    std::vector<std::vector<int>> q(kXcd);
+    std::vector<long> load(kXcd, 0);
+    for (const auto& e : tw) {
+      const int x = (int)(std::min_element(load.begin(), load.end()) - load.begin());
+      load[(size_t)x] += e.first;
+      for (int i = 0; i < walkers[e.second]; ++i) q[(size_t)x].push_back((int)(first[(size_t)e.second] + i));
+    }
+    std::vector<size_t> head(kXcd, 0);
+    long left = 0;
+    for (int x = 0; x < kXcd; ++x) left += (long)q[(size_t)x].size();
+    for (long p = 0; p < left; ++p) {
+      int x = (int)(p % kXcd);
+      if (head[(size_t)x] == q[(size_t)x].size()) {  // dry: take from the longest remaining queue
+        size_t best = 0;
+        for (int y = 0; y < kXcd; ++y)
+          if (q[(size_t)y].size() - head[(size_t)y] > best) {
+            best = q[(size_t)y].size() - head[(size_t)y];
+            x = y;
+          }
+      }
+      list.push_back(q[(size_t)x][head[(size_t)x]++]);
     }
     c->class_slab[cl] = hbk::wave_slab_bytes(nmax > 0 ? nmax : 2);
     c->class_work[cl] = work;
