@@ -57,22 +57,42 @@ struct AccArgs {
   int pad;
 };
 
+// Everything the Hastings test of local slot j reads besides the new logL.
+// None of it depends on the likelihood, so the eval kernel loads it when the
+// wave starts and the test at the end of the wave waits on nothing but exp.
+struct AccPre {
+  int jg, chain;
+  double lx, temp, dlp, alpha, xo, yn;
+};
+__device__ inline AccPre accept_prefetch(const AccArgs& A, int j, int lane) {
+  AccPre p;
+  p.jg = j + A.lo;
+  p.chain = A.idx[p.jg];
+  p.lx = A.logL[p.chain];
+  p.temp = A.temp[p.jg];
+  p.dlp = A.logPy[j] - A.logP[p.chain];
+  p.alpha = A.alpha2[j];
+  p.xo = 0.0;
+  p.yn = 0.0;
+  if (lane < kNp) {
+    p.xo = A.x[(size_t)p.chain * kNp + lane];
+    p.yn = A.y[(size_t)j * kNp + lane];
+  }
+  return p;
+}
+
 // Hastings test of local slot j (global slot lo + j) whose proposal has logL
 // ly, by one wave: lane n < 21 moves coordinate n (x[chain] = y if accepted,
 // history row k = x[chain]); lane 0 does the scalar bookkeeping.  Same
 // operations and order of effects as ds_accept.
-__device__ inline void accept_slot_wave(const AccArgs& A, int j, double ly, int lane) {
-  const int jg = j + A.lo;
-  const int chain = A.idx[jg];
-  const double lx = A.logL[chain];
-  const double H = hbglibc::exp((ly - lx) / A.temp[jg] + (A.logPy[j] - A.logP[chain]));
-  const bool acc = A.alpha2[j] <= H;
+__device__ inline void accept_slot_wave_pre(const AccArgs& A, int j, double ly, int lane, const AccPre& p) {
+  const int jg = p.jg;
+  const int chain = p.chain;
+  const double lx = p.lx;
+  const double H = hbglibc::exp((ly - lx) / p.temp + p.dlp);
+  const bool acc = p.alpha <= H;
   const int k = (int)(A.iter - (A.iter / A.NPAST) * A.NPAST);
-  double xo = 0.0, yn = 0.0;
-  if (lane < kNp) {
-    xo = A.x[(size_t)chain * kNp + lane];
-    yn = A.y[(size_t)j * kNp + lane];
-  }
+  const double xo = p.xo, yn = p.yn;
   if (acc) {
     if ((lx / ly <= 0.5) && (A.iter > 10000) && (jg <= 5) && A.log_on) {
       int e = 0;
@@ -114,6 +134,9 @@ __device__ inline void accept_slot_wave(const AccArgs& A, int j, double ly, int 
     if (acc) A.x[(size_t)chain * kNp + lane] = v;
     A.hist[((size_t)j * A.NPAST + k) * kNp + lane] = v;
   }
+}
+__device__ inline void accept_slot_wave(const AccArgs& A, int j, double ly, int lane) {
+  accept_slot_wave_pre(A, j, ly, lane, accept_prefetch(A, j, lane));
 }
 
 }  // namespace hbds

@@ -322,6 +322,8 @@ extern "C" int hbx_loglik_accept_dev(hb_ctx* c, const double* d_params, int w, d
                                      void* stream) {
   if (!c) return set_err_msg("null context");
   if (c->plan.vpt == 0) return 1;
+  static const bool split = getenv("HB_DS_SPLIT_ACCEPT") != nullptr;  // experiment knob: separate ds_accept
+  if (split) return 1;
   return run_batch(c, d_params, w, d_logl, nullptr, (hipStream_t)stream,
                    static_cast<const hbds::AccArgs*>(acc));
 }

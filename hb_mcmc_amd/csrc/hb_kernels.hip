@@ -1346,9 +1346,12 @@ __global__ __launch_bounds__(64 * WPB) HB_WPE_ATTR void hb_eval_wave_kernel(
   }
 #endif
   if (!valid) return;
+  // the Hastings test's operands are loaded now, not after the likelihood
+  hbds::AccPre apre{};
+  if (ACC) apre = hbds::accept_prefetch(hst, wv, lane);
   if (roche_exit) {  // likelihood3.c:866-869, see hb_eval_kernel
     if (lane == 0) logl[wv] = -kBig / 2.0;
-    if (ACC) hbds::accept_slot_wave(hst, wv, -kBig / 2.0, lane);
+    if (ACC) hbds::accept_slot_wave_pre(hst, wv, -kBig / 2.0, lane, apre);
     HB_CLK_END(wv);
     return;
   }
@@ -1463,7 +1466,7 @@ __global__ __launch_bounds__(64 * WPB) HB_WPE_ATTR void hb_eval_wave_kernel(
   if (ACC) {
     double c = chi2 + w.chi2_extra;  // wave-uniform (the DPP sum ends in readlanes)
     if (w.roche != 0.0) c = kBig;
-    hbds::accept_slot_wave(hst, wv, __shfl(-c / 2.0, 0), lane);
+    hbds::accept_slot_wave_pre(hst, wv, __shfl(-c / 2.0, 0), lane, apre);
   }
   HB_CLK_END(wv);
 }

@@ -80,6 +80,9 @@ res = {
                 "sampler_shuffled": time_eval(xs[np.random.default_rng(1).permutation(W)])},
     "e_mean": {"bench": float(syn[:, 3].mean()), "sampler": float(xs[:, 3].mean()),
                "sampler_e_gt_0.6": float((xs[:, 3] > 0.6).mean())},
+    "e_quantiles_sampler": [float(x) for x in np.quantile(xs[:, 3], [0.1, 0.25, 0.5, 0.75, 0.9])],
+    "e_gt_0.65_frac": {"bench": float((syn[:, 3] > 0.65).mean()), "sampler": float((xs[:, 3] > 0.65).mean())},
+    "sampler_low_e_x": time_eval(np.concatenate([xs[xs[:, 3] < 0.6]] * 8)[:W]),
     "inc_near_90deg_frac": {"bench": float((np.abs(syn[:, 4] - np.pi / 2) < 0.2).mean()),
                             "sampler": float((np.abs(xs[:, 4] - np.pi / 2) < 0.2).mean())},
 }
