@@ -17,6 +17,7 @@
 // once hb_reserve() sized the workspace.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -601,7 +602,7 @@ __device__ __forceinline__ void ecl_apply(const WalkerConst& w, double* vals, co
 #define HB_CHAIN_VPT_MIN 8
 #endif
 #ifndef HB_CHAIN_VPT_MAX
-#define HB_CHAIN_VPT_MAX 16
+#define HB_CHAIN_VPT_MAX 32
 #endif
 __device__ __forceinline__ bool chain_eligible(const WalkerConst& w, double gap) {
   const double e = w.e;
@@ -1382,7 +1383,7 @@ __global__ __launch_bounds__(64 * WPB) HB_WPE_ATTR void hb_eval_wave_kernel(
   // (slot v >= rc reads row position rc - 1) so the VPT LDS reads are in
   // flight together, then masked; min/max run on the order keys (exact
   // bracket, NaN keys included, no IEEE min/max canonicalisation).
-  constexpr int kCh = VPT < 8 ? VPT : 8;  // slots per batch of loads in flight
+  constexpr int kCh = VPT < 8 ? VPT : (VPT >= 32 ? 4 : 8);  // slots per batch of loads in flight
   kmn = ~0ull;
   kmx = 0ull;
 #pragma unroll
@@ -2123,7 +2124,8 @@ EvalPlan make_plan(long n) {
   EvalPlan pl;
   pl.n = n;
   pl.kth = (n % 2 == 0) ? n / 2 : n / 2 + 1;  // likelihood3.c:97-99
-  if (n <= 64 * 32) {  // one wave per walker, keys in registers
+  static const long wave_max = getenv("HB_WAVE_NMAX") ? atol(getenv("HB_WAVE_NMAX")) : 64 * 32;  // A/B knob
+  if (n <= wave_max && n <= 64 * 32) {  // one wave per walker, keys in registers
     pl.vpt = wave_vpt_for(n);
     pl.nw = 1;
     pl.lds = true;
