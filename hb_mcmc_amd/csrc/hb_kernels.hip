@@ -69,20 +69,29 @@ using namespace hbdev;
 // Experiment builds only (HB_WAVE_CLOCKS): per-wave shader clock at entry and
 // exit plus HW_ID / XCC_ID, read back by hb_debug_wave_clocks().
 #ifdef HB_WAVE_CLOCKS
-__device__ unsigned long long hb_wave_clk[4 * 65536];
-#define HB_CLK_BEGIN() const unsigned long long clk0_ = __builtin_amdgcn_s_memtime()
+// 8 words per wave: start, phase marks 1..3 (after the model pass, the keys,
+// the select; 0 if not reached), end, HW_ID, XCC_ID, spare
+__device__ unsigned long long hb_wave_clk[8 * 65536];
+#define HB_CLK_BEGIN()                                     \
+  const unsigned long long clk0_ = __builtin_amdgcn_s_memtime(); \
+  unsigned long long clkm_[3] = {0ull, 0ull, 0ull}
+#define HB_CLK_MARK(i) clkm_[(i)] = __builtin_amdgcn_s_memtime()
 #define HB_CLK_END(wv)                                                                  \
   do {                                                                                  \
     const unsigned long long clk1_ = __builtin_amdgcn_s_memtime();                      \
     if ((threadIdx.x & 63) == 0 && (wv) < 65536) {                                      \
-      hb_wave_clk[4 * (wv) + 0] = clk0_;                                                \
-      hb_wave_clk[4 * (wv) + 1] = clk1_;                                                \
-      hb_wave_clk[4 * (wv) + 2] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);  \
-      hb_wave_clk[4 * (wv) + 3] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 20); \
+      hb_wave_clk[8 * (wv) + 0] = clk0_;                                                \
+      hb_wave_clk[8 * (wv) + 1] = clkm_[0];                                             \
+      hb_wave_clk[8 * (wv) + 2] = clkm_[1];                                             \
+      hb_wave_clk[8 * (wv) + 3] = clkm_[2];                                             \
+      hb_wave_clk[8 * (wv) + 4] = clk1_;                                                \
+      hb_wave_clk[8 * (wv) + 5] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);  \
+      hb_wave_clk[8 * (wv) + 6] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 20); \
     }                                                                                   \
   } while (0)
 #else
 #define HB_CLK_BEGIN() do { } while (0)
+#define HB_CLK_MARK(i) do { } while (0)
 #define HB_CLK_END(wv) do { } while (0)
 #endif
 
@@ -1372,6 +1381,7 @@ __global__ __launch_bounds__(64 * WPB) HB_WPE_ATTR void hb_eval_wave_kernel(
       model_pass_cold(t, ph, (int)n, rw, w, vals, lane, pc);
     }
   }
+  HB_CLK_MARK(0);
 #if HB_PRIO == 2
   if (pc.prog != nullptr) {
     if (lane == 0) pc.prog[wib] = pc.tag | 0xffffu;  // model pass done: stop holding the others back
@@ -1408,6 +1418,7 @@ __global__ __launch_bounds__(64 * WPB) HB_WPE_ATTR void hb_eval_wave_kernel(
   kmn = wave_reduce_u64(kmn, OpMinU64());
   kmx = wave_reduce_u64(kmx, OpMaxU64());
 #endif
+  HB_CLK_MARK(1);
   HB_WSYNC();  // the slab becomes the histogram
 #if HB_ABLATE_SELECT
   const double med = dval(kmn);
@@ -1419,6 +1430,7 @@ __global__ __launch_bounds__(64 * WPB) HB_WPE_ATTR void hb_eval_wave_kernel(
 #endif
 #endif
 
+  HB_CLK_MARK(2);
   const double blend = w.blend, one_m_blend = 1.0 - w.blend, tune = w.tune;
   if (mode == 1) {
     double* o = tmpl_out + (size_t)wv * (size_t)n;
@@ -2172,7 +2184,7 @@ extern "C" int hb_dbg_chain_stats(unsigned long long* out, int reset) {
 #ifdef HB_WAVE_CLOCKS
 extern "C" int hb_debug_wave_clocks(unsigned long long* out, int nwaves) {
   if (nwaves > 65536) nwaves = 65536;
-  hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(hb_wave_clk), 4 * sizeof(unsigned long long) * nwaves);
+  hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(hb_wave_clk), 8 * sizeof(unsigned long long) * nwaves);
   return e == hipSuccess ? 0 : -1;
 }
 #endif

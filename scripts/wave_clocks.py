@@ -33,17 +33,22 @@ for _ in range(a.reps):
     L.evaluate_dev(w, out, 0, st)
 torch.cuda.synchronize()
 lib = _lib.lib()
-buf = (C.c_ulonglong * (4 * w))()
+buf = (C.c_ulonglong * (8 * w))()
 assert lib.hb_debug_wave_clocks(buf, w) == 0
-c = np.frombuffer(buf, dtype=np.uint64).reshape(w, 4).astype(np.int64)
-t0, t1, hw, xcc = c[:, 0], c[:, 1], c[:, 2], c[:, 3]
+c = np.frombuffer(buf, dtype=np.uint64).reshape(w, 8).astype(np.int64)
+t0, t1, hw, xcc = c[:, 0], c[:, 4], c[:, 5], c[:, 6]
+marks = c[:, 1:4]
 simd = (hw >> 4) & 3
 cu = (hw >> 8) & 15
 se = (hw >> 13) & 7
 xid = xcc & 15
 key = ((xid * 8 + se) * 16 + cu) * 4 + simd
 life = t1 - t0
-res = {"waves": int(w), "life_mean": float(life.mean()), "life_min": int(life.min()), "life_max": int(life.max()),
+full = (marks > 0).all(axis=1)
+ph = np.diff(np.concatenate([t0[:, None], marks, t1[:, None]], axis=1), axis=1)[full]
+res = {"phase_names": ["model pass", "keys+minmax", "select", "chi2+epilogue"],
+       "phase_mean_cycles": [float(x) for x in ph.mean(axis=0)] if len(ph) else None,
+       "waves": int(w), "life_mean": float(life.mean()), "life_min": int(life.min()), "life_max": int(life.max()),
        "life_pct": [float(x) for x in np.percentile(life, [5, 25, 50, 75, 95])]}
 spans, occ, order = [], [], []
 for k in np.unique(key):
