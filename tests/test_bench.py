@@ -51,3 +51,40 @@ def test_config_defaults():
         assert "65536 walkers" in bench.workload_label(a, 1024, 8192, 8)
     finally:
         sys.argv = argv
+
+
+def test_roofline_uses_counters_of_this_build_only(tmp_path, monkeypatch):
+    """roofline(): with a PMC entry for this kernel build the bound is the fp64
+    VALU (counted flops over the timed duration, VALU-issue fraction, measured
+    HBM traffic) and the SURVEY 8(d) HBM figure moves to roofline.hbm; an
+    entry for another build is ignored (HBM figure primary, traffic null)."""
+    sys.path.insert(0, ROOT)
+    import bench
+    from hb_mcmc_amd._lib import kernel_build_id
+
+    bid = kernel_build_id()
+    prof = tmp_path / "profiles"
+    prof.mkdir()
+    entry = {"fp64_flop_per_call": 8.0e11, "hbm_bytes_per_call": 4.0e6, "valu_issue_cycles_per_call": 5.0e7,
+             "source": "profiles/x.json"}
+    (prof / "pmc_counters.json").write_text(json.dumps({bid: {"C2": entry}, "0" * 16: {"C3": entry}}))
+    monkeypatch.setattr(bench, "ROOT", str(tmp_path))
+    r = bench.roofline("C2", 0.04, 4096.0, 1.0e8, {"kernel_ms": 0.04})
+    assert r["bound"] == "valu" and r["unit"] == "TFLOP/s"
+    assert abs(r["achieved"] - 8.0e11 / 0.04e-3 / 1e12) < 1e-9
+    assert abs(r["frac"] - r["achieved"] / bench.FP64_PEAK_TFLOPS) < 1e-12
+    assert r["traffic"] == 4.0e6 and r["counters"]["build"] == bid
+    assert abs(r["valu_issue_frac"] - 5.0e7 / (bench.SIMDS * bench.CLOCK_HZ * 0.04e-3)) < 1e-12
+    assert abs(r["hbm"]["achieved"] - 1.0e8 / 0.04e-3 / 1e9) < 1e-6 and r["kernel_ms"] == 0.04
+    r3 = bench.roofline("C3", 0.9, 4096.0, 2.0e9, {})
+    assert r3["bound"] == "hbm" and r3["traffic"] is None and r3["counters"]["source"] is None
+
+
+def test_kernel_build_id_tracks_sources():
+    sys.path.insert(0, ROOT)
+    from hb_mcmc_amd import _lib
+
+    a = _lib.kernel_build_id()
+    assert len(a) == 16 and a == _lib.kernel_build_id()
+    for name in _lib.KERNEL_SOURCES:
+        assert os.path.exists(os.path.join(_lib.CSRC, name)), name
