@@ -258,6 +258,49 @@ def test_dropin_loglikelihood_mutates_noise(hbmi):
     assert np.abs(out - g["templates"][0]).max() <= lc_tol(pv[3])
 
 
+def test_dropin_concurrent_calls_are_combined_exactly(hbmi):
+    """The drop-in combines concurrent loglikelihood() calls on one light curve
+    into batched launches (hb_capi.hip dropin_loglik): 16 threads x 24 calls
+    (ctypes releases the GIL) give each caller exactly the value a lone call
+    gives, and two light curves in flight at once keep their own contexts."""
+    import threading
+
+    g = golden("lc_synth1024.npz")
+    t, f, s = g["t"].copy(), g["f"].copy(), g["s"].copy()
+    t2 = t[:883].copy()
+    f2, s2 = f[:883].copy(), s[:883].copy()
+    mag, err = g["mag"].copy(), g["magerr"].copy()
+    P = np.ascontiguousarray(g["params"][:24])
+    solo = [hbmi.loglikelihood(p(t), p(f), p(s), len(t), p(P[i].copy()), p(mag), p(err)) for i in range(24)]
+    solo2 = [hbmi.loglikelihood(p(t2), p(f2), p(s2), len(t2), p(P[i].copy()), p(mag), p(err)) for i in range(24)]
+    res, res2, errs = {}, {}, []
+
+    def worker(k):
+        try:
+            for r in range(24):
+                i = (k * 7 + r) % 24
+                pv = P[i].copy()
+                if (k + r) % 3 == 0:
+                    res2[(k, r)] = (i, hbmi.loglikelihood(p(t2), p(f2), p(s2), len(t2), p(pv), p(mag), p(err)))
+                else:
+                    res[(k, r)] = (i, hbmi.loglikelihood(p(t), p(f), p(s), len(t), p(pv), p(mag), p(err)))
+        except Exception as e:  # pragma: no cover
+            errs.append(e)
+
+    th = [threading.Thread(target=worker, args=(k,)) for k in range(16)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    assert not errs
+    assert len(res) + len(res2) == 16 * 24
+    for i, v in res.values():
+        assert v == solo[i] or (np.isnan(v) and np.isnan(solo[i]))
+    for i, v in res2.values():
+        assert v == solo2[i] or (np.isnan(v) and np.isnan(solo2[i]))
+    close_logl(solo, g["logl"][:24])
+
+
 # ------------------------------------------------- full-size (config C2)
 def test_full_size_c2_against_oracle_and_properties(hbmi, oracle):
     """W=4096, N=1024: oracle on a 256-walker sample; size-independent
