@@ -79,6 +79,9 @@ enum ProbeOp {
 };
 
 EvalPlan make_plan(long n);
+// the multi-wave plan for any n (the batched path's choice above 2048 cadences,
+// and the latency plan of small batches below)
+EvalPlan make_block_plan(long n);
 // 90th percentile of |t[i+1] - t[i]| (host; the eval kernel's warm-chain gate)
 double cadence_gap(const double* t, long n);
 // forces the load of hb_kernels.hip's code object on the current device

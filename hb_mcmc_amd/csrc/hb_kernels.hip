@@ -2145,6 +2145,15 @@ EvalPlan make_plan(long n) {
     pl.lds_bytes = wave_lds_bytes(pl.slab_bytes, pl.vpt);
     return pl;
   }
+  return make_block_plan(n);
+}
+
+// NW waves per walker (N > 2048; for N <= 2048 the latency plan of small
+// batches, hb_capi.hip run_batch): the walker's cadences over more SIMDs
+EvalPlan make_block_plan(long n) {
+  EvalPlan pl;
+  pl.n = n;
+  pl.kth = (n % 2 == 0) ? n / 2 : n / 2 + 1;  // likelihood3.c:97-99
   const size_t lds_cap = 163840;
   const size_t need = sizeof(SelShared) + (size_t)n * sizeof(double);
   if (need <= lds_cap) {

@@ -32,7 +32,7 @@ def _p(a: np.ndarray):
 
 
 class HBLikelihood:
-    def __init__(self, t, flux, sigma, mag_data=None, magerr=None, device: int = 0):
+    def __init__(self, t, flux, sigma, mag_data=None, magerr=None, device: int = 0, latency_plan: bool = False):
         self.lib = _lib.lib()
         t, flux, sigma = _f64(t), _f64(flux), _f64(sigma)
         if not (t.shape == flux.shape == sigma.shape) or t.ndim != 1:
@@ -49,6 +49,8 @@ class HBLikelihood:
         if not h:
             raise _lib.HBMIError("hb_create: " + _lib.last_error())
         self._h = C.c_void_p(h)
+        if latency_plan:  # multi-wave kernel for batches < 512 walkers (hb_ctx_set_latency_plan)
+            self.lib.hb_ctx_set_latency_plan(self._h, 1)
 
     # -- bookkeeping --
     def close(self):

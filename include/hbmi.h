@@ -163,6 +163,14 @@ int hb_ctx_template_in_lds(const hb_ctx *ctx);
  * per walker), 1 hb_eval_block_kernel (register keys, N <= 32 x 64 x waves),
  * 2 hb_eval_kernel (LDS-walking select; template in LDS or an HBM slab). */
 int hb_ctx_eval_kind(const hb_ctx *ctx);
+/* on != 0: batches of fewer than 512 walkers (N <= 2048) run the multi-wave
+ * kernel (several waves per walker: lower latency when most SIMDs would sit
+ * idle).  Default off: one wave per walker at every batch size, which keeps a
+ * context's results bit-identical across batch sizes and with the device
+ * sampler (the two kernels sum chi2 in different orders; both within the
+ * stated tolerance of likelihood3.c).  The drop-in loglikelihood() turns it on
+ * for its cached contexts.  Returns 0. */
+int hb_ctx_set_latency_plan(hb_ctx *ctx, int on);
 
 /* Last error message of the calling thread ("" if none). */
 const char *hb_last_error(void);

@@ -138,12 +138,15 @@ def test_median_sort_partition_exact(hbmi):
 LC_FIXTURES = ["lc_synth1024.npz", "lc_synth7.npz", "lc_real231937440.npz"]
 
 
+@pytest.mark.parametrize("latency", [True, False], ids=["small-batch-plan", "one-wave-plan"])
 @pytest.mark.parametrize("name", LC_FIXTURES)
-def test_batched_templates_and_logl(hbmi, name):
+def test_batched_templates_and_logl(hbmi, name, latency):
+    """Small batches take the multi-wave latency plan by default; the one-wave
+    kernel (every batch of 512+ walkers) is checked on the same goldens."""
     from hb_mcmc_amd.likelihood import HBLikelihood
 
     g = golden(name)
-    with HBLikelihood(g["t"], g["f"], g["s"], g["mag"], g["magerr"]) as L:
+    with HBLikelihood(g["t"], g["f"], g["s"], g["mag"], g["magerr"], latency_plan=latency) as L:
         tm = L.light_curve(g["params"])
         ll = L.loglike(g["params"])
     ref_t = g["templates"]
@@ -192,8 +195,9 @@ def test_block_kernel_sizes(hbmi, oracle, n):
     assert (np.abs(tm - ref) <= tol).all()
 
 
+@pytest.mark.parametrize("latency", [True, False], ids=["small-batch-plan", "one-wave-plan"])
 @pytest.mark.parametrize("n", [1024, 6001])
-def test_phase_table_and_direct_paths(hbmi, oracle, n):
+def test_phase_table_and_direct_paths(hbmi, oracle, n, latency):
     """Walkers on the batch's table period (walker 0's P) take the phase-table
     Kepler start, the others the direct sincos; both against the oracle, and a
     walker's logL agrees whichever path it takes.  T0 = 0 and T0 = t_k put
@@ -209,7 +213,7 @@ def test_phase_table_and_direct_paths(hbmi, oracle, n):
     P[9, 3] = 0.6  # larger steps: direct sincos inside the Newton loop
     Q = P.copy()
     Q[0, 2] += 2e-3  # walker 0 moves: now every other walker is off the table period
-    with HBLikelihood(t, f, s) as L:
+    with HBLikelihood(t, f, s, latency_plan=latency) as L:
         a = L.loglike(P)
         b = L.loglike(Q)
         tm = L.light_curve(P)
@@ -220,11 +224,12 @@ def test_phase_table_and_direct_paths(hbmi, oracle, n):
     assert (np.abs(tm - oracle.light_curve_batch(t, P, 8)) <= tol).all()
 
 
-def test_real_1861_cadences(hbmi):
+@pytest.mark.parametrize("latency", [True, False], ids=["small-batch-plan", "one-wave-plan"])
+def test_real_1861_cadences(hbmi, latency):
     from hb_mcmc_amd.likelihood import HBLikelihood
 
     g = golden("lc_real237957506.npz")
-    with HBLikelihood(g["t"], g["f"], g["s"], g["mag"], g["magerr"]) as L:
+    with HBLikelihood(g["t"], g["f"], g["s"], g["mag"], g["magerr"], latency_plan=latency) as L:
         close_logl(L.loglike(g["params"]), g["logl"])
 
 
