@@ -36,6 +36,15 @@ struct Event {  // LogSuspiciousJumps (:520-528) arguments
 // A sampler may own only the slots [lo, lo + nl) of the W-slot ladder (one
 // rank of a sharded run): arrays "by slot" hold those nl slots (local index
 // j - lo), arrays "by chain" and idx/temp keep all W entries.
+constexpr int kEvalOrdMax = 8192;  // walkers the prep launch orders by e (AccArgs::ord)
+constexpr int kOrdBins = 64;
+// e bin of a proposal, descending e -> ascending bin (NaN -> last)
+__device__ __forceinline__ int e_bin_desc(double e) {
+  const double q = e * kOrdBins;
+  const int b = q >= 0.0 ? (q < (double)kOrdBins ? (int)q : kOrdBins - 1) : 0;
+  return kOrdBins - 1 - b;
+}
+
 struct AccArgs {
   const int* idx;      // [W] slot -> chain
   double* logL;        // [W] by chain
@@ -55,6 +64,8 @@ struct AccArgs {
   long long iter;
   int lo;              // first owned slot
   int pad;
+  int* ord;            // [nl] eval wave -> local slot (null: wave w takes slot w); the prep launch writes it
+  const unsigned char* ebin;  // [nl] e_bin_desc of each proposal (ds_propose), the key of ord
 };
 
 // Everything the Hastings test of local slot j reads besides the new logL.

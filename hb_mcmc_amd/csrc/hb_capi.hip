@@ -20,6 +20,7 @@
 #include <algorithm>
 #include <vector>
 
+#include "hb_accept.hpp"
 #include "hb_device.hpp"
 #include "hb_internal.hpp"
 
@@ -328,7 +329,8 @@ static int run_batch(hb_ctx* c, const double* d_params, int w, double* d_logl, d
     int rc = hb_reserve(c, w);
     if (rc) return rc;
   }
-  HB_TRY(hbk::launch_prep(d_params, w, c->mags, c->d_wc, s, nullptr, nullptr, c->d_t, c->plan.n, c->d_ph),
+  HB_TRY(hbk::launch_prep(d_params, w, c->mags, c->d_wc, s, nullptr, nullptr, c->d_t, c->plan.n, c->d_ph, nullptr, 0,
+                          acc != nullptr ? acc->ord : nullptr, acc != nullptr ? acc->ebin : nullptr),
          "hb_prep_kernel");
   const EvalPlan& pl = (acc == nullptr && c->has_lat && w < kLatencyW) ? c->lat : c->plan;
   HB_TRY(hbk::launch_eval(pl, c->d_t, c->d_ph, c->d_f, c->d_s, c->d_rows, c->d_wc, w, d_logl, d_tmpl, c->d_scratch,

@@ -110,6 +110,8 @@ struct Dev {
   int* logP_ok;    // [W] by chain
   int* idx;        // [W] slot -> chain
   int* order;      // [nl] propose wave -> (global) slot, hottest rungs first (dispatch order)
+  int* eord;       // [nl] eval wave -> local slot, by descending e of the proposal (written by the prep launch)
+  unsigned char* ebin;  // [nl] e bin of each proposal (e_bin_desc), the key of eord
   double* temp;    // [W]
   int* idum;       // [nl] ran2 state by slot
   int* idum2;
@@ -492,6 +494,7 @@ __global__ __launch_bounds__(64 * kPW) void ds_propose(Dev D, int W, int NPAST, 
   const double alpha2 = S.uniform();  // drawn after the likelihood calls in the reference; same stream order
   S.slide();
   if (lane < kNp) D.y[(size_t)jl * kNp + lane] = yn;
+  if (lane == 3) D.ebin[jl] = (unsigned char)e_bin_desc(yn);  // the eval order's key (hb_prep_kernel)
   if (lane < NTAB) D.iv[(size_t)jl * NTAB + lane] = S.b_tab;
   if (lane == 0) {
     D.logPy[jl] = lpy;
@@ -855,6 +858,7 @@ struct hb_dsampler {
   // nlmin = smallest (edge windows are capped at it)
   int lo = 0, nl = 0, R = 1, rank = 0, m = 0, nlmin = 0;
   bool lds_swap = true;
+  bool no_eord = getenv("HB_DS_NO_EORD") != nullptr;  // experiment knob: eval waves in slot order
   size_t swap_lds = 0;
   std::vector<void*> allocs;
   // swap schedules: pinned ring -> device ring, copied on their own stream
@@ -965,6 +969,7 @@ static hb_dsampler* ds_create(hb_sampler* s, hb_ctx* ctx, const int* chain_of_sl
   // by chain / ladder: W entries; by slot: the nl owned slots
   if ((e = d->alloc(&D.x, Wz * kNp)) || (e = d->alloc(&D.logL, Wz)) || (e = d->alloc(&D.logP, Wz)) ||
       (e = d->alloc(&D.logP_ok, Wz)) || (e = d->alloc(&D.idx, Wz)) || (e = d->alloc(&D.order, Nz)) ||
+      (e = d->alloc(&D.eord, Nz)) || (e = d->alloc(&D.ebin, Nz)) ||
       (e = d->alloc(&D.temp, Wz)) || (e = d->alloc(&D.idum, Nz)) || (e = d->alloc(&D.idum2, Nz)) ||
       (e = d->alloc(&D.iy, Nz)) || (e = d->alloc(&D.iset, Nz)) || (e = d->alloc(&D.gset, Nz)) ||
       (e = d->alloc(&D.cts, Nz)) || (e = d->alloc(&D.iv, Nz * NTAB)) || (e = d->alloc(&D.y, Nz * kNp)) ||
@@ -1289,7 +1294,8 @@ static long ds_begin(hb_dsampler* d, long iter, double* send, long cap) {
   // likelihood with the Hastings test fused into its waves' epilogue
   // (hb_accept.hpp); ds_accept only where the plan has no one-wave kernel
   const AccArgs acc{D.idx, D.logL, D.logP, D.logPy, D.temp, D.alpha2, D.jump, D.jtype, D.x, D.y, D.hist,
-                    D.DEacc_arr, D.ctr, D.ev, d->P.log_on, NPAST, (long long)iter, d->lo, 0};
+                    D.DEacc_arr, D.ctr, D.ev, d->P.log_on, NPAST, (long long)iter, d->lo, 0,
+                    (nl <= kEvalOrdMax && !d->no_eord) ? D.eord : nullptr, D.ebin};
   int rc = hbx_loglik_accept_dev(d->ctx, D.y, nl, D.logLy, &acc, (void*)s);
   if (rc == 1) {
     rc = hb_loglik_batch_dev(d->ctx, D.y, nl, D.logLy, (void*)s);

@@ -90,10 +90,13 @@ hipError_t preload_code_object();
 // DAY 2pi/P) for P = the period of the light curve's first walker (walker 0,
 // or catalog target k's w0[k]), written here and read by the eval launch;
 // walkers with another period get tab = 0
+// ord (optional, nwalk <= hbds::kEvalOrdMax): one more workgroup writes the
+// walkers by descending e (eccentricity) for the eval launch's waves, from the
+// bins ebin[w] = hbds::e_bin_desc(params[w][3]) the caller wrote
 hipError_t launch_prep(const double* d_params, int nwalk, const MagArgs& ma, hbdev::WalkerConst* d_wc,
                        hipStream_t s, const TargetDesc* tab = nullptr, const int* wt = nullptr,
                        const double* t = nullptr, long n = 0, double2* ph = nullptr, const int* w0 = nullptr,
-                       int ntargets = 0);
+                       int ntargets = 0, int* ord = nullptr, const unsigned char* ebin = nullptr);
 // catalog mode: walkers list[0..count) of one size class (cadences per lane
 // vpt), each reading its target's slice through tab[wt[walker]]
 hipError_t launch_eval_multi(int vpt, size_t slab_bytes, const double* t, const double2* ph, const double* f,

@@ -128,6 +128,52 @@ __device__ __forceinline__ void sincos_table(double x, double& sv, double& cv) {
   }
 }
 
+// Eval order by descending e, written by one extra prep workgroup (device
+// sampler).  The eval launch is one resident round of waves, four per SIMD,
+// so it lasts as long as the SIMD whose walkers cost most; cost follows e
+// (high e leaves the warm Kepler chains for the cold path).  Waves taking the
+// walkers by descending e give every SIMD walkers from the whole e range
+// (sampler states of a 200-iteration run: 53 us in slot order, 47 us sorted).
+// A counting sort over 64 bins of the bytes ds_propose wrote (contiguous: the
+// one workgroup does not gather the scattered parameter rows): LDS counters,
+// one wave scan, one scatter; the order within a bin is immaterial (each
+// wave's result depends on its walker only).
+__device__ void order_by_e(const unsigned char* __restrict__ ebin, int nwalk, int* __restrict__ ord) {
+  using hbds::kOrdBins;
+  __shared__ int cnt[kOrdBins];
+  const int tid = threadIdx.x;
+  constexpr int T = kPrepThreads, U = (hbds::kEvalOrdMax + T - 1) / T;
+  if (tid < kOrdBins) cnt[tid] = 0;
+  int b[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int j = tid + u * T;
+    b[u] = j < nwalk ? ebin[j] : 0;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+    if (tid + u * T < nwalk) atomicAdd(&cnt[b[u]], 1);
+  __syncthreads();
+  if (tid < kOrdBins) {  // exclusive scan by wave 0 (lane = bin): first position of each bin
+    const int v = cnt[tid];
+    int incl = v;
+#pragma unroll
+    for (int d = 1; d < kOrdBins; d <<= 1) {
+      const int o = __shfl_up(incl, d);
+      if (tid >= d) incl += o;
+    }
+    cnt[tid] = incl - v;
+  }
+  __syncthreads();
+  int q[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) q[u] = tid + u * T < nwalk ? atomicAdd(&cnt[b[u]], 1) : 0;
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+    if (tid + u * T < nwalk) ord[q[u]] = tid + u * T;
+}
+
 __global__ __launch_bounds__(kPrepThreads) void hb_prep_kernel(const double* __restrict__ params,
                                                               int nwalk, MagArgs ma,
                                                               WalkerConst* __restrict__ out,
@@ -135,9 +181,16 @@ __global__ __launch_bounds__(kPrepThreads) void hb_prep_kernel(const double* __r
                                                               const int* __restrict__ wt,
                                                               const double* __restrict__ tcad, int ncad,
                                                               double2* __restrict__ ph,
-                                                              const int* __restrict__ w0, int ntargets) {
+                                                              const int* __restrict__ w0, int ntargets,
+                                                              int* __restrict__ ord,
+                                                              const unsigned char* __restrict__ ebin) {
   __shared__ double sp[kPrepWalkers * kNpars];
   __shared__ double so[kPrepWalkers * kWcDoubles];
+  const int G = (int)gridDim.x - (ord != nullptr ? 1 : 0);  // walker blocks; the order block is the last
+  if (ord != nullptr && (int)blockIdx.x == G) {           // workgroup-uniform
+    order_by_e(ebin, nwalk, ord);
+    return;
+  }
   // per-star results: [star][item][walker]; items 0 m, 1 r, 2 tk, 3 ab, 4..15 star-2 terms
   __shared__ double xs[2][16][kPrepWalkers];
   __shared__ double gs[3][kPrepWalkers];  // wave 2's Gaia term and sin/cos omega
@@ -154,7 +207,7 @@ __global__ __launch_bounds__(kPrepThreads) void hb_prep_kernel(const double* __r
   // wave 2's first phase-table operands (single context), in flight with the parameters
   double t_first = 0.0, lp0 = 0.0;
   if (ph != nullptr && tab == nullptr && tid >= 2 * kPrepWalkers && tid < 3 * kPrepWalkers) {
-    const int i0 = blockIdx.x + gridDim.x * (tid - 2 * kPrepWalkers);
+    const int i0 = blockIdx.x + G * (tid - 2 * kPrepWalkers);
     if (i0 < ncad) t_first = tcad[i0];
     lp0 = params[2];
   }
@@ -320,7 +373,6 @@ __global__ __launch_bounds__(kPrepThreads) void hb_prep_kernel(const double* __r
     // loaded at kernel start)
     if (ph != nullptr && tab == nullptr) {
       const double mA0 = kTwoPi / (exp10(lp0) * kDay);
-      const int G = gridDim.x;
       double ti = t_first;
       for (int i = blockIdx.x + G * j; i < ncad; i += G * kPrepWalkers) {
         double sv, cv;
@@ -397,7 +449,7 @@ __global__ __launch_bounds__(kPrepThreads) void hb_prep_kernel(const double* __r
   // context's table is written by wave 2 above.)
   if (ph && tab != nullptr) {
     {
-      for (int k = blockIdx.x; k < ntargets; k += gridDim.x) {
+      for (int k = blockIdx.x; k < ntargets; k += G) {
         if (w0[k] < 0) continue;
         const double mA0 = kTwoPi / (exp10(params[(size_t)w0[k] * kNpars + 2]) * kDay);
         const long off = tab[k].off;
@@ -1319,6 +1371,7 @@ __global__ __launch_bounds__(64 * WPB) HB_WPE_ATTR void hb_eval_wave_kernel(
   const bool valid = WPB == 1 || slot < count;
   unsigned char* smem = smem_all + (size_t)wib * (size_t)lds_per;
   int wv = slot;
+  if (ACC && hst.ord != nullptr) wv = hst.ord[slot];  // device sampler: slots by descending e (ds_propose)
   if (MULTI && valid) {
     wv = list[slot];
     const TargetDesc& td = tab[wt[wv]];
@@ -1842,11 +1895,13 @@ __global__ __launch_bounds__(1024) void hb_sort_step_kernel(uint64_t* __restrict
 // ---------------------------------------------------------------------------
 hipError_t launch_prep(const double* d_params, int nwalk, const MagArgs& ma, WalkerConst* d_wc,
                        hipStream_t s, const TargetDesc* tab, const int* wt, const double* t, long n,
-                       double2* ph, const int* w0, int ntargets) {
+                       double2* ph, const int* w0, int ntargets, int* ord, const unsigned char* ebin) {
   if (nwalk <= 0) return hipSuccess;
   if (t == nullptr || (tab != nullptr && w0 == nullptr) || !HB_PHASE_TAB) ph = nullptr;
-  hipLaunchKernelGGL(hb_prep_kernel, dim3((nwalk + kPrepWalkers - 1) / kPrepWalkers), dim3(kPrepThreads), 0, s,
-                     d_params, nwalk, ma, d_wc, tab, wt, t, (int)n, ph, w0, ntargets);
+  if (nwalk > hbds::kEvalOrdMax || ebin == nullptr) ord = nullptr;
+  const int nb = (nwalk + kPrepWalkers - 1) / kPrepWalkers;
+  hipLaunchKernelGGL(hb_prep_kernel, dim3(nb + (ord != nullptr ? 1 : 0)), dim3(kPrepThreads), 0, s,
+                     d_params, nwalk, ma, d_wc, tab, wt, t, (int)n, ph, w0, ntargets, ord, ebin);
   return hipGetLastError();
 }
 
