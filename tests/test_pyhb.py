@@ -1,9 +1,16 @@
 """hb_mcmc_amd.pyHB against outputs of the REFERENCE Cython module pyHB
-(compiled from src/pyHB.pyx; captured in tests/golden/pyhb.npz)."""
+(compiled from src/pyHB.pyx; captured in tests/golden/pyhb.npz), and
+INTEGRATION.md Option B (the reference pyHB.pyx relinked against libhbmi.so)."""
+import os
+import subprocess
+import sys
+
 import numpy as np
 import pytest
 
-from conftest import golden
+from conftest import ROOT, golden
+
+REF_PYX = "/root/reference/src/pyHB.pyx"
 
 
 def test_parspace_boxes_and_pinning():
@@ -55,3 +62,38 @@ def test_pyhb_surface_matches_reference_module(hbmi):
     rl = np.array([[pyHB.test_roche_lobe(list(p) + [0.0]), pyHB.test_roche_lobe(list(p) + [0.0], "Eggleton")]
                    for p in P])
     assert np.allclose(rl, g["roche"], rtol=1e-12, atol=0)
+
+
+def test_option_b_reference_pyhb_relinked_against_libhbmi(tmp_path):
+    """INTEGRATION.md section 4, Option B: the reference's pyHB.pyx, unmodified,
+    compiled against include/hbmi.h (oracle/pyhb_hbmi/likelihood3.pxd) and
+    linked to libhbmi.so.  Built here in a temporary directory (the module
+    embeds the reference's source, so it never travels to the GPU box): it
+    imports, its seven likelihood3 entry points resolve from libhbmi.so, and
+    without a GPU a call fails loudly instead of falling back to the CPU."""
+    if not os.path.exists(REF_PYX):
+        pytest.skip("the reference sources exist in the development container only")
+    out = str(tmp_path / "pyhb_hbmi")
+    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "pyhb_hbmi", f"PYHB_HBMI_DIR={out}"],
+                   check=True, capture_output=True, timeout=600)
+    so = [f for f in os.listdir(out) if f.startswith("pyHB") and f.endswith(".so")]
+    assert len(so) == 1
+    und = subprocess.run(["nm", "-D", "--undefined-only", os.path.join(out, so[0])], capture_output=True,
+                         text=True, check=True).stdout.split()
+    entry = ["calc_light_curve", "calc_radii_and_Teffs", "calc_mags", "_getT", "_getR", "envelope_Radius",
+             "envelope_Temp"]
+    assert all(e in und for e in entry)
+    libs = subprocess.run(["ldd", os.path.join(out, so[0])], capture_output=True, text=True, check=True).stdout
+    assert os.path.join(ROOT, "hb_mcmc_amd", "lib", "libhbmi.so") in libs
+    probe = ("import sys; sys.path.insert(0, %r); import pyHB; "
+             "names = ['lightcurve3', 'calc_mags', 'calc_radii_and_Teffs', 'getR', 'getT', 'envelope_Temp', "
+             "'envelope_Radius', 'likelihood', 'parspace', 'test_roche_lobe']; "
+             "print('missing', [n for n in names if not hasattr(pyHB, n)], flush=True)" % out)
+    r = subprocess.run([sys.executable, "-c", probe], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "missing []" in r.stdout, r.stderr[-2000:]
+    from hb_mcmc_amd import _lib
+
+    if not _lib.device_available():
+        r = subprocess.run([sys.executable, "-c", probe + "; pyHB.getR(0.1)"], capture_output=True, text=True,
+                           timeout=300)
+        assert r.returncode != 0 and "no HIP device" in r.stderr
