@@ -174,8 +174,18 @@ HBW_FN double apply_wall(double v, double lo, double hi, double fl, double fh) {
                           : mode == kFfBinade ? bottom * (1.0 - 0x1p-53)  // |v| >= bottom
                                               : edge - lim2 - edge * 0x1p-48;
       const int smax = mode >= kFfBinade ? kGuard : 16;
-      for (int s = 0; guard < kGuard && (v < lo || v > hi) && (s < 4 || (s < smax && fabs(v) > stop)); ++s, ++guard)
-        v = (v < lo ? lo2 : hi2) - v;
+      // the plain loop's folds, two per trip: the second is taken under the
+      // same test, so the sequence and the count are unchanged, and a GPU
+      // lane pays one exec-mask branch per two dependent folds
+      for (int s = 0;;) {
+        if (!(guard < kGuard && (v < lo || v > hi) && (s < 4 || (s < smax && fabs(v) > stop)))) break;
+        const double v1 = (v < lo ? lo2 : hi2) - v;
+        const bool two = guard + 1 < kGuard && (v1 < lo || v1 > hi) && (s + 1 < 4 || (s + 1 < smax && fabs(v1) > stop));
+        v = two ? (v1 < lo ? lo2 : hi2) - v1 : v1;
+        s += two ? 2 : 1;
+        guard += two ? 2 : 1;
+        if (!two) break;
+      }
     }
   } else {
     for (; guard < kGuard; ++guard) {
