@@ -360,7 +360,18 @@ __device__ double gauss_batch(WaveStream& S, int& iset, double& gset, const hbgl
 // hot rungs' long wall runs are dispatched first, and a workgroup's waves
 // (spread over its CU's SIMDs) share each SIMD with colder slots of the CU's
 // later workgroups (measured 37.5 -> 35.2 us against order[b + w grid]).
-__global__ __launch_bounds__(64 * kPW) void ds_propose(Dev D, int W, int NPAST, long long iter) {
+// The iteration's swap schedule (n8 words) is copied from the pinned ring
+// entry into its device ring entry on the way (the coldest slots' waves, which
+// finish first, issue the reads; system-scope loads bypass the GPU caches),
+// so ds_swap depends on nothing outside this stream: a separate copy stream
+// cost an inter-queue event wait of ~10 us per iteration before ds_swap.
+__global__ __launch_bounds__(64 * kPW) void ds_propose(Dev D, int W, int NPAST, long long iter,
+                                                       const unsigned long long* __restrict__ sch_src,
+                                                       unsigned long long* __restrict__ sch_dst, long long n8) {
+  const long long sgt = (long long)(gridDim.x - 1 - blockIdx.x) * blockDim.x + threadIdx.x;
+  const long long sgs = (long long)gridDim.x * blockDim.x;
+  unsigned long long sv = 0;
+  if (sgt < n8) sv = __hip_atomic_load(sch_src + sgt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   __shared__ uint64_t tab_s[hbglibc::kTabWords];  // exp / log / pow tables (divergent lookups)
   __shared__ double gs_s[kPW][32];
   const Params* P = D.P;
@@ -404,6 +415,9 @@ __global__ __launch_bounds__(64 * kPW) void ds_propose(Dev D, int W, int NPAST, 
   WaveStream S;
   S.init(D.idum[jl], D.idum2[jl], D.iy[jl], lane < NTAB ? D.iv[(size_t)jl * NTAB + lane] : 0);
   __syncthreads();  // tables staged
+  if (sgt < n8) sch_dst[sgt] = sv;
+  for (long long q = sgt + sgs; q < n8; q += sgs)
+    sch_dst[q] = __hip_atomic_load(sch_src + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 #if HB_DS_ABL == 4
   return;
 #endif
@@ -859,6 +873,7 @@ struct hb_dsampler {
   int lo = 0, nl = 0, R = 1, rank = 0, m = 0, nlmin = 0;
   bool lds_swap = true;
   bool no_eord = getenv("HB_DS_NO_EORD") != nullptr;  // experiment knob: eval waves in slot order
+  bool copy_stream = getenv("HB_DS_COPY_STREAM") != nullptr;  // A/B knob: schedule copy on cst (old path)
   size_t swap_lds = 0;
   std::vector<void*> allocs;
   // swap schedules: pinned ring -> device ring, copied on their own stream
@@ -1284,12 +1299,16 @@ static long ds_begin(hb_dsampler* d, long iter, double* send, long cap) {
     e.lnb = log(d->beta[i]);
     betas[q] = d->beta[i];
   }
-  const size_t used_bytes = sched_beta_off(W) + sizeof(double) * (size_t)W;
-  DS_TRY(hipMemcpyAsync(d->d_sched[r], d->pin[r], used_bytes, hipMemcpyHostToDevice, d->cst), "schedule upload");
-  DS_TRY(hipEventRecord(d->ev_copy[r], d->cst), "schedule ring");
+  const size_t used_bytes = sched_beta_off(W) + sizeof(double) * (size_t)W;  // a multiple of 8
+  if (d->copy_stream) {
+    DS_TRY(hipMemcpyAsync(d->d_sched[r], d->pin[r], used_bytes, hipMemcpyHostToDevice, d->cst), "schedule upload");
+    DS_TRY(hipEventRecord(d->ev_copy[r], d->cst), "schedule ring");
+  }
 
   const int NPAST = d->NPAST, nl = d->nl;
-  ds_propose<<<(nl + kPW - 1) / kPW, 64 * kPW, 0, s>>>(D, W, NPAST, (long long)iter);
+  ds_propose<<<(nl + kPW - 1) / kPW, 64 * kPW, 0, s>>>(
+      D, W, NPAST, (long long)iter, reinterpret_cast<const unsigned long long*>(d->pin[r]),
+      reinterpret_cast<unsigned long long*>(d->d_sched[r]), d->copy_stream ? 0LL : (long long)(used_bytes / 8));
   DS_TRY(hipGetLastError(), "ds_propose");
   // likelihood with the Hastings test fused into its waves' epilogue
   // (hb_accept.hpp); ds_accept only where the plan has no one-wave kernel
@@ -1335,7 +1354,7 @@ static int ds_end(hb_dsampler* d, long iter, const double* recv, long n) {
   const SwapEnt* d_ent = reinterpret_cast<const SwapEnt*>(d->d_sched[r]);
   const int* d_off = reinterpret_cast<const int*>(d->d_sched[r] + sizeof(SwapEnt) * (size_t)W);
   const Gathered X{d->R > 1 ? recv : nullptr, (long long)n, d->R, d->rank, d->m, 0};
-  DS_TRY(hipStreamWaitEvent(s, d->ev_copy[r], 0), "schedule wait");
+  if (d->copy_stream) DS_TRY(hipStreamWaitEvent(s, d->ev_copy[r], 0), "schedule wait");
   if (d->lds_swap)
     ds_swap<true><<<1, kSwapThreads, d->swap_lds, s>>>(D, W, d_ent, d_off, nlv, (long long)iter, X);
   else
