@@ -70,7 +70,10 @@ constexpr int kBlk = 64;                   // slots per workgroup of the gather 
 #define HB_DS_KPW 4
 #endif
 constexpr int kPW = HB_DS_KPW;             // propose waves (one slot each) per workgroup
-constexpr int kSwapThreads = 1024;
+#ifndef HB_DS_SWAPT  // experiment knob: ds_swap workgroup size
+#define HB_DS_SWAPT 1024
+#endif
+constexpr int kSwapThreads = HB_DS_SWAPT;
 constexpr int kMaxLevels = 255;            // swap levels staged in LDS (W = 4096 needs ~10)
 
 // run constants (kernel argument)
