@@ -94,7 +94,7 @@ void runtime_init() {
         (void)hipFree(nullptr);  // context creation
         (void)hbk::preload_code_object();  // hb_kernels.hip's code object
         hipFuncAttributes a;
-        (void)hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&hb_capi_anchor_kernel));  // this file's (hipCUB)
+        (void)hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&hb_capi_anchor_kernel));  // this file's code object
         // the runtime's own blit kernels (copy/fill) load on first use, also through comgr
         double h[64] = {0}, *d0 = nullptr, *d1 = nullptr;
         if (hipMalloc(&d0, sizeof h) == hipSuccess && hipMalloc(&d1, sizeof h) == hipSuccess) {
