@@ -151,12 +151,13 @@ extern "C" void hb_timer_destroy(void* t) {
 // ---------------------------------------------------------------------------
 // Batches of fewer than kLatencyW walkers leave most SIMDs empty under the
 // one-wave-per-walker plan, and each walker's wave runs alone (latency-bound);
-// the multi-wave plan (NW waves per walker) finishes them sooner.  The
-// drop-in's combined loglikelihood() batches (<= ~25 walkers): 990 -> 1380
-// sampler iterations/s.  Opt-in (hb_ctx_set_latency_plan; the drop-in turns it
-// on): the two kernels sum chi2 in different orders, and a context's results
-// stay bit-identical across batch sizes and with the device sampler only on
-// one plan.
+// the multi-wave plan (NW waves per walker) finishes them sooner: 18.6 vs
+// 23.7 us per call at N = 756 (profiles/r02e_latency_probe.txt).  Opt-in only
+// (hb_ctx_set_latency_plan / HBLikelihood(latency_plan=True)): the drop-in
+// keeps the one-wave plan, since the relinked reference sampler is bound by
+// its host threads (no measurable gain in iterations/s), and the two kernels
+// sum chi2 in different orders -- a context's results stay bit-identical
+// across batch sizes and with the device sampler only on one plan.
 constexpr int kLatencyW = 512;
 
 struct hb_ctx {
@@ -174,6 +175,7 @@ struct hb_ctx {
   int cap = 0;
   WalkerConst* d_wc = nullptr;
   double* d_scratch = nullptr;   // cap x n (only when the template does not fit LDS)
+  double* d_dq = nullptr;        // the one-wave kernel's deferred cadence queue, cap walkers
   // host-API staging
   int hcap = 0;
   size_t hout = 0;               // elements in d_out
@@ -187,8 +189,10 @@ extern "C" int hbx_ctx_device(const hb_ctx* c) { return c ? c->device : 0; }
 static int ctx_release_ws(hb_ctx* c) {
   if (c->d_wc) (void)hipFree(c->d_wc);
   if (c->d_scratch) (void)hipFree(c->d_scratch);
+  if (c->d_dq) (void)hipFree(c->d_dq);
   c->d_wc = nullptr;
   c->d_scratch = nullptr;
+  c->d_dq = nullptr;
   c->cap = 0;
   return 0;
 }
@@ -202,6 +206,8 @@ extern "C" int hb_reserve(hb_ctx* c, int max_walkers) {
   if (!c->plan.lds)
     HB_TRY(hipMalloc(&c->d_scratch, sizeof(double) * (size_t)max_walkers * (size_t)c->plan.n),
            "hipMalloc(template scratch)");
+  const size_t qb = c->plan.vpt > 0 ? hbk::wave_queue_bytes(c->plan.vpt, max_walkers) : 0;
+  if (qb) HB_TRY(hipMalloc(&c->d_dq, qb), "hipMalloc(deferred cadence queue)");
   c->cap = max_walkers;
   return 0;
 }
@@ -334,7 +340,7 @@ static int run_batch(hb_ctx* c, const double* d_params, int w, double* d_logl, d
          "hb_prep_kernel");
   const EvalPlan& pl = (acc == nullptr && c->has_lat && w < kLatencyW) ? c->lat : c->plan;
   HB_TRY(hbk::launch_eval(pl, c->d_t, c->d_ph, c->d_f, c->d_s, c->d_rows, c->d_wc, w, d_logl, d_tmpl, c->d_scratch,
-                          d_tmpl ? 1 : 0, s, acc),
+                          d_tmpl ? 1 : 0, s, acc, c->d_dq),
          "hb_eval_kernel");
   return 0;
 }
@@ -374,7 +380,7 @@ extern "C" int hb_evaluate_dev(hb_ctx* c, int w, double* d_out, int mode, void* 
   HB_TRY(hipSetDevice(c->device), "hipSetDevice");
   const EvalPlan& pl = (c->has_lat && w < kLatencyW) ? c->lat : c->plan;
   HB_TRY(hbk::launch_eval(pl, c->d_t, c->d_ph, c->d_f, c->d_s, c->d_rows, c->d_wc, w, mode == 0 ? d_out : nullptr,
-                          mode == 1 ? d_out : nullptr, c->d_scratch, mode, (hipStream_t)stream),
+                          mode == 1 ? d_out : nullptr, c->d_scratch, mode, (hipStream_t)stream, nullptr, c->d_dq),
          "hb_eval_kernel");
   return 0;
 }
@@ -459,6 +465,11 @@ struct hb_catalog {
   WalkerConst* d_wc = nullptr;
   double* d_params = nullptr;    // host-API staging
   double* d_out = nullptr;
+  // the one-wave kernel's deferred cadence queues, one region per class (the
+  // classes run concurrently on the forked streams)
+  double* d_dq = nullptr;
+  size_t dq_bytes = 0;
+  size_t class_dq[kCatClasses] = {0};    // byte offset of class c's region
   std::mutex mu;
 };
 
@@ -468,7 +479,7 @@ extern "C" void hb_catalog_destroy(hb_catalog* c) {
   for (void* p : {(void*)c->d_t, (void*)c->d_f, (void*)c->d_s, (void*)c->d_ph, (void*)c->d_rows, (void*)c->d_w0,
                   (void*)c->d_tab,
                   (void*)c->d_wt, (void*)c->d_list,
-                  (void*)c->d_wc, (void*)c->d_params, (void*)c->d_out})
+                  (void*)c->d_wc, (void*)c->d_params, (void*)c->d_out, (void*)c->d_dq})
     if (p) (void)hipFree(p);
   for (int i = 0; i < kCatStreams - 1; ++i) {
     if (c->aux[i]) (void)hipStreamDestroy(c->aux[i]);
@@ -638,6 +649,18 @@ static int catalog_layout(hb_catalog* c, const int* walkers, hipStream_t s) {
     c->class_work[cl] = work;
   }
   c->class_off[kCatClasses] = (int)list.size();
+  size_t qb = 0;
+  for (int cl = 0; cl < kCatClasses; ++cl) {
+    c->class_dq[cl] = qb;
+    qb += (hbk::wave_queue_bytes(kCatRcHi[cl], c->class_off[cl + 1] - c->class_off[cl]) + 255) & ~(size_t)255;
+  }
+  if (qb > c->dq_bytes) {
+    if (c->d_dq) (void)hipFree(c->d_dq);
+    c->d_dq = nullptr;
+    c->dq_bytes = 0;
+    if (hipMalloc(&c->d_dq, qb) != hipSuccess) return set_err_msg("hb_catalog: hipMalloc(deferred cadence queue) failed");
+    c->dq_bytes = qb;
+  }
   if ((int)total > c->cap) {
     for (void* p : {(void*)c->d_wt, (void*)c->d_list, (void*)c->d_wc, (void*)c->d_params, (void*)c->d_out})
       if (p) (void)hipFree(p);
@@ -691,7 +714,8 @@ static int catalog_run(hb_catalog* c, const double* d_params, double* d_logl, hi
     while (vpt < kCatRcHi[cl]) vpt <<= 1;
     hipStream_t sj = (j % ns == 0) ? s : c->aux[j % ns - 1];
     HB_TRY(hbk::launch_eval_multi(vpt, c->class_slab[cl], c->d_t, c->d_ph, c->d_f, c->d_s, c->d_rows, c->d_tab, c->d_wt,
-                                  c->d_list + c->class_off[cl], cnt, c->d_wc, d_logl, sj),
+                                  c->d_list + c->class_off[cl], cnt, c->d_wc, d_logl, sj,
+                                  reinterpret_cast<double*>(reinterpret_cast<unsigned char*>(c->d_dq) + c->class_dq[cl])),
            "eval launch");
   }
   for (int i = 0; i < ns - 1; ++i) {

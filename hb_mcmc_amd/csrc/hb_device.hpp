@@ -80,9 +80,10 @@ struct alignas(16) WalkerConst {
   // sin u (1 - e cos E) = sw (cos E - e) + cwq sin E
   double swq, cwq;               // sin/cos omega0 x sqrt(1 - e^2)
   double ci2;                    // cos^2 inc
+  double aR2, rsum2;             // aR^2, rsum^2 (the eclipse test dd aR^2 < rsum^2)
   double pad0;
 };
-static_assert(sizeof(WalkerConst) == 46 * 8, "WalkerConst layout");
+static_assert(sizeof(WalkerConst) == 48 * 8, "WalkerConst layout");
 
 // ------------------------------------------------------------------------
 // small helpers
@@ -386,6 +387,8 @@ __device__ inline void hb_prepare_walker(const double* __restrict__ p, const dou
   w.swq = w.sw * w.sq1me2;
   w.cwq = w.cw * w.sq1me2;
   w.ci2 = w.ci * w.ci;
+  w.aR2 = w.aR * w.aR;
+  w.rsum2 = w.rsum * w.rsum;
   w.pad0 = 0.0;
 }
 
@@ -444,6 +447,11 @@ __device__ __forceinline__ double overlap_area(double ra, double rb, double dc, 
 
 // area * Norm_k / (pi R_k^2) for the star in front; out of line (rare)
 __device__ __noinline__ double eclipse_term(const WalkerConst* w, double dR, double zz) {
+  const double area = overlap_area(w->rbig, w->rsml, w->dcrit, dR);
+  return area * (zz < 0.0 ? w->ecl2 : w->ecl1);
+}
+// the same, inlined (the deferred queue applies it after the model loop)
+__device__ __forceinline__ double eclipse_term_inl(const WalkerConst* w, double dR, double zz) {
   const double area = overlap_area(w->rbig, w->rsml, w->dcrit, dR);
   return area * (zz < 0.0 ? w->ecl2 : w->ecl1);
 }
@@ -623,7 +631,7 @@ __device__ __forceinline__ void cold_start_k(const double (&t)[K], const double2
       c[k] = fma(cx, w.cdel, -(sx * sd));
     }
   }
-  if (__any(exact)) {  // rare: x near a multiple of 2pi, or r == 0
+  if (wave_any(exact)) {  // rare: x near a multiple of 2pi, or r == 0
 #pragma unroll
     for (int k = 0; k < K; ++k) {
       const double x = fma(t[k], kDay, w.mB) * w.mA;
@@ -675,13 +683,13 @@ __device__ __forceinline__ bool newton_k(double e, const double (&m)[K], double 
       conv &= e * z[k] <= 0x1p-51 * den;
     }
     // rotation degree by the wave's largest step (wave-uniform branches)
-    if (__all(tiny)) {
+    if (wave_all(tiny)) {
 #pragma unroll
       for (int k = 0; k < K; ++k) rotate_back_tiny(d[k], z[k], s[k], c[k]);
-    } else if (__all(mid)) {
+    } else if (wave_all(mid)) {
 #pragma unroll
       for (int k = 0; k < K; ++k) rotate_back_mid(d[k], z[k], s[k], c[k]);
-    } else if (__all(small)) {
+    } else if (wave_all(small)) {
 #pragma unroll
       for (int k = 0; k < K; ++k) rotate_back_wide(d[k], z[k], s[k], c[k]);
     } else {
@@ -692,7 +700,7 @@ __device__ __forceinline__ bool newton_k(double e, const double (&m)[K], double 
         sincos_fast(E[k], &s[k], &c[k]);
       }
     }
-    if (__all(conv)) return true;
+    if (wave_all(conv)) return true;
   }
   return false;
 }
@@ -703,14 +711,18 @@ __device__ __forceinline__ bool newton_k(double e, const double (&m)[K], double 
 #ifndef HB_FLUX_V
 #define HB_FLUX_V 2  // 2: numerator form (beta = 1 / den); 1: through cos/sin nu
 #endif
+// inv[k] = 1 / (1 - e cos E) of the caller (flux_poly_k computes it)
 template <int K>
-__device__ __forceinline__ void flux_poly_k(const double (&s)[K], const double (&c)[K], const WalkerConst& w,
-                                            double (&v)[K], double (&dd)[K], double (&zz)[K]) {
+__device__ __forceinline__ void flux_poly_inv_k(const double (&s)[K], const double (&c)[K], const double (&invk)[K],
+                                                const WalkerConst& w, double (&v)[K], double (&dd)[K],
+                                                double (&zz)[K]) {
   const double e = w.e;
 #pragma unroll
   for (int k = 0; k < K; ++k) {
+    const double inv = invk[k];
+#if HB_FLUX_V != 2
     const double den = fma(-e, c[k], 1.0);
-    const double inv = fast_rcp(den);
+#endif
 #if HB_FLUX_V == 2
     // u = omega0 + nu from the numerators of cos/sin nu (den > 0): beta =
     // (1 + e cos nu) / (1 - e^2) = 1 / (1 - e cos E) identically, and the
@@ -751,11 +763,19 @@ __device__ __forceinline__ void flux_poly_k(const double (&s)[K], const double (
     v[k] = fma(b2, h, fma(w.kb, cu, w.kconst));
   }
 }
+template <int K>
+__device__ __forceinline__ void flux_poly_k(const double (&s)[K], const double (&c)[K], const WalkerConst& w,
+                                            double (&v)[K], double (&dd)[K], double (&zz)[K]) {
+  double inv[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) inv[k] = fast_rcp(fma(-w.e, c[k], 1.0));
+  flux_poly_inv_k<K>(s, c, inv, w, v, dd, zz);
+}
 
 // squared test: a lane within an ulp of tangency may go either way, where
 // the overlap area (~eps^1.5) is zero to working precision
 __device__ __forceinline__ bool eclipse_lane(const WalkerConst& w, double dd, double zz) {
-  return (dd * (w.aR * w.aR) < w.rsum * w.rsum) & (zz != 0.0);
+  return (dd * w.aR2 < w.rsum2) & (zz != 0.0);
 }
 
 template <int K>
@@ -766,12 +786,29 @@ __device__ __forceinline__ void flux_from_sc_k(const double (&s)[K], const doubl
   bool need_ecl = false;
 #pragma unroll
   for (int k = 0; k < K; ++k) need_ecl |= eclipse_lane(w, dd[k], zz[k]);
-  if (__any(need_ecl)) {
+  if (wave_any(need_ecl)) {
 #pragma unroll
     for (int k = 0; k < K; ++k) {
       if (eclipse_lane(w, dd[k], zz[k])) v[k] -= eclipse_term(&w, sqrt(dd[k]) * w.aR, zz[k]);
     }
   }
+}
+
+// the polynomial part of K cadences, dd / zz for the caller's eclipse test
+template <int K>
+__device__ __forceinline__ void hb_cadence_poly_k(const double (&t)[K], const double2 (&ph)[K], bool tab,
+                                                  const WalkerConst& w, double (&v)[K], double (&dd)[K],
+                                                  double (&zz)[K], bool& bad) {
+  double m[K], E[K], s[K], c[K], yk[K];
+  bool ok = true, exact = false, plus[K];
+  mean_anomaly_k<K>(t, w, m, plus, ok, exact);
+  cold_start_k<K>(t, ph, tab, exact, w, m, plus, E, s, c, ok);
+  (void)newton_k<K>(w.e, m, E, s, c, yk, ok);
+#if HB_SPLIT_LIVE
+  __asm__ volatile("" ::: "memory");
+#endif
+  flux_poly_k<K>(s, c, w, v, dd, zz);
+  bad = !ok;
 }
 
 template <int K>
@@ -810,9 +847,21 @@ constexpr double kWarmEmax = 0.8;
 // The chain carries the previous cadence's solved E and (sin, cos)(E); its
 // mean anomaly is E - e sin E (Kepler's equation, to rounding) and its
 // 1 / (1 - e cos E) a bare v_rcp_f64 -- the start only needs dE to ~1e-8.
+// HB_RCP_REUSE: the chain also carries 1 / (1 - e cos E) of its last cadence
+// (the polynomial's beta), which is the warm start's 1 / f'(E_p); and the
+// polynomial's reciprocal is seeded with the Newton step's 1 / f' (one ulp
+// class from the final one: two Newton refinements make it full precision)
+// instead of a fresh v_rcp_f64 -- two quarter-rate transcendentals fewer per
+// warm cadence.
+#ifndef HB_RCP_REUSE
+#define HB_RCP_REUSE 1
+#endif
 template <int K>
 struct ChainState {
   double E[K], s[K], c[K];
+#if HB_RCP_REUSE
+  double inv[K];
+#endif
 };
 
 // v: the polynomial part only; the caller applies the eclipse where
@@ -851,7 +900,7 @@ __device__ __forceinline__ void hb_cadence_flux_chain(const double (&t)[K], cons
 #else
   mean_anomaly_k<K>(t, w, m, plus, ok, exact);
   // e <= kWarmEmax is the caller's walker-uniform gate (model_pass_chain)
-  bool warm = HB_WARM && !first && !__any(exact);
+  bool warm = HB_WARM && !first && !wave_any(exact);
 #endif
   HB_STAT(0);
   if (warm) {
@@ -870,14 +919,21 @@ __device__ __forceinline__ void hb_cadence_flux_chain(const double (&t)[K], cons
     // then (sin, cos)(E0) by the degree-9 rotation and ONE Newton step.
     // |d| <= 2^-22 with e d^2 <= 2^-51 (1 - e cos E) means the next correction
     // is below 2^-52 (converged, like the two-step path below).
+#if HB_RCP_REUSE
+    double ys[K];  // the Newton step's 1 / f' (seeds the polynomial's reciprocal)
+#endif
 #pragma unroll
     for (int k = 0; k < K; ++k) {
       const double D = m[k] - fma(-e, st.s[k], st.E[k]);
       const double q = rint(D * 0.15915494309189533577);
       const double Dc = fma(-q, kTwoPi, D);
+#if HB_RCP_REUSE
+      const double r = st.inv[k];
+#else
       const double g = fma(-e, st.c[k], 1.0);
       double r = __builtin_amdgcn_rcp(g);
       r = fma(fma(-g, r, 1.0), r, r);
+#endif
       const double x = Dc * r;
       const double A = (e * st.s[k]) * (0.5 * r);
       const double B = (e * st.c[k]) * (r * (1.0 / 6.0));
@@ -907,6 +963,9 @@ __device__ __forceinline__ void hb_cadence_flux_chain(const double (&t)[K], cons
       E[k] = E0;
       s[k] = s0;
       c[k] = c0;
+#if HB_RCP_REUSE
+      ys[k] = y;
+#endif
     }
 #else
 #pragma unroll
@@ -950,8 +1009,19 @@ __device__ __forceinline__ void hb_cadence_flux_chain(const double (&t)[K], cons
       c[k] = c0;
     }
 #endif
-    if (__all(fine)) {
+    if (wave_all(fine)) {
       HB_STAT(2);
+#if HB_RCP_REUSE
+      double inv[K];
+#pragma unroll
+      for (int k = 0; k < K; ++k) {  // 1 / (1 - e cos E) from the seed: |d| <= 2^-22 moved den by <= e 2^-22
+        const double den = fma(-e, c[k], 1.0);
+        double y = ys[k];
+        y = fma(fma(-den, y, 1.0), y, y);
+        inv[k] = fma(fma(-den, y, 1.0), y, y);
+        st.inv[k] = inv[k];
+      }
+#endif
 #pragma unroll
       for (int k = 0; k < K; ++k) {
         st.E[k] = E[k];
@@ -961,7 +1031,11 @@ __device__ __forceinline__ void hb_cadence_flux_chain(const double (&t)[K], cons
 #if HB_SPLIT_LIVE
       __asm__ volatile("" ::: "memory");
 #endif
+#if HB_RCP_REUSE
+      flux_poly_inv_k<K>(s, c, inv, w, v, dd, zz);
+#else
       flux_poly_k<K>(s, c, w, v, dd, zz);
+#endif
       bad = !ok;
       return;
     }
@@ -993,10 +1067,22 @@ __device__ __forceinline__ void hb_cadence_flux_chain(const double (&t)[K], cons
     st.s[k] = s[k];
     st.c[k] = c[k];
   }
+#if HB_RCP_REUSE
+  double inv[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    inv[k] = fast_rcp(fma(-e, c[k], 1.0));
+    st.inv[k] = inv[k];
+  }
+#endif
 #if HB_SPLIT_LIVE
   __asm__ volatile("" ::: "memory");
 #endif
+#if HB_RCP_REUSE
+  flux_poly_inv_k<K>(s, c, inv, w, v, dd, zz);
+#else
   flux_poly_k<K>(s, c, w, v, dd, zz);
+#endif
   bad = !ok;
 }
 

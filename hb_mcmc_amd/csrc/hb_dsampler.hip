@@ -874,6 +874,10 @@ struct hb_dsampler {
   // sharding: owned slots [lo, lo + nl) of R ranks; m = largest shard,
   // nlmin = smallest (edge windows are capped at it)
   int lo = 0, nl = 0, R = 1, rank = 0, m = 0, nlmin = 0;
+  // step_begin / all-gather / step_end: every sharded sampler, and a
+  // one-rank one made by hb_dsampler_create_shard (the exchange path on a
+  // single GPU: RCCL world size 1 in tests)
+  bool xchg = false;
   bool lds_swap = true;
   bool no_eord = getenv("HB_DS_NO_EORD") != nullptr;  // experiment knob: eval waves in slot order
   bool copy_stream = getenv("HB_DS_COPY_STREAM") != nullptr;  // A/B knob: schedule copy on cst (old path)
@@ -956,6 +960,7 @@ static hb_dsampler* ds_create(hb_sampler* s, hb_ctx* ctx, const int* chain_of_sl
   d->NPAST = v.NPAST;
   d->R = R;
   d->rank = rank;
+  d->xchg = chain_of_slot != nullptr;
   d->lo = v.lo;
   d->nl = v.hi - v.lo;
   d->m = 0;
@@ -1220,6 +1225,12 @@ static int ds_drain_events(hb_dsampler* d) {
 }
 
 namespace hbds {
+// MAP tracker seeded with the chain in slot 0
+__global__ void ds_seed_map(Dev D) {
+  const int c0 = D.idx[0];
+  if (threadIdx.x < kNp) D.ctr->xmap[threadIdx.x] = D.x[(size_t)c0 * kNp + threadIdx.x];
+  if (threadIdx.x == 0) D.ctr->logLmap = D.logL[c0];
+}
 // logL[chain of owned slot j] = ls[j]
 __global__ __launch_bounds__(kBlk) void ds_scatter_logl(Dev D, const double* __restrict__ ls) {
   const int j = blockIdx.x * kBlk + threadIdx.x;
@@ -1243,9 +1254,11 @@ extern "C" int hb_dsampler_init_logl(hb_dsampler* d) {
     ds_scatter_logl<<<(d->nl + kBlk - 1) / kBlk, kBlk, 0, d->st>>>(d->D, d->d_ls);
     DS_TRY(hipGetLastError(), "scatter");
   }
-  // logLmap = logL(x of chain 0), xmap = x of chain 0
-  DS_TRY(hipMemcpyAsync(&d->D.ctr->logLmap, d->D.logL, sizeof(double), hipMemcpyDeviceToDevice, d->st), "map");
-  DS_TRY(hipMemcpyAsync(d->D.ctr->xmap, d->D.x, sizeof(double) * kNp, hipMemcpyDeviceToDevice, d->st), "map");
+  // logLmap / xmap of the chain in slot 0 (chain 0 at the reference's start,
+  // :342; the rank owning slot 0 computed its logL above, whatever the
+  // chain_of_slot permutation of an advanced state)
+  ds_seed_map<<<1, 64, 0, d->st>>>(d->D);
+  DS_TRY(hipGetLastError(), "map");
   return 0;
 }
 
@@ -1328,7 +1341,7 @@ static long ds_begin(hb_dsampler* d, long iter, double* send, long cap) {
     return rc;
   }
   long n = 0;
-  if (d->R > 1) {
+  if (d->xchg) {
     const int ke = std::min(nlv, d->nlmin);  // edge window (a level moves a chain by one slot)
     n = (long)d->m + 2L * ke * kRec;
     if (!send || n > cap) return hbx_set_error("hb_dsampler_step_begin: send buffer missing or too small");
@@ -1349,14 +1362,14 @@ static int ds_end(hb_dsampler* d, long iter, const double* recv, long n) {
   const Dev& D = d->D;
   hipStream_t s = d->st;
   if (d->cur_iter != iter) return hbx_set_error("hb_dsampler_step_end: no step_begin for this iteration");
-  if (d->R > 1 && (!recv || n != d->cur_n))
+  if (d->xchg && (!recv || n != d->cur_n))
     return hbx_set_error("hb_dsampler_step_end: gathered buffer missing or of the wrong size");
   const int r = d->cur_ring, nlv = d->cur_nlv;
   d->cur_iter = -1;
   DS_TRY(hipSetDevice(d->device), "hipSetDevice");
   const SwapEnt* d_ent = reinterpret_cast<const SwapEnt*>(d->d_sched[r]);
   const int* d_off = reinterpret_cast<const int*>(d->d_sched[r] + sizeof(SwapEnt) * (size_t)W);
-  const Gathered X{d->R > 1 ? recv : nullptr, (long long)n, d->R, d->rank, d->m, 0};
+  const Gathered X{d->xchg ? recv : nullptr, (long long)n, d->R, d->rank, d->m, 0};
   if (d->copy_stream) DS_TRY(hipStreamWaitEvent(s, d->ev_copy[r], 0), "schedule wait");
   if (d->lds_swap)
     ds_swap<true><<<1, kSwapThreads, d->swap_lds, s>>>(D, W, d_ent, d_off, nlv, (long long)iter, X);
@@ -1371,7 +1384,7 @@ static int ds_end(hb_dsampler* d, long iter, const double* recv, long n) {
 
 extern "C" long hb_dsampler_step_begin(hb_dsampler* d, long iter, double* send, long cap) {
   if (!d) return hbx_set_error("hb_dsampler_step_begin: null");
-  if (d->R == 1) return hbx_set_error("hb_dsampler_step_begin: single-rank sampler, use hb_dsampler_step");
+  if (!d->xchg) return hbx_set_error("hb_dsampler_step_begin: sampler made by hb_dsampler_create, use hb_dsampler_step");
   return ds_begin(d, iter, send, cap);
 }
 
@@ -1383,7 +1396,7 @@ extern "C" int hb_dsampler_step_end(hb_dsampler* d, long iter, const double* rec
 // one iteration, enqueued on the sampler's stream (no host wait)
 extern "C" int hb_dsampler_step(hb_dsampler* d, long iter) {
   if (!d) return hbx_set_error("hb_dsampler_step: null");
-  if (d->R > 1) return hbx_set_error("hb_dsampler_step: sharded sampler, use step_begin / all-gather / step_end");
+  if (d->xchg) return hbx_set_error("hb_dsampler_step: sharded sampler, use step_begin / all-gather / step_end");
   const long rc = ds_begin(d, iter, nullptr, 0);
   if (rc < 0) {
     d->cur_iter = -1;

@@ -102,8 +102,11 @@ hipError_t launch_prep(const double* d_params, int nwalk, const MagArgs& ma, hbd
 hipError_t launch_eval_multi(int vpt, size_t slab_bytes, const double* t, const double2* ph, const double* f,
                              const double* sg, const double* rows,
                              const TargetDesc* tab, const int* wt, const int* list, int count,
-                             const hbdev::WalkerConst* wc, double* logl, hipStream_t s);
-int wave_vpt_for(long n);  // cadences per lane of the one-wave path, 0 if n > 2048
+                             const hbdev::WalkerConst* wc, double* logl, hipStream_t s, double* dq);
+int wave_vpt_for(long n);
+// device bytes of the one-wave kernel's deferred cadence queue for `count`
+// walkers at `vpt` cadences per lane (the dq argument of launch_eval*)
+size_t wave_queue_bytes(int vpt, long count);  // cadences per lane of the one-wave path, 0 if n > 2048
 size_t wave_slab_bytes(long n);
 size_t wave_lds_bytes(size_t slab, int vpt);
 // t, f, 1/sigma in the one-wave kernel's lane-row order (3 x 64 x ceil(n/64) doubles)
@@ -114,7 +117,8 @@ void build_rows(const double* t, const double* f, const double* isg, long n, dou
 // multi-wave path
 hipError_t launch_eval(const EvalPlan& pl, const double* t, const double2* ph, const double* f, const double* sg,
                        const double* rows, const hbdev::WalkerConst* wc, int nwalk, double* logl, double* tmpl,
-                       double* scratch, int mode, hipStream_t s, const hbds::AccArgs* acc = nullptr);
+                       double* scratch, int mode, hipStream_t s, const hbds::AccArgs* acc = nullptr,
+                       double* dq = nullptr);
 hipError_t launch_traj(const double* d_times, int nt, const TrajArgs& ta, double* d, double* z1,
                        double* z2, double* rr, double* ff, hipStream_t s);
 hipError_t launch_probe(int op, const double* d_in, double* d_out, hipStream_t s);

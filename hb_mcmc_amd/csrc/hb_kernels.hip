@@ -69,12 +69,13 @@ using namespace hbdev;
 // Experiment builds only (HB_WAVE_CLOCKS): per-wave shader clock at entry and
 // exit plus HW_ID / XCC_ID, read back by hb_debug_wave_clocks().
 #ifdef HB_WAVE_CLOCKS
-// 8 words per wave: start, phase marks 1..3 (after the model pass, the keys,
-// the select; 0 if not reached), end, HW_ID, XCC_ID, spare
+// 8 words per wave: start, phase marks 0..2 (after the model pass, the keys,
+// the select; 0 if not reached), end, HW_ID, XCC_ID, mark 3 (the model loop's
+// end, before the deferred queue is applied)
 __device__ unsigned long long hb_wave_clk[8 * 65536];
 #define HB_CLK_BEGIN()                                     \
   const unsigned long long clk0_ = __builtin_amdgcn_s_memtime(); \
-  unsigned long long clkm_[3] = {0ull, 0ull, 0ull}
+  unsigned long long clkm_[4] = {0ull, 0ull, 0ull, 0ull}
 #define HB_CLK_MARK(i) clkm_[(i)] = __builtin_amdgcn_s_memtime()
 #define HB_CLK_END(wv)                                                                  \
   do {                                                                                  \
@@ -87,6 +88,7 @@ __device__ unsigned long long hb_wave_clk[8 * 65536];
       hb_wave_clk[8 * (wv) + 4] = clk1_;                                                \
       hb_wave_clk[8 * (wv) + 5] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);  \
       hb_wave_clk[8 * (wv) + 6] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 20); \
+      hb_wave_clk[8 * (wv) + 7] = clkm_[3];                                             \
     }                                                                                   \
   } while (0)
 #else
@@ -328,6 +330,7 @@ __global__ __launch_bounds__(kPrepThreads) void hb_prep_kernel(const double* __r
       wc->rsml = r2 > r1 ? r1 : r2;
       wc->dcrit = sqrt(wc->rbig * wc->rbig - wc->rsml * wc->rsml);
       wc->rsum = wc->rbig + wc->rsml;
+      wc->rsum2 = wc->rsum * wc->rsum;
       // Roche overflow (RocheOverflow :953-974)
       const double q12 = m1 / m2;
       const double peri = a_cgs * (1.0 - e);
@@ -405,6 +408,7 @@ __global__ __launch_bounds__(kPrepThreads) void hb_prep_kernel(const double* __r
     wc->swq = gs[1][j] * sq1me2;
     wc->cwq = gs[2][j] * sq1me2;
     wc->aR = aR;
+    wc->aR2 = aR * aR;
     wc->mA = mA;
     wc->mB = -wc->T0c;
     // polynomial coefficients
@@ -546,7 +550,7 @@ __device__ __forceinline__ void model_pass(const double* __restrict__ t, const d
 #endif
     hb_cadence_flux_k<K>(tk, pk, tab, w, v, bad);
 #endif
-    if (__any(bad)) {  // out-of-domain angles: reference-order ocml path
+    if (wave_any(bad)) {  // out-of-domain angles: reference-order ocml path
       if (bad) {
 #pragma unroll
         for (int k = 0; k < K; ++k) v[k] = hb_cadence_flux_slow(tk[k], &w);
@@ -581,7 +585,7 @@ __device__ __forceinline__ void model_pass(const double* __restrict__ t, const d
   // keys of the extremes; -0.0 / +0.0 compare equal but key apart: take the
   // outer key of a zero extreme so [kmn, kmx] brackets every key
   uint64_t kmn = dkey(vmn == 0.0 ? -0.0 : vmn), kmx = dkey(vmx == 0.0 ? 0.0 : vmx);
-  if (__any(nan)) {
+  if (wave_any(nan)) {
     kmn = ~0ull;
     kmx = 0ull;
     for (int i = tid; i < n; i += NT) {
@@ -597,32 +601,37 @@ __device__ __forceinline__ void model_pass(const double* __restrict__ t, const d
 // One-wave kernel: lane l owns the rc = ceil(n/64) consecutive cadences
 // l*rc .. l*rc + rc - 1 (its row of the LDS slab, later its select keys).
 // The chain path solves a row as KC chains whose Kepler starts are warm
-// (hb_cadence_flux_chain) after each chain's first cadence.  Row stride: rc
-// when rc is a power of two, position c stored at c ^ (lane mod rc) (a wave's
-// accesses at one position then spread over all banks); otherwise rc | 1, an
-// odd stride that is conflict-free as it stands.  The slab is ~n * 8 bytes,
-// so short light curves of a catalog class keep more waves per CU.
+// (hb_cadence_flux_chain) after each chain's first cadence.  Row stride
+// rc | 1: an odd stride spreads a wave's accesses at one row position over
+// the banks, and position c of a lane's row sits at a constant offset from
+// the row's start, so the key loads take immediate offsets (no per-key
+// address arithmetic).  The slab is ~n * 8 bytes, so short light curves of a
+// catalog class keep more waves per CU.
 #ifndef HB_KC
 #define HB_KC 2  // chains per lane
+#endif
+#ifndef HB_ODD_STRIDE
+#define HB_ODD_STRIDE 1  // 0: power-of-two rows stored at c ^ (lane mod rc) (stride rc)
 #endif
 struct Rows {
   int rc;      // cadences per lane row
   int stride;  // row stride [doubles]
-  int swz;     // XOR swizzle mask (rc - 1 for a power-of-two rc, else 0)
+  int swz;     // XOR swizzle mask (HB_ODD_STRIDE == 0, power-of-two rc: rc - 1; else 0)
   float rcp;   // 1 / rc (row of cadence i, i < 2^11: exact after rounding)
 };
-__host__ __device__ __forceinline__ int rows_stride(int rc) { return (rc & (rc - 1)) == 0 ? rc : (rc | 1); }
+__host__ __device__ __forceinline__ int rows_stride(int rc) {
+  return (HB_ODD_STRIDE || (rc & (rc - 1)) != 0) ? (rc | 1) : rc;
+}
 __device__ __forceinline__ Rows make_rows(int n) {
   Rows r;
   r.rc = (n + 63) >> 6;
-  const bool p2 = (r.rc & (r.rc - 1)) == 0;
   r.stride = rows_stride(r.rc);
-  r.swz = p2 ? r.rc - 1 : 0;
+  r.swz = (!HB_ODD_STRIDE && (r.rc & (r.rc - 1)) == 0) ? r.rc - 1 : 0;
   r.rcp = 1.0f / (float)r.rc;
   return r;
 }
 __device__ __forceinline__ int slab_pos(const Rows& r, int lane, int c) {
-  return lane * r.stride + (c ^ (lane & r.swz));
+  return HB_ODD_STRIDE ? lane * r.stride + c : lane * r.stride + (c ^ (lane & r.swz));
 }
 // slab position of cadence i: row q = i / rc by the fp32 reciprocal
 // ((i + 0.5) / rc is >= 1/(2 rc) away from an integer, far above its error)
@@ -646,6 +655,69 @@ __device__ __forceinline__ void ecl_apply(const WalkerConst& w, double* vals, co
     const double q = eq_dd[first + lane];
     const double dR = sqrt(fabs(q)) * w.aR;  // projected separation [Rsun]
     vals[eq_code[first + lane]] -= eclipse_term(&w, dR, signbit(q) ? -1.0 : 1.0);  // out of line
+  }
+}
+
+// Deferred cadence queue (HB_GQ = 1): the model pass writes every cadence's
+// polynomial value to the slab and appends the cadences that need more to a
+// per-wave region of global memory -- eclipsing ones (dd with the sign of zz,
+// slab position) and the rare ones outside the fast sincos/fmod domain
+// (cadence index, slab position | kSlowFlag).  After the pass, 64 entries at
+// a time, the eclipse term (inlined) is subtracted from the slab value -- the
+// same v - term as inline -- and slow-path cadences are recomputed in
+// reference order.  The model loop then holds no function call: nothing of
+// the loop's state is saved around one, and the out-of-line callee's
+// register conventions no longer shape the loop's allocation.  Capacity per
+// wave: 64 VPT entries (every cadence, worst case).
+#ifndef HB_GQ
+#define HB_GQ 1
+#endif
+constexpr int kSlowFlag = 1 << 30;
+// One 16-B entry per queued cadence: (dd with the sign of zz, code = slab
+// position | kSlowFlag for the slow path); one store, one load.
+struct DeferQ {
+  char* e;  // this wave's entries (the base is held in VGPRs: no SGPR spill reloads per push)
+  int n;    // entries (wave-uniform)
+};
+__device__ __forceinline__ void dq_push(DeferQ& q, bool push, double a, int code) {
+  const unsigned long long bal = wave_ballot(push);
+  if (push) {
+    const uint32_t pos = __builtin_amdgcn_mbcnt_hi((unsigned)(bal >> 32),
+                                                   __builtin_amdgcn_mbcnt_lo((unsigned)bal, (unsigned)q.n));
+    // global address space spelled out (the VGPR base hides it from inference)
+    typedef __attribute__((address_space(1))) double gdouble;
+    typedef __attribute__((address_space(1))) long long glong;
+    gdouble* p = (gdouble*)(q.e + (size_t)(pos << 4));
+    p[0] = a;
+    ((glong*)p)[1] = (long long)code;
+  }
+  q.n += __popcll(bal);
+}
+// t: the light curve's times in cadence order (slow-path entries: the cadence
+// is recovered from the slab position, row = position / stride)
+__device__ __forceinline__ void dq_apply(const WalkerConst& w, double* vals, const DeferQ& q,
+                                         const double* __restrict__ t, const Rows& rw, int n, int lane) {
+  if (q.n == 0) return;
+  // the queue's stores are complete (acknowledged) before this wave reads them back
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  for (int b = 0; b < q.n; b += 64) {  // wave-uniform
+    const int i = b + lane;
+    if (i < q.n) {
+      typedef __attribute__((address_space(1))) const double gcdouble;
+      typedef __attribute__((address_space(1))) const long long gclong;
+      const gcdouble* p = (const gcdouble*)(q.e + (size_t)i * 16);
+      const double a = p[0];
+      const int code = (int)((const gclong*)p)[1];
+      if (code & kSlowFlag) {  // rare: reference-order path (eclipse included)
+        const int sp = code & ~kSlowFlag;
+        const int row = sp / rw.stride;
+        const int cad = min(row * rw.rc + (sp - row * rw.stride), n - 1);
+        vals[sp] = hb_cadence_flux_slow(t[cad], &w);
+      } else {
+        const double dR = sqrt(fabs(a)) * w.aR;  // projected separation [Rsun]
+        vals[code] -= eclipse_term_inl(&w, dR, signbit(a) ? -1.0 : 1.0);
+      }
+    }
   }
 }
 
@@ -733,7 +805,7 @@ struct Pacer {
 // at the lane-row slab positions (slab_pos_of) that the key load reads.
 __device__ __forceinline__ void model_pass_cold(const double* __restrict__ t, const double2* __restrict__ ph,
                                                 int n, const Rows& rw, const WalkerConst& w, double* vals,
-                                                int lane, Pacer pc) {
+                                                int lane, Pacer pc, DeferQ& dq) {
   constexpr int K = HB_K;
   const bool tab = (ph != nullptr) && (w.tab != 0.0);  // walker-uniform
   const int last = n - 1;
@@ -753,8 +825,20 @@ __device__ __forceinline__ void model_pass_cold(const double* __restrict__ t, co
 #if HB_SPLIT_LIVE
     __asm__ volatile("" ::: "memory");
 #endif
+#if HB_GQ
+    double dd[K], zz[K];
+    hb_cadence_poly_k<K>(tk, pk, tab, w, v, dd, zz, bad);
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const int i = base + k * 64 + lane;
+      const int sp = slab_pos_of(rw, i);
+      if (i < n) vals[sp] = v[k];
+      const bool need = (!bad) & eclipse_lane(w, dd[k], zz[k]);
+      dq_push(dq, (i < n) & (bad | need), copysign(dd[k], zz[k]), sp | (bad ? kSlowFlag : 0));
+    }
+#else
     hb_cadence_flux_k<K>(tk, pk, tab, w, v, bad);
-    if (__any(bad)) {  // out-of-domain angles: reference-order ocml path
+    if (wave_any(bad)) {  // out-of-domain angles: reference-order ocml path
       if (bad) {
 #pragma unroll
         for (int k = 0; k < K; ++k) v[k] = hb_cadence_flux_slow(tk[k], &w);
@@ -765,6 +849,7 @@ __device__ __forceinline__ void model_pass_cold(const double* __restrict__ t, co
       const int i = base + k * 64 + lane;
       if (i < n) vals[slab_pos_of(rw, i)] = v[k];
     }
+#endif
   }
 }
 
@@ -774,13 +859,13 @@ __device__ __forceinline__ void model_pass_cold(const double* __restrict__ t, co
 template <int VPT>
 __device__ __forceinline__ void model_pass_chain(const double* __restrict__ tT, const double2* __restrict__ ph,
                                                  int n, const Rows& rw, const WalkerConst& w, double* vals,
-                                                 double* eq_dr, int* eq_code, int lane, Pacer pc) {
+                                                 double* eq_dr, int* eq_code, int lane, Pacer pc, DeferQ& dq) {
   constexpr int KC = VPT < HB_KC ? VPT : HB_KC;
   const int lc = (rw.rc + KC - 1) / KC;  // chain length (wave-uniform)
   const bool tab = (ph != nullptr) && (w.tab != 0.0);  // walker-uniform
   const int last = n - 1;
   const int base = lane * rw.rc;
-  const int rs = lane * rw.stride, lsw = lane & rw.swz;  // slab_pos(rw, lane, c) = rs + (c ^ lsw)
+  const int rs = lane * rw.stride, lsw = HB_ODD_STRIDE ? 0 : (lane & rw.swz);  // slab_pos = rs + (c ^ lsw)
   const uint64_t lt_mask = (1ull << lane) - 1ull;
   int qn = 0;  // queued eclipse cadences (wave-uniform)
   ChainState<KC> st;
@@ -830,7 +915,21 @@ __device__ __forceinline__ void model_pass_chain(const double* __restrict__ tT, 
       hb_cadence_flux_chain<KC>(tk, p0, false, false, w, st, v, dd, zz, bad);
     }
 #endif
-    if (__any(bad)) {  // out-of-domain angles: reference-order ocml path (eclipse included)
+#if HB_GQ
+#pragma unroll
+    for (int k = 0; k < KC; ++k) {
+      const int c = k * lc + j;
+      if (c < rw.rc) {  // wave-uniform: the last chain may run past the row end
+        // cadences past n (the last row's padding) store harmless values: their keys are masked
+        const int sp = rs + (c ^ lsw);
+        vals[sp] = v[k];
+        const bool need = (!bad) & eclipse_lane(w, dd[k], zz[k]);
+        dq_push(dq, bad | need, copysign(dd[k], zz[k]), sp | (bad ? kSlowFlag : 0));
+      }
+      tk[k] = tn[k];
+    }
+#else
+    if (wave_any(bad)) {  // out-of-domain angles: reference-order ocml path (eclipse included)
       if (bad) {
 #pragma unroll
         for (int k = 0; k < KC; ++k) v[k] = hb_cadence_flux_slow(tk[k], &w);
@@ -848,7 +947,7 @@ __device__ __forceinline__ void model_pass_chain(const double* __restrict__ tT, 
 #else
         const bool need = !bad && eclipse_lane(w, dd[k], zz[k]);
 #endif
-        const uint64_t bal = __ballot(need);
+        const uint64_t bal = wave_ballot(need);
         const int pos = need ? qn + __popcll(bal & lt_mask) : kEclQ;
         eq_dr[pos] = copysign(dd[k], zz[k]);  // sign bit: which star is in front
         eq_code[pos] = sp;
@@ -862,6 +961,7 @@ __device__ __forceinline__ void model_pass_chain(const double* __restrict__ tT, 
         qn -= cnt;
       }
     }
+#endif
   }
 }
 
@@ -1041,7 +1141,7 @@ __global__ __launch_bounds__(64 * NW) void hb_eval_kernel(
 constexpr int kSelBits = HB_SEL_BITS1;   // first digit (whole light curve)
 constexpr int kSelBits2 = HB_SEL_BITS2;  // later digits (the survivors of one bin)
 #ifndef HB_SEL_V
-#define HB_SEL_V 2  // 1: shuffle-based select (previous version)
+#define HB_SEL_V 3  // 3: leaner keys / select / chi^2 (below); 2: previous version; 1: shuffle-based select
 #endif
 #ifndef HB_CAND
 #define HB_CAND 64
@@ -1098,7 +1198,7 @@ __device__ double wave_select(const uint64_t (&key)[VPT], uint32_t kth, uint64_t
       if (lane >= off) incl += o;
     }
     const uint32_t excl = incl - local;
-    const unsigned long long own = __ballot(excl <= kk && kk < incl);
+    const unsigned long long own = wave_ballot(excl <= kk && kk < incl);
     const int owner = __ffsll((long long)own) - 1;
     uint32_t bin = 0, before = 0, c = 0;
     if (lane == owner) {
@@ -1145,7 +1245,7 @@ __device__ double wave_select(const uint64_t (&key)[VPT], uint32_t kth, uint64_t
 #pragma unroll
   for (int v = 0; v < VPT; ++v) {
     const bool m = (key[v] & mask) == prefix;
-    const unsigned long long bal = __ballot(m);
+    const unsigned long long bal = wave_ballot(m);
     if (m) cand[basec + __popcll(bal & ((1ull << lane) - 1ull))] = key[v];
     basec += (uint32_t)__popcll(bal);
   }
@@ -1156,7 +1256,7 @@ __device__ double wave_select(const uint64_t (&key)[VPT], uint32_t kth, uint64_t
     const uint64_t o = cand[j];
     r += (o < mine) | ((o == mine) & (j < (uint32_t)lane));
   }
-  const unsigned long long hit = __ballot((uint32_t)lane < cnt && r == kk);
+  const unsigned long long hit = wave_ballot((uint32_t)lane < cnt && r == kk);
   const int who = __ffsll((long long)hit) - 1;
   const uint64_t ans = __shfl(mine, who, 64);
   return dval(ans);
@@ -1244,7 +1344,7 @@ __device__ __forceinline__ void wave_pick_bin(const uint32_t* hist, int lane, ui
   }
   const uint32_t incl = wave_scan_incl(local);
   const uint32_t excl = incl - local;
-  const unsigned long long own = __ballot(excl <= kk && kk < incl);
+  const unsigned long long own = wave_ballot(excl <= kk && kk < incl);
   const int owner = __builtin_amdgcn_readfirstlane(__ffsll((long long)own) - 1);
   // every lane walks its own bins (group of 4, then bin); the owner's is kept
   uint32_t before = excl;
@@ -1314,7 +1414,7 @@ __device__ __forceinline__ double wave_select2(const uint64_t (&key)[VPT], uint3
 #pragma unroll
   for (int v = 0; v < VPT; ++v) {
     const bool m = (key[v] & mask) == prefix;
-    const unsigned long long bal = __ballot(m);
+    const unsigned long long bal = wave_ballot(m);
     if (m) cand[basec + __popcll(bal & ((1ull << lane) - 1ull))] = key[v];
     basec += (uint32_t)__popcll(bal);
   }
@@ -1325,9 +1425,204 @@ __device__ __forceinline__ double wave_select2(const uint64_t (&key)[VPT], uint3
     const uint64_t o = cand[j];
     r += (o < mine) | ((o == mine) & (j < (uint32_t)lane));
   }
-  const unsigned long long hit = __ballot((uint32_t)lane < cnt && r == kk);
+  const unsigned long long hit = wave_ballot((uint32_t)lane < cnt && r == kk);
   const int who = __builtin_amdgcn_readfirstlane(__ffsll((long long)hit) - 1);
   return dval(readlane_u64(mine, who));
+}
+
+// ---------------------------------------------------------------------------
+// HB_SEL_V == 3: the same keys, median and chi^2 with fewer non-fp64
+// instructions (bit-identical results):
+//  * order keys in 3-4 VALU (okey/oval: a sign mask instead of compare+select);
+//  * the select's bracket from the keys' high words (32-bit min/max, DPP): it
+//    holds every live key, and only its common prefix is used;
+//  * pass 1 needs no prefix test (every live key shares the bracket's prefix;
+//    padding keys ~0 land in the top bin, above the k-th);
+//  * digits by one shift of the high word (bfe) or a funnel shift (alignbit),
+//    the prefix test of later passes on the high word when the prefix is there;
+//  * a light curve that fills every lane row (n = 64 VPT: C2, C4) drops the
+//    per-key liveness masks (a wave-uniform branch into a FULL instantiation).
+// ---------------------------------------------------------------------------
+#ifndef HB_SEL_V
+#define HB_SEL_V 3
+#endif
+__device__ __forceinline__ uint64_t okey(double v) {  // == dkey(v)
+  const uint32_t lo = (uint32_t)__double2loint(v), hi = (uint32_t)__double2hiint(v);
+  const uint32_t m = (uint32_t)((int32_t)hi >> 31);
+  return ((uint64_t)(hi ^ (m | 0x80000000u)) << 32) | (uint64_t)(lo ^ m);
+}
+__device__ __forceinline__ double oval(uint64_t k) {  // == dval(k)
+  const uint32_t lo = (uint32_t)k, hi = (uint32_t)(k >> 32);
+  uint32_t m;  // sign-extended top bit (asm: kept a shift, not a compare + selects)
+  __asm__("v_ashrrev_i32 %0, 31, %1" : "=v"(m) : "v"(hi));
+  return __hiloint2double((int)(hi ^ (~m | 0x80000000u)), (int)~(lo ^ m));
+}
+template <class Op>
+__device__ __forceinline__ uint32_t wave_reduce_u32(uint32_t v, Op op) {
+  v = op(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xf, 0xf, false));   // quad_perm [1,0,3,2]
+  v = op(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xf, 0xf, false));   // quad_perm [2,3,0,1]
+  v = op(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xf, 0xf, false));  // row_half_mirror
+  v = op(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x140, 0xf, 0xf, false));  // row_mirror
+  const uint32_t a = (uint32_t)__builtin_amdgcn_readlane((int)v, 0), b = (uint32_t)__builtin_amdgcn_readlane((int)v, 16);
+  const uint32_t c = (uint32_t)__builtin_amdgcn_readlane((int)v, 32), d = (uint32_t)__builtin_amdgcn_readlane((int)v, 48);
+  return op(op(a, b), op(c, d));
+}
+struct OpMinU32 { __device__ uint32_t operator()(uint32_t a, uint32_t b) const { return a < b ? a : b; } };
+struct OpMaxU32 { __device__ uint32_t operator()(uint32_t a, uint32_t b) const { return a > b ? a : b; } };
+
+// Whether key k carries `prefix` in its bits >= pshift (the digits fixed so
+// far), and its digit [shift, shift + width).  HT: pshift >= 32 (the test on
+// the high word), HD: shift >= 32 (the digit in the high word); wave-uniform.
+template <bool HT>
+__device__ __forceinline__ bool key_match(uint64_t k, int pshift, uint64_t prefix) {
+  if (HT) return ((uint32_t)(k >> 32) >> (pshift - 32)) == (uint32_t)(prefix >> pshift);
+  return (k >> pshift) == (prefix >> pshift);
+}
+template <bool HD>
+__device__ __forceinline__ uint32_t key_digit(uint64_t k, int shift, uint32_t dm) {
+  if (HD) return ((uint32_t)(k >> 32) >> (shift - 32)) & dm;
+  return __builtin_amdgcn_alignbit((uint32_t)(k >> 32), (uint32_t)k, (uint32_t)shift) & dm;
+}
+template <int VPT, bool TEST, bool HT, bool HD>
+__device__ __forceinline__ void select3_hist(const uint64_t (&key)[VPT], uint32_t* hist, int pshift, uint64_t prefix,
+                                             int shift, uint32_t dm, uint32_t dummy) {
+#pragma unroll
+  for (int v = 0; v < VPT; ++v) {
+    const uint32_t b = key_digit<HD>(key[v], shift, dm);
+    atomicAdd(&hist[TEST ? (key_match<HT>(key[v], pshift, prefix) ? b : dummy) : b], 1u);
+  }
+}
+// One radix pass of 2^B bins (TEST: later passes; pass 1 counts every key).
+template <int VPT, int B, bool TEST>
+__device__ __forceinline__ void select3_pass(const uint64_t (&key)[VPT], uint32_t* hist, int lane, int& hi,
+                                             int& pshift, uint64_t& prefix, uint32_t& kk, uint32_t& cnt) {
+  static_assert(!TEST || (4 << B) + 256 <= (4 << kSelBits), "the TEST pass dummies fit in the slab");
+  constexpr int PER = (1 << B) / 64, Q = PER / 4;
+  const int width = hi + 1 < B ? hi + 1 : B;
+  const int shift = hi + 1 - width;
+  const uint32_t dm = (1u << width) - 1u;
+  uint4* h4 = reinterpret_cast<uint4*>(hist);
+#pragma unroll
+  for (int q = 0; q < Q; ++q) h4[lane * Q + q] = make_uint4(0u, 0u, 0u, 0u);
+  HB_WSYNC();
+  // the non-matching keys' bin in TEST passes: one per lane, past the 2^B bins
+  // (one shared dummy would be a 64-way same-address atomic per key)
+  const uint32_t dummy = (1u << B) + (uint32_t)lane;
+  if (shift >= 32) select3_hist<VPT, TEST, true, true>(key, hist, pshift, prefix, shift, dm, dummy);
+  else if (!TEST || pshift >= 32) select3_hist<VPT, TEST, true, false>(key, hist, pshift, prefix, shift, dm, dummy);
+  else select3_hist<VPT, TEST, false, false>(key, hist, pshift, prefix, shift, dm, dummy);
+  HB_WSYNC();
+  uint32_t bin, before;
+  wave_pick_bin<B>(hist, lane, kk, bin, before, cnt);
+  kk -= before;
+  prefix |= (uint64_t)bin << shift;
+  pshift = shift;
+  hi = shift - 1;
+  HB_WSYNC();  // histogram reads done before the next clear
+}
+template <int VPT, bool HT>
+__device__ __forceinline__ uint32_t select3_compact(const uint64_t (&key)[VPT], uint64_t* cand, int pshift,
+                                                    uint64_t prefix) {
+  uint32_t basec = 0;
+#pragma unroll
+  for (int v = 0; v < VPT; ++v) {
+    const bool m = key_match<HT>(key[v], pshift, prefix);
+    const unsigned long long bal = wave_ballot(m);
+    if (m) {  // exec-masked: a shared dummy slot would serialise the non-matching lanes' writes
+      const uint32_t pos = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, basec));
+      cand[pos] = key[v];
+    }
+    basec += (uint32_t)__popcll(bal);
+  }
+  return basec;
+}
+// k-th smallest key (0-based) over the wave; hmin/hmax: min / max high words
+// of the live keys
+template <int VPT>
+__device__ __forceinline__ double wave_select3(const uint64_t (&key)[VPT], uint32_t kth, uint32_t hmin, uint32_t hmax,
+                                               uint32_t* hist, uint64_t* cand) {
+  const int lane = threadIdx.x & 63;
+  const uint64_t kmin = (uint64_t)hmin << 32, kmax = ((uint64_t)hmax << 32) | 0xffffffffull;
+  int hi = 63 - __builtin_clzll(kmin ^ kmax);  // >= 31
+  uint64_t prefix = hi == 63 ? 0ull : (kmin & ~((2ull << hi) - 1ull));
+  int pshift = hi + 1;
+  uint32_t kk = kth, cnt = 0;
+  select3_pass<VPT, kSelBits, false>(key, hist, lane, hi, pshift, prefix, kk, cnt);
+  while (cnt > (uint32_t)kCandMax && hi >= 0) select3_pass<VPT, kSelBits2, true>(key, hist, lane, hi, pshift, prefix, kk, cnt);
+  if (hi < 0) return oval(prefix);
+  const uint32_t nc = pshift >= 32 ? select3_compact<VPT, true>(key, cand, pshift, prefix)
+                                   : select3_compact<VPT, false>(key, cand, pshift, prefix);
+  HB_WSYNC();
+  const uint64_t mine = (uint32_t)lane < nc ? cand[lane] : ~0ull;
+  uint32_t r = 0;
+  for (uint32_t j = 0; j < nc; ++j) {
+    const uint64_t o = cand[j];
+    r += (o < mine) | ((o == mine) & (j < (uint32_t)lane));
+  }
+  const unsigned long long hit = wave_ballot((uint32_t)lane < nc && r == kk);
+  const int who = __builtin_amdgcn_readfirstlane(__ffsll((long long)hit) - 1);
+  return oval(readlane_u64(mine, who));
+}
+// keys of this lane's row (slot v: cadence lane rc + v; slots v >= lim are
+// padding ~0) and the lane's min / max key high words over its live slots
+template <int VPT, bool FULL>
+__device__ __forceinline__ void load_keys3(const double* vals, const Rows& rw, int lane, int lim, uint64_t (&key)[VPT],
+                                           uint32_t& hmn, uint32_t& hmx) {
+  constexpr int kCh = VPT < 8 ? VPT : (VPT >= 32 ? 4 : 8);
+  hmn = ~0u;
+  hmx = 0u;
+#pragma unroll
+  for (int v0 = 0; v0 < VPT; v0 += kCh) {
+    double x[kCh];
+#pragma unroll
+    for (int u = 0; u < kCh; ++u) x[u] = vals[slab_pos(rw, lane, FULL ? v0 + u : (v0 + u < rw.rc ? v0 + u : rw.rc - 1))];
+#pragma unroll
+    for (int u = 0; u < kCh; ++u) {
+      const int v = v0 + u;
+      const uint64_t kv = okey(x[u]);
+      const uint32_t h = (uint32_t)(kv >> 32);
+      if (FULL) {
+        key[v] = kv;
+        hmn = h < hmn ? h : hmn;
+        hmx = h > hmx ? h : hmx;
+      } else {
+        const bool act = v < lim;
+        key[v] = act ? kv : ~0ull;
+        hmn = (act && h < hmn) ? h : hmn;
+        hmx = (act && h > hmx) ? h : hmx;
+      }
+    }
+  }
+}
+// chi^2 partial of this lane (the reference's per-cadence operations,
+// likelihood3.c:679-685 and :822-832) or, mode 1, the template values
+template <int VPT, bool FULL>
+__device__ __forceinline__ double chi2_keys3(const uint64_t (&key)[VPT], double med, const WalkerConst& w,
+                                             const double* __restrict__ fT, const double* __restrict__ iT,
+                                             const Rows& rw, int lane, int lim) {
+  constexpr int kCh = VPT < 8 ? VPT : (VPT >= 32 ? 4 : 8);
+  const double blend = w.blend, one_m_blend = 1.0 - w.blend, tune = w.tune;
+  double acc = 0.0;
+#pragma unroll
+  for (int v0 = 0; v0 < VPT; v0 += kCh) {
+    double fv[kCh], iv[kCh];
+#pragma unroll
+    for (int u = 0; u < kCh; ++u) {  // row block vc (wave-uniform) + lane: scalar base, lane offset
+      const int vc = FULL ? v0 + u : (v0 + u < rw.rc ? v0 + u : rw.rc - 1);
+      fv[u] = (fT + vc * 64)[lane];
+      iv[u] = (iT + vc * 64)[lane];
+    }
+#pragma unroll
+    for (int u = 0; u < kCh; ++u) {
+      const int v = v0 + u;
+      double m = (oval(key[v]) - med) + 1.0;
+      m = (blend + m * one_m_blend) * tune;
+      const double r = (m - fv[u]) * iv[u];
+      if (FULL) acc += r * r;
+      else acc += v < lim ? r * r : 0.0;
+    }
+  }
+  return acc;
 }
 
 #ifndef HB_PHASE_TAB
@@ -1363,7 +1658,8 @@ __global__ __launch_bounds__(64 * WPB) HB_WPE_ATTR void hb_eval_wave_kernel(
     const double* __restrict__ isg, const double* __restrict__ rows,
     long n, long kth, const WalkerConst* __restrict__ wcs, double* __restrict__ logl,
     double* __restrict__ tmpl_out, int mode, int slab_bytes, double gap, const TargetDesc* __restrict__ tab,
-    const int* __restrict__ wt, const int* __restrict__ list, hbds::AccArgs hst, int count, int lds_per) {
+    const int* __restrict__ wt, const int* __restrict__ list, hbds::AccArgs hst, int count, int lds_per,
+    double* __restrict__ dqbuf) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_all[];
   const int lane = threadIdx.x & 63;
   const int wib = WPB > 1 ? __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) : 0;
@@ -1371,7 +1667,7 @@ __global__ __launch_bounds__(64 * WPB) HB_WPE_ATTR void hb_eval_wave_kernel(
   const bool valid = WPB == 1 || slot < count;
   unsigned char* smem = smem_all + (size_t)wib * (size_t)lds_per;
   int wv = slot;
-  if (ACC && hst.ord != nullptr) wv = hst.ord[slot];  // device sampler: slots by descending e (ds_propose)
+  if (ACC && hst.ord != nullptr && valid) wv = hst.ord[slot];  // device sampler: slots by descending e (ds_propose)
   if (MULTI && valid) {
     wv = list[slot];
     const TargetDesc& td = tab[wt[wv]];
@@ -1424,16 +1720,26 @@ __global__ __launch_bounds__(64 * WPB) HB_WPE_ATTR void hb_eval_wave_kernel(
   const Rows rw = make_rows((int)n);
   const double* __restrict__ fT = rows + 64 * rw.rc;   // f and 1/sigma in lane-row order
   const double* __restrict__ iT = rows + 128 * rw.rc;
+  DeferQ dq{nullptr, 0};
+  if (HB_GQ) {  // this wave's region of the deferred queue (64 VPT entries of 16 B)
+    dq.e = reinterpret_cast<char*>(dqbuf) + (size_t)slot * (size_t)(64 * VPT * 16);
+    __asm__ volatile("" : "+v"(dq.e));  // a VGPR pair, not one more scalar to spill
+  }
   {
     if (VPT >= HB_CHAIN_VPT_MIN && VPT <= HB_CHAIN_VPT_MAX && chain_eligible(w, MULTI ? tab[wt[wv]].gap : gap)) {
       // the eclipse queue shares the select's candidate area (dead until the select)
       double* eq_dr = reinterpret_cast<double*>(smem + slab_bytes);
       int* eq_code = reinterpret_cast<int*>(eq_dr + kEclQ + 1);
-      model_pass_chain<VPT>(rows, ph, (int)n, rw, w, vals, eq_dr, eq_code, lane, pc);
+      model_pass_chain<VPT>(rows, ph, (int)n, rw, w, vals, eq_dr, eq_code, lane, pc, dq);
     } else {
-      model_pass_cold(t, ph, (int)n, rw, w, vals, lane, pc);
+      model_pass_cold(t, ph, (int)n, rw, w, vals, lane, pc, dq);
     }
   }
+#if HB_GQ
+  HB_CLK_MARK(3);
+  HB_WSYNC();  // the slab values of every lane are in place
+  dq_apply(w, vals, dq, t, rw, (int)n, lane);
+#endif
   HB_CLK_MARK(0);
 #if HB_PRIO == 2
   if (pc.prog != nullptr) {
@@ -1442,6 +1748,44 @@ __global__ __launch_bounds__(64 * WPB) HB_WPE_ATTR void hb_eval_wave_kernel(
   }
 #endif
   HB_WSYNC();
+#if HB_SEL_V == 3
+  {
+    // live key slots of this lane; a light curve of 64 VPT cadences fills every row
+    const int lim = min(rw.rc, max(0, (int)n - lane * rw.rc));
+    const bool full = (rw.rc == VPT) && (n == 64L * VPT);  // wave-uniform
+    uint32_t hmn, hmx;
+    if (full) load_keys3<VPT, true>(vals, rw, lane, lim, key, hmn, hmx);
+    else load_keys3<VPT, false>(vals, rw, lane, lim, key, hmn, hmx);
+    hmn = wave_reduce_u32(hmn, OpMinU32());
+    hmx = wave_reduce_u32(hmx, OpMaxU32());
+    HB_CLK_MARK(1);
+    HB_WSYNC();  // the slab becomes the histogram
+    const double med = wave_select3<VPT>(key, (uint32_t)kth, hmn, hmx, hist, cand);
+    HB_CLK_MARK(2);
+    if (mode == 1) {
+      const double blend = w.blend, one_m_blend = 1.0 - w.blend, tune = w.tune;
+      double* o = tmpl_out + (size_t)wv * (size_t)n;
+#pragma unroll
+      for (int v = 0; v < VPT; ++v) {
+        if (v < lim) {
+          const double m = (oval(key[v]) - med) + 1.0;
+          o[key_index(rw, v, lane)] = (blend + m * one_m_blend) * tune;
+        }
+      }
+      HB_CLK_END(wv);
+      return;
+    }
+    const double acc = full ? chi2_keys3<VPT, true>(key, med, w, fT, iT, rw, lane, lim)
+                            : chi2_keys3<VPT, false>(key, med, w, fT, iT, rw, lane, lim);
+    const double chi2 = wave_sum_dpp(acc);
+    double c = chi2 + w.chi2_extra;
+    if (w.roche != 0.0) c = kBig;
+    if (lane == 0) logl[wv] = -c / 2.0;
+    if (ACC) hbds::accept_slot_wave_pre(hst, wv, -c / 2.0, lane, apre);  // c is wave-uniform (readlanes)
+    HB_CLK_END(wv);
+    return;
+  }
+#endif
   // keys, and the lane's min/max keys.  Every slot is loaded unconditionally
   // (slot v >= rc reads row position rc - 1) so the VPT LDS reads are in
   // flight together, then masked; min/max run on the order keys (exact
@@ -1569,7 +1913,7 @@ __device__ __forceinline__ void block_select_pass(const uint64_t (&key)[VPT], ui
     const uint32_t b = m ? ((uint32_t)(key[v] >> shift) & dm) : 0xffffffffu;
     const uint32_t bp = (uint32_t)__builtin_amdgcn_update_dpp((int)0xfffffffeu, (int)b, 0x111, 0xf, 0xf, false);
     const bool head = m && (b != bp);
-    const unsigned long long bound = __ballot(head || !m);  // lanes that start a run or hold no key
+    const unsigned long long bound = wave_ballot(head || !m);  // lanes that start a run or hold no key
     if (head) {
       const int lane = tid & 63;
       const unsigned long long after = lane < 63 ? (bound >> (lane + 1)) : 0ull;
@@ -1624,7 +1968,7 @@ __device__ double block_select2(const uint64_t (&key)[VPT], uint32_t kth, uint64
       const uint64_t o = cand[j];
       r += (o < mine) | ((o == mine) & (j < (uint32_t)tid));
     }
-    const unsigned long long hit = __ballot((uint32_t)tid < cnt && r == kk);
+    const unsigned long long hit = wave_ballot((uint32_t)tid < cnt && r == kk);
     const int who = __builtin_amdgcn_readfirstlane(__ffsll((long long)hit) - 1);
     const uint64_t ans = readlane_u64(mine, who);
     if (tid == 0) sh->ans = ans;
@@ -1959,7 +2303,7 @@ static hipError_t launch_wave_g(size_t lds_per, int count, hipStream_t s, const 
                                 const double* f, const double* sg, const double* rows, long n, long kth, const WalkerConst* wc,
                                 double* logl, double* tmpl, int mode, size_t slab, double gap,
                                 const TargetDesc* tab, const int* wt, const int* list,
-                                const hbds::AccArgs& acc) {
+                                const hbds::AccArgs& acc, double* dq) {
   auto kern = hb_eval_wave_kernel<VPT, MULTI, ACC, WPB>;
   const size_t lds = (size_t)WPB * lds_per + (WPB > 1 ? 64 : 0);
   static bool attr_set = false;  // per instantiation; benign race (idempotent)
@@ -1970,7 +2314,7 @@ static hipError_t launch_wave_g(size_t lds_per, int count, hipStream_t s, const 
     attr_set = true;
   }
   hipLaunchKernelGGL(kern, dim3((count + WPB - 1) / WPB), dim3(64 * WPB), lds, s, t, ph, f, sg, rows, n, kth, wc, logl,
-                     tmpl, mode, (int)slab, gap, tab, wt, list, acc, count, (int)lds_per);
+                     tmpl, mode, (int)slab, gap, tab, wt, list, acc, count, (int)lds_per, dq);
   return hipGetLastError();
 }
 
@@ -1978,22 +2322,22 @@ template <int VPT, bool MULTI, bool ACC>
 static hipError_t launch_wave_w(size_t slab, int count, hipStream_t s, const double* t, const double2* ph,
                                 const double* f, const double* sg, const double* rows, long n, long kth, const WalkerConst* wc,
                                 double* logl, double* tmpl, int mode, double gap, const TargetDesc* tab,
-                                const int* wt, const int* list, const hbds::AccArgs& acc) {
+                                const int* wt, const int* list, const hbds::AccArgs& acc, double* dq) {
   const size_t per = wave_lds_bytes(slab, VPT);
   switch (wave_wpb(count, per)) {
 #if HB_WPB_MAX >= 16
     case 16:
       return launch_wave_g<VPT, MULTI, ACC, 16>(per, count, s, t, ph, f, sg, rows, n, kth, wc, logl, tmpl, mode, slab,
-                                                gap, tab, wt, list, acc);
+                                                gap, tab, wt, list, acc, dq);
 #endif
 #if HB_WPB_MAX >= 4
     case 4:
       return launch_wave_g<VPT, MULTI, ACC, 4>(per, count, s, t, ph, f, sg, rows, n, kth, wc, logl, tmpl, mode, slab,
-                                               gap, tab, wt, list, acc);
+                                               gap, tab, wt, list, acc, dq);
 #endif
     default:
       return launch_wave_g<VPT, MULTI, ACC, 1>(per, count, s, t, ph, f, sg, rows, n, kth, wc, logl, tmpl, mode, slab,
-                                               gap, tab, wt, list, acc);
+                                               gap, tab, wt, list, acc, dq);
   }
 }
 
@@ -2001,68 +2345,69 @@ template <int VPT>
 static hipError_t launch_wave_t(const EvalPlan& pl, const double* t, const double2* ph, const double* f,
                                 const double* sg, const double* rows,
                                 const WalkerConst* wc, int nwalk, double* logl, double* tmpl, int mode,
-                                hipStream_t s) {
+                                hipStream_t s, double* dq) {
   return launch_wave_w<VPT, false, false>(pl.slab_bytes, nwalk, s, t, ph, f, sg, rows, pl.n, pl.kth, wc, logl, tmpl,
-                                          mode, pl.gap, nullptr, nullptr, nullptr, hbds::AccArgs{});
+                                          mode, pl.gap, nullptr, nullptr, nullptr, hbds::AccArgs{}, dq);
 }
 
 template <int VPT>
 static hipError_t launch_wave_acc_t(const EvalPlan& pl, const double* t, const double2* ph, const double* f,
                                     const double* sg, const double* rows, const WalkerConst* wc, int nwalk,
-                                    double* logl, hipStream_t s, const hbds::AccArgs& acc) {
+                                    double* logl, hipStream_t s, const hbds::AccArgs& acc, double* dq) {
   return launch_wave_w<VPT, false, true>(pl.slab_bytes, nwalk, s, t, ph, f, sg, rows, pl.n, pl.kth, wc, logl, nullptr,
-                                         0, pl.gap, nullptr, nullptr, nullptr, acc);
+                                         0, pl.gap, nullptr, nullptr, nullptr, acc, dq);
 }
 
 template <int VPT>
 static hipError_t launch_multi_t(size_t slab, const double* t, const double2* ph, const double* f,
                                  const double* sg, const double* rows,
                                  const TargetDesc* tab, const int* wt, const int* list, int count,
-                                 const WalkerConst* wc, double* logl, hipStream_t s) {
+                                 const WalkerConst* wc, double* logl, hipStream_t s, double* dq) {
   return launch_wave_w<VPT, true, false>(slab, count, s, t, ph, f, sg, rows, 0L, 0L, wc, logl, nullptr, 0, 0.0, tab, wt,
-                                         list, hbds::AccArgs{});
+                                         list, hbds::AccArgs{}, dq);
 }
 
 hipError_t launch_eval_multi(int vpt, size_t slab, const double* t, const double2* ph, const double* f,
                              const double* sg, const double* rows,
                              const TargetDesc* tab, const int* wt, const int* list, int count,
-                             const WalkerConst* wc, double* logl, hipStream_t s) {
+                             const WalkerConst* wc, double* logl, hipStream_t s, double* dq) {
   if (count <= 0) return hipSuccess;
   switch (vpt) {
-    case 1: return launch_multi_t<1>(slab, t, ph, f, sg, rows, tab, wt, list, count, wc, logl, s);
-    case 2: return launch_multi_t<2>(slab, t, ph, f, sg, rows, tab, wt, list, count, wc, logl, s);
-    case 4: return launch_multi_t<4>(slab, t, ph, f, sg, rows, tab, wt, list, count, wc, logl, s);
-    case 8: return launch_multi_t<8>(slab, t, ph, f, sg, rows, tab, wt, list, count, wc, logl, s);
-    case 16: return launch_multi_t<16>(slab, t, ph, f, sg, rows, tab, wt, list, count, wc, logl, s);
-    case 32: return launch_multi_t<32>(slab, t, ph, f, sg, rows, tab, wt, list, count, wc, logl, s);
+    case 1: return launch_multi_t<1>(slab, t, ph, f, sg, rows, tab, wt, list, count, wc, logl, s, dq);
+    case 2: return launch_multi_t<2>(slab, t, ph, f, sg, rows, tab, wt, list, count, wc, logl, s, dq);
+    case 4: return launch_multi_t<4>(slab, t, ph, f, sg, rows, tab, wt, list, count, wc, logl, s, dq);
+    case 8: return launch_multi_t<8>(slab, t, ph, f, sg, rows, tab, wt, list, count, wc, logl, s, dq);
+    case 16: return launch_multi_t<16>(slab, t, ph, f, sg, rows, tab, wt, list, count, wc, logl, s, dq);
+    case 32: return launch_multi_t<32>(slab, t, ph, f, sg, rows, tab, wt, list, count, wc, logl, s, dq);
     default: return hipErrorInvalidValue;
   }
 }
 
 hipError_t launch_eval(const EvalPlan& pl, const double* t, const double2* ph, const double* f, const double* sg,
                        const double* rows, const WalkerConst* wc, int nwalk, double* logl, double* tmpl, double* scratch,
-                       int mode, hipStream_t s, const hbds::AccArgs* acc) {
+                       int mode, hipStream_t s, const hbds::AccArgs* acc, double* dq) {
   if (nwalk <= 0) return hipSuccess;
+  if (pl.vpt > 0 && HB_GQ && dq == nullptr) return hipErrorInvalidValue;  // the one-wave path's deferred queue
   if (acc != nullptr) {  // fused Hastings epilogue: one-wave path only
     if (mode != 0) return hipErrorInvalidValue;
     switch (pl.vpt) {
-      case 1: return launch_wave_acc_t<1>(pl, t, ph, f, sg, rows, wc, nwalk, logl, s, *acc);
-      case 2: return launch_wave_acc_t<2>(pl, t, ph, f, sg, rows, wc, nwalk, logl, s, *acc);
-      case 4: return launch_wave_acc_t<4>(pl, t, ph, f, sg, rows, wc, nwalk, logl, s, *acc);
-      case 8: return launch_wave_acc_t<8>(pl, t, ph, f, sg, rows, wc, nwalk, logl, s, *acc);
-      case 16: return launch_wave_acc_t<16>(pl, t, ph, f, sg, rows, wc, nwalk, logl, s, *acc);
-      case 32: return launch_wave_acc_t<32>(pl, t, ph, f, sg, rows, wc, nwalk, logl, s, *acc);
+      case 1: return launch_wave_acc_t<1>(pl, t, ph, f, sg, rows, wc, nwalk, logl, s, *acc, dq);
+      case 2: return launch_wave_acc_t<2>(pl, t, ph, f, sg, rows, wc, nwalk, logl, s, *acc, dq);
+      case 4: return launch_wave_acc_t<4>(pl, t, ph, f, sg, rows, wc, nwalk, logl, s, *acc, dq);
+      case 8: return launch_wave_acc_t<8>(pl, t, ph, f, sg, rows, wc, nwalk, logl, s, *acc, dq);
+      case 16: return launch_wave_acc_t<16>(pl, t, ph, f, sg, rows, wc, nwalk, logl, s, *acc, dq);
+      case 32: return launch_wave_acc_t<32>(pl, t, ph, f, sg, rows, wc, nwalk, logl, s, *acc, dq);
       default: return hipErrorNotSupported;
     }
   }
   switch (pl.vpt) {
     case 0: break;
-    case 1: return launch_wave_t<1>(pl, t, ph, f, sg, rows, wc, nwalk, logl, tmpl, mode, s);
-    case 2: return launch_wave_t<2>(pl, t, ph, f, sg, rows, wc, nwalk, logl, tmpl, mode, s);
-    case 4: return launch_wave_t<4>(pl, t, ph, f, sg, rows, wc, nwalk, logl, tmpl, mode, s);
-    case 8: return launch_wave_t<8>(pl, t, ph, f, sg, rows, wc, nwalk, logl, tmpl, mode, s);
-    case 16: return launch_wave_t<16>(pl, t, ph, f, sg, rows, wc, nwalk, logl, tmpl, mode, s);
-    case 32: return launch_wave_t<32>(pl, t, ph, f, sg, rows, wc, nwalk, logl, tmpl, mode, s);
+    case 1: return launch_wave_t<1>(pl, t, ph, f, sg, rows, wc, nwalk, logl, tmpl, mode, s, dq);
+    case 2: return launch_wave_t<2>(pl, t, ph, f, sg, rows, wc, nwalk, logl, tmpl, mode, s, dq);
+    case 4: return launch_wave_t<4>(pl, t, ph, f, sg, rows, wc, nwalk, logl, tmpl, mode, s, dq);
+    case 8: return launch_wave_t<8>(pl, t, ph, f, sg, rows, wc, nwalk, logl, tmpl, mode, s, dq);
+    case 16: return launch_wave_t<16>(pl, t, ph, f, sg, rows, wc, nwalk, logl, tmpl, mode, s, dq);
+    case 32: return launch_wave_t<32>(pl, t, ph, f, sg, rows, wc, nwalk, logl, tmpl, mode, s, dq);
     default: return hipErrorInvalidValue;
   }
   if (pl.bvpt > 0) {
@@ -2155,11 +2500,17 @@ size_t wave_slab_bytes(long n) {
   return (slab + 15) & ~(size_t)15;
 }
 
+// bytes of the one-wave kernel's deferred queue for `count` waves (HB_GQ)
+size_t wave_queue_bytes(int vpt, long count) {
+  return HB_GQ ? (size_t)count * (size_t)64 * (size_t)vpt * 16 : 0;
+}
+
 // slab | select candidates | eclipse queue (chain model pass only)
 size_t wave_lds_bytes(size_t slab, int vpt) {
   const bool chain = vpt >= HB_CHAIN_VPT_MIN && vpt <= HB_CHAIN_VPT_MAX;
-  const size_t q = chain ? (size_t)(kEclQ + 1) * (8 + 4) : 0;  // eclipse queue aliases the candidates
-  return (slab + (q > 8 * kCandMax ? q : 8 * kCandMax) + 15) & ~(size_t)15;
+  const size_t q = (chain && !HB_GQ) ? (size_t)(kEclQ + 1) * (8 + 4) : 0;  // eclipse queue aliases the candidates
+  const size_t cb = 8 * (size_t)kCandMax;
+  return (slab + (q > cb ? q : cb) + 15) & ~(size_t)15;
 }
 
 // t, f and 1/sigma in the one-wave kernel's lane-row order: row block c holds

@@ -19,6 +19,16 @@
 
 namespace hbdev {
 
+// Wave votes on a lane predicate without materialising it as an int: HIP's
+// __any/__all/__ballot take an int, so a compare result held as a lane mask
+// is turned into 0/1 (v_cndmask) and back (v_cmp) -- two VALU instructions
+// per vote.  The ballot builtin on a bool is a scalar AND with exec.
+__device__ __forceinline__ unsigned long long wave_ballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
+__device__ __forceinline__ bool wave_any(bool p) { return __builtin_amdgcn_ballot_w64(p) != 0ull; }
+__device__ __forceinline__ bool wave_all(bool p) {
+  return __builtin_amdgcn_ballot_w64(p) == __builtin_amdgcn_ballot_w64(true);
+}
+
 // v_rcp_f64 is good to ~2^-24 (2.5e8 ulp, scripts/probes/rcp_probe.hip on
 // the MI355X); one Newton step gives <= 11 ulp, two give the correctly
 // rounded reciprocal on every probed input.

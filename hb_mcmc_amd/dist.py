@@ -166,25 +166,27 @@ def run_sharded(t, flux, sigma, niter, run_id, log10_period, run=0, nchains=50, 
             if r == 0 and Lp[0] > logLmap:  # :565-572
                 xmap = S.get()[0][0].copy()
                 logLmap = float(Lp[0])
-            if verbose and it % 1000 == 0:  # :575-589 (counters summed over ranks)
+            # collectives at fixed iterations on every rank (not keyed to a
+            # rank's own verbose / out_root, which only select what rank 0 does)
+            if it % 1000 == 0:  # :575-589 (counters summed over ranks)
                 st = S.stats()
                 acc, de_acc, de_trial = comm.allreduce_sum([st["acc"], st["DEacc"], st["DEtrial"]])
                 x_all = comm.gather_rows(S.get()[0], counts)
-                if r == 0:
+                if verbose and r == 0:
                     with np.errstate(divide="ignore", invalid="ignore"):
                         print("%d/%d logL=%.10g acc=%.3g DEacc=%.3g" % (
                             it, niter, Lp[0], np.float64(acc) / np.float64(st["atrial"]),
                             np.float64(de_acc) / np.float64(de_trial)))
                     print("Parameter values: ")
                     print("".join("%f\t" % v for v in x_all[min(10, W - 1), :5]))
-            if it % 100 == 0 and out_root:  # :593-649
+            if it % 100 == 0:  # :593-649
                 x_all = comm.gather_rows(S.get()[0], counts)
-                if r == 0:
+                if out_root and r == 0:
                     writer.step(it, Lp, x_all)
                     writer.light_curve(t, flux, np.asarray(model(xmap), dtype=np.float64))
                     writer.pars(False, x_all[0])
             S.end_iter(it)
-        x_all = comm.gather_rows(S.get()[0], counts) if out_root else None
+        x_all = comm.gather_rows(S.get()[0], counts)
         if r == 0 and out_root:  # :655-681
             writer.light_curve(t, flux, np.asarray(model(xmap), dtype=np.float64))
             writer.pars(True, x_all[0])
@@ -244,14 +246,17 @@ def run_sharded_device(t, flux, sigma, niter, run_id, log10_period, run=0, nchai
         model = (lambda p: gpu.light_curve(p[None, :])[0])
         for it in range(int(niter)):
             D.step(it)
-            show = verbose and it % 1000 == 0
-            write = bool(out_root) and it % 100 == 0
-            if not (show or write):
+            # collective cadence fixed by the iteration number alone (every
+            # rank calls the same collectives whatever its own verbose /
+            # out_root); the flags only decide what rank 0 prints or writes
+            if it % 100 != 0:
                 continue
+            show = verbose and it % 1000 == 0
+            write = bool(out_root)
             x_all, l_all, xmap, _, st = D.gather_all()
-            if show:  # :575-589 (counters summed over ranks)
+            if it % 1000 == 0:  # :575-589 (counters summed over ranks)
                 acc, de_acc, de_trial = comm.allreduce_sum([st["acc"], st["DEacc"], st["DEtrial"]])
-                if r == 0:
+                if show and r == 0:
                     with np.errstate(divide="ignore", invalid="ignore"):
                         print("%d/%d logL=%.10g acc=%.3g DEacc=%.3g" % (
                             it, niter, l_all[0], np.float64(acc) / np.float64(st["atrial"]),

@@ -107,9 +107,15 @@ class ShardedDeviceSampler:
             for it in range(niter):
                 D.step(it)                                   # no host wait under RCCL
             x, logl, xmap, logLmap, stats = D.gather()       # this rank's slots
+
+    exchange: run step_begin -> all-gather -> step_end even on one rank
+    (default: only when R > 1; a one-rank sampler otherwise takes the plain
+    hb_dsampler_step).  With backend "nccl" and R = 1 that is a real RCCL
+    all-gather of world size 1 on the sampler's stream -- the ordering of
+    ds_pack -> RCCL -> ds_swap that C4 relies on, testable on one GPU.
     """
 
-    def __init__(self, sampler: SlotSampler, likelihood, group=None):
+    def __init__(self, sampler: SlotSampler, likelihood, group=None, exchange=None):
         import torch
         import torch.distributed as dist
 
@@ -128,9 +134,15 @@ class ShardedDeviceSampler:
         _, _, cid = sampler.get()
         chain_of_slot = np.ascontiguousarray(self._gather_rows(cid.astype(np.float64), counts).astype(np.int32))
         self.device = torch.device("cuda", likelihood.device)
-        self._h = self.lib.hb_dsampler_create_shard(sampler._h, likelihood._h,
-                                                    chain_of_slot.ctypes.data_as(C.POINTER(C.c_int)),
-                                                    self.R, self.rank)
+        self.exchange = self.R > 1 if exchange is None else bool(exchange)
+        if self.R > 1 and not self.exchange:
+            raise ValueError("a sharded sampler always exchanges")
+        if self.exchange:
+            self._h = self.lib.hb_dsampler_create_shard(sampler._h, likelihood._h,
+                                                        chain_of_slot.ctypes.data_as(C.POINTER(C.c_int)),
+                                                        self.R, self.rank)
+        else:
+            self._h = self.lib.hb_dsampler_create(sampler._h, likelihood._h)
         if not self._h:
             raise _lib.HBMIError("hb_dsampler_create_shard: " + _lib.last_error())
         self.cap = int(self.lib.hb_dsampler_exchange_cap(self._h))
@@ -174,7 +186,7 @@ class ShardedDeviceSampler:
         self._check(self.lib.hb_dsampler_init_logl(self._h), "hb_dsampler_init_logl")
 
     def step(self, it):
-        if self.R == 1:
+        if not self.exchange:
             self._check(self.lib.hb_dsampler_step(self._h, int(it)), "hb_dsampler_step")
             return
         n = int(self.lib.hb_dsampler_step_begin(self._h, int(it), C.c_void_p(self.send.data_ptr()), self.cap))

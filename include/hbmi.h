@@ -57,8 +57,9 @@ typedef struct RNG_Vars RNG_Vars;
 double partition(double arr[], int low, int high);
 
 /* likelihood3.h:69 / likelihood3.c:70-83.  Sorts arr[low..high] ascending on
- * the GPU (radix sort).  Output equals quickSort's for all non-NaN inputs;
- * the relative order of -0.0 and +0.0 (which compare equal) may differ. */
+ * the GPU (bitonic sort of order-preserving keys: LDS tiles, then global
+ * merge steps).  Output equals quickSort's for all non-NaN inputs; the
+ * relative order of -0.0 and +0.0 (which compare equal) may differ. */
 void quickSort(double arr[], int low, int high);
 
 /* likelihood3.h:70 / likelihood3.c:86-105.  Subtracts the element of rank
@@ -168,13 +169,16 @@ int hb_ctx_eval_kind(const hb_ctx *ctx);
  * idle).  Default off: one wave per walker at every batch size, which keeps a
  * context's results bit-identical across batch sizes and with the device
  * sampler (the two kernels sum chi2 in different orders; both within the
- * stated tolerance of likelihood3.c).  The drop-in loglikelihood() turns it on
- * for its cached contexts.  Returns 0. */
+ * stated tolerance of likelihood3.c).  Opt-in only (HBLikelihood(latency_plan=
+ * True)): the drop-in loglikelihood() keeps the one-wave plan, because the
+ * relinked reference sampler is bound by its own host threads (18.6 vs 23.7 us
+ * of device time per call, no measurable change in iterations/s;
+ * profiles/r02e_latency_probe.txt).  Returns 0. */
 int hb_ctx_set_latency_plan(hb_ctx *ctx, int on);
 
 /* Last error message of the calling thread ("" if none). */
 const char *hb_last_error(void);
-/* 1 if a HIP device is usable, 0 otherwise (never falls back to the CPU). */
+
 /* ---- catalog mode (config C5): many independent light curves on one GPU.
  * Target k: t[k], flux[k], sigma[k] of n[k] cadences (2..2048), magnitude
  * data mag5[5k..5k+4] / magerr4[4k..4k+3] (NULL: the reference fallback
@@ -193,6 +197,7 @@ int hb_catalog_loglik(hb_catalog *cat, const double *params, const int *walkers,
 int hb_catalog_loglik_dev(hb_catalog *cat, const double *d_params, const int *walkers, double *d_logl,
                           void *stream);
 
+/* 1 if a HIP device is usable, 0 otherwise (never falls back to the CPU). */
 int hb_device_available(void);
 
 /* ---- measurement helpers (bench.py): HIP events recorded on the caller's

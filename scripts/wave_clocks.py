@@ -38,6 +38,8 @@ assert lib.hb_debug_wave_clocks(buf, w) == 0
 c = np.frombuffer(buf, dtype=np.uint64).reshape(w, 8).astype(np.int64)
 t0, t1, hw, xcc = c[:, 0], c[:, 4], c[:, 5], c[:, 6]
 marks = c[:, 1:4]
+if (c[:, 7] > 0).any():  # mark 3: the model loop's end, before the deferred queue
+    marks = np.concatenate([c[:, 7:8], marks], axis=1)
 simd = (hw >> 4) & 3
 cu = (hw >> 8) & 15
 se = (hw >> 13) & 7
@@ -46,7 +48,10 @@ key = ((xid * 8 + se) * 16 + cu) * 4 + simd
 life = t1 - t0
 full = (marks > 0).all(axis=1)
 ph = np.diff(np.concatenate([t0[:, None], marks, t1[:, None]], axis=1), axis=1)[full]
-res = {"phase_names": ["model pass", "keys+minmax", "select", "chi2+epilogue"],
+names = ["model pass", "keys+minmax", "select", "chi2+epilogue"]
+if marks.shape[1] == 4:
+    names = ["model loop", "deferred queue"] + names[1:]
+res = {"phase_names": names,
        "phase_mean_cycles": [float(x) for x in ph.mean(axis=0)] if len(ph) else None,
        "waves": int(w), "life_mean": float(life.mean()), "life_min": int(life.min()), "life_max": int(life.max()),
        "life_pct": [float(x) for x in np.percentile(life, [5, 25, 50, 75, 95])]}

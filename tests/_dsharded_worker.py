@@ -6,7 +6,10 @@ ranks and each rank's RNG streams / history, for comparison with a
 single-process device run of the same configuration.
 
     python -m torch.distributed.run --nproc-per-node R tests/_dsharded_worker.py \\
-        OUT.npz W NITER LADDER NPAST N [gloo|nccl]
+        OUT.npz W NITER LADDER NPAST N [gloo|nccl] [x]
+
+`x`: force the exchange path (step_begin / all-gather / step_end) even on one
+rank -- with nccl that is an RCCL all-gather of world size 1.
 """
 import os
 import sys
@@ -20,6 +23,7 @@ if ROOT not in sys.path:
 def main():
     out, W, niter, ladder, npast, n = sys.argv[1], *map(int, sys.argv[2:7])
     backend = sys.argv[7] if len(sys.argv) > 7 else "gloo"
+    exchange = True if (len(sys.argv) > 8 and sys.argv[8] == "x") else None
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -39,7 +43,7 @@ def main():
         L = HBLikelihood(t, f, s, device=local)
         lo, hi = shard(W, r, R)
         S = SlotSampler(niter, W, synth.THETA_STAR[2], lo, hi, run=0, npast=npast, ladder=ladder)
-        with ShardedDeviceSampler(S, L) as D:
+        with ShardedDeviceSampler(S, L, exchange=exchange) as D:
             D.init_logl()
             for it in range(niter):
                 D.step(it)

@@ -77,13 +77,13 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _sharded(tmp, W, niter, ladder, npast, n, ranks, backend="gloo"):
+def _sharded(tmp, W, niter, ladder, npast, n, ranks, backend="gloo", exchange=False):
     out = os.path.join(str(tmp), f"sharded_{W}_{ranks}.npz")
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={ranks}",
                         "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
                         os.path.join(ROOT, "tests", "_dsharded_worker.py"), out, str(W), str(niter), str(ladder),
-                        str(npast), str(n), backend],
+                        str(npast), str(n), backend] + (["x"] if exchange else []),
                        capture_output=True, text=True, timeout=600, cwd=ROOT, env=env)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     return np.load(out)
@@ -137,6 +137,20 @@ def test_sharded_device_sampler_c4_equals_single_process(tmp_path):
     _compare(a, b)
     # the exchange stays small: logL of a shard plus a few dozen edge records
     assert float(a["exchanged"]) / niter < W / 2 + 2 * 64 * 24
+
+
+@pytest.mark.gpu
+def test_rccl_exchange_one_rank_equals_device_sampler(tmp_path):
+    """The RCCL branch of ShardedDeviceSampler.step on one GPU: world size 1
+    under backend nccl with the exchange forced, so every iteration runs
+    ds_pack -> all_gather_into_tensor on the sampler's stream -> ds_swap's
+    import (the C4 exchange, mcmc_wrapper2.c:554-563).  W = 4096, 100
+    iterations: bit-identical to the plain DeviceSampler."""
+    W, niter, ladder, npast, n = 4096, 100, 1, 20, 1024
+    a = _sharded(tmp_path, W, niter, ladder, npast, n, 1, backend="nccl", exchange=True)
+    b = _single(W, niter, ladder, npast, n)
+    _compare(a, b)
+    assert float(a["exchanged"]) >= niter * W  # the logL block went through RCCL every iteration
 
 
 @pytest.mark.gpu
