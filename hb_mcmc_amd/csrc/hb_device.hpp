@@ -409,7 +409,7 @@ __device__ __forceinline__ double asin01(double x) {
 #else
   const bool big = x >= 0.5;
   const double t = big ? (1.0 - x) * 0.5 : x * x;
-  const double s = big ? sqrt(t) : x;
+  const double s = big ? sqrt_fast(t) : x;  // t exact (Sterbenz); a few ulp of s are within asin01's 2 ulp
   double p = 0.028757851367421566;
   p = __builtin_fma(p, t, -0.014851887071247204);
   p = __builtin_fma(p, t, 0.01740087944269402);
@@ -431,8 +431,10 @@ __device__ __forceinline__ double asin01(double x) {
 __device__ __forceinline__ double overlap_partial(double ra, double rb, double d, bool inner) {
   const double cq = d * d - rb * rb + ra * ra;
   const double hh = sqrt((4. * d * d * ra * ra - cq * cq) / (4. * d * d));
-  const double la = ra * ra * asin01(hh / ra) - hh * sqrt(ra * ra - hh * hh);
-  const double lb = rb * rb * asin01(hh / rb) - hh * sqrt(rb * rb - hh * hh);
+  // hh and the chord ratios keep the reference's IEEE operations (asin's slope
+  // is unbounded at hh = rb); sqrt(r^2 - hh^2) only needs its output to an ulp
+  const double la = ra * ra * asin01(hh / ra) - hh * sqrt_fast(ra * ra - hh * hh);
+  const double lb = rb * rb * asin01(hh / rb) - hh * sqrt_fast(rb * rb - hh * hh);
   return inner ? (kPi * rb * rb - (-la + lb)) : (la + lb);
 }
 

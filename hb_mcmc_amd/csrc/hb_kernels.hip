@@ -698,23 +698,34 @@ __device__ __forceinline__ void dq_push(DeferQ& q, bool push, double a, int code
 __device__ __forceinline__ void dq_apply(const WalkerConst& w, double* vals, const DeferQ& q,
                                          const double* __restrict__ t, const Rows& rw, int n, int lane) {
   if (q.n == 0) return;
+  typedef __attribute__((address_space(1))) const double gcdouble;
+  typedef __attribute__((address_space(1))) const long long gclong;
+  const gcdouble* qa = (const gcdouble*)q.e;
   // the queue's stores are complete (acknowledged) before this wave reads them back
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  double a_n = 0.0;
+  int c_n = 0;
+  if (lane < q.n) {
+    a_n = qa[2 * lane];
+    c_n = (int)((const gclong*)qa)[2 * lane + 1];
+  }
   for (int b = 0; b < q.n; b += 64) {  // wave-uniform
-    const int i = b + lane;
-    if (i < q.n) {
-      typedef __attribute__((address_space(1))) const double gcdouble;
-      typedef __attribute__((address_space(1))) const long long gclong;
-      const gcdouble* p = (const gcdouble*)(q.e + (size_t)i * 16);
-      const double a = p[0];
-      const int code = (int)((const gclong*)p)[1];
+    const double a = a_n;
+    const int code = c_n;
+    const bool live = b + lane < q.n;
+    const int i2 = b + 64 + lane;
+    if (i2 < q.n) {  // the next batch's entries in flight while this one computes
+      a_n = qa[2 * i2];
+      c_n = (int)((const gclong*)qa)[2 * i2 + 1];
+    }
+    if (live) {
       if (code & kSlowFlag) {  // rare: reference-order path (eclipse included)
         const int sp = code & ~kSlowFlag;
         const int row = sp / rw.stride;
         const int cad = min(row * rw.rc + (sp - row * rw.stride), n - 1);
         vals[sp] = hb_cadence_flux_slow(t[cad], &w);
       } else {
-        const double dR = sqrt(fabs(a)) * w.aR;  // projected separation [Rsun]
+        const double dR = sqrt_fast(fabs(a)) * w.aR;  // projected separation [Rsun]
         vals[code] -= eclipse_term_inl(&w, dR, signbit(a) ? -1.0 : 1.0);
       }
     }
@@ -859,7 +870,11 @@ __device__ __forceinline__ void model_pass_cold(const double* __restrict__ t, co
 template <int VPT>
 __device__ __forceinline__ void model_pass_chain(const double* __restrict__ tT, const double2* __restrict__ ph,
                                                  int n, const Rows& rw, const WalkerConst& w, double* vals,
-                                                 double* eq_dr, int* eq_code, int lane, Pacer pc, DeferQ& dq) {
+                                                 double* eq_dr, int* eq_code, int lane, Pacer pc, DeferQ& dq
+#ifdef HB_CLK_STEP0
+                                                 , unsigned long long& clk_step0
+#endif
+                                                 ) {
   constexpr int KC = VPT < HB_KC ? VPT : HB_KC;
   const int lc = (rw.rc + KC - 1) / KC;  // chain length (wave-uniform)
   const bool tab = (ph != nullptr) && (w.tab != 0.0);  // walker-uniform
@@ -875,6 +890,9 @@ __device__ __forceinline__ void model_pass_chain(const double* __restrict__ tT, 
   pc.begin(lc);
   for (int j = 0; j < lc; ++j) {
     pc.step(j, lc);
+#ifdef HB_CLK_STEP0  // experiment builds only: the chains' cold first step ends here
+    if (j == 1) clk_step0 = __builtin_amdgcn_s_memtime();
+#endif
 #if defined(HB_PAD_V) || defined(HB_PAD_S)  // experiment builds only: issue-cost probes
     {
       int x = j;
@@ -1730,13 +1748,19 @@ __global__ __launch_bounds__(64 * WPB) HB_WPE_ATTR void hb_eval_wave_kernel(
       // the eclipse queue shares the select's candidate area (dead until the select)
       double* eq_dr = reinterpret_cast<double*>(smem + slab_bytes);
       int* eq_code = reinterpret_cast<int*>(eq_dr + kEclQ + 1);
-      model_pass_chain<VPT>(rows, ph, (int)n, rw, w, vals, eq_dr, eq_code, lane, pc, dq);
+      model_pass_chain<VPT>(rows, ph, (int)n, rw, w, vals, eq_dr, eq_code, lane, pc, dq
+#ifdef HB_CLK_STEP0
+                            , clkm_[3]
+#endif
+                            );
     } else {
       model_pass_cold(t, ph, (int)n, rw, w, vals, lane, pc, dq);
     }
   }
 #if HB_GQ
+#ifndef HB_CLK_STEP0
   HB_CLK_MARK(3);
+#endif
   HB_WSYNC();  // the slab values of every lane are in place
   dq_apply(w, vals, dq, t, rw, (int)n, lane);
 #endif

@@ -52,6 +52,23 @@ __device__ __forceinline__ double fast_div(double n, double d) {
   return fma(fma(-d, q, n), y, q);
 }
 
+// sqrt(x) for x >= 0 in the normal range or 0: the v_rsq_f64 seed, one
+// Goldschmidt step and the final residual correction (the sequence behind the
+// library sqrt, without its denormal scaling and class fix-ups), within an
+// ulp.  For square roots whose input is exact and whose output only needs a
+// few ulp (the overlap area's sqrt(r^2 - h^2), asin's half-angle, the
+// projected separation).
+__device__ __forceinline__ double sqrt_fast(double x) {
+  const double y = __builtin_amdgcn_rsq(x);
+  double s = x * y, h = 0.5 * y;
+  const double r = fma(-s, h, 0.5);
+  s = fma(s, r, s);
+  h = fma(h, r, h);
+  const double d = fma(-s, s, x);
+  s = fma(d, h, s);
+  return x == 0.0 ? 0.0 : s;  // rsq(0) = inf
+}
+
 // fdlibm kernels, |r| <= pi/4
 __device__ __forceinline__ double ksin(double x, double z) {
   const double S1 = -1.66666666666666324348e-01, S2 = 8.33333333332248946124e-03,
