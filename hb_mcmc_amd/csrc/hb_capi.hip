@@ -170,6 +170,7 @@ struct hb_ctx {
   double* d_f = nullptr;
   double* d_s = nullptr;          // 1 / max(sigma, 1e-5)
   double2* d_ph = nullptr;        // shared-period phase table, written by every prep launch
+  double* d_tab_pc = nullptr;     // its period [s] (NaN: none yet); one word behind the table
   double* d_rows = nullptr;       // t, f, 1/sigma in lane-row order (hbk::build_rows; one-wave path)
   // per-walker workspace
   int cap = 0;
@@ -272,14 +273,17 @@ extern "C" hb_ctx* hb_create(const double* t, const double* f, const double* sig
   }
   const size_t bytes = sizeof(double) * (size_t)n;
   if (hipMalloc(&c->d_t, bytes) != hipSuccess || hipMalloc(&c->d_f, bytes) != hipSuccess ||
-      hipMalloc(&c->d_s, bytes) != hipSuccess || hipMalloc(&c->d_ph, 2 * bytes) != hipSuccess) {
+      hipMalloc(&c->d_s, bytes) != hipSuccess || hipMalloc(&c->d_ph, 2 * bytes + 16) != hipSuccess) {
     set_err_msg("hb_create: hipMalloc failed");
     hb_destroy(c.release());
     return nullptr;
   }
+  c->d_tab_pc = reinterpret_cast<double*>(c->d_ph + n);
+  const double no_tab = __builtin_nan("");
   if (hipMemcpy(c->d_t, t, bytes, hipMemcpyHostToDevice) != hipSuccess ||
       hipMemcpy(c->d_f, f, bytes, hipMemcpyHostToDevice) != hipSuccess ||
-      hipMemcpy(c->d_s, s.data(), bytes, hipMemcpyHostToDevice) != hipSuccess) {
+      hipMemcpy(c->d_s, s.data(), bytes, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(c->d_tab_pc, &no_tab, sizeof(double), hipMemcpyHostToDevice) != hipSuccess) {
     set_err_msg("hb_create: upload failed");
     hb_destroy(c.release());
     return nullptr;
@@ -325,7 +329,7 @@ extern "C" int hb_ctx_eval_kind(const hb_ctx* c) {
 }
 
 static int run_batch(hb_ctx* c, const double* d_params, int w, double* d_logl, double* d_tmpl,
-                     hipStream_t s, const hbds::AccArgs* acc = nullptr) {
+                     hipStream_t s, const hbds::AccArgs* acc = nullptr, bool prep = true) {
   if (!c) return set_err_msg("null context");
   if (w < 0) return set_err_msg("negative walker count");
   if (w == 0) return 0;
@@ -335,9 +339,10 @@ static int run_batch(hb_ctx* c, const double* d_params, int w, double* d_logl, d
     int rc = hb_reserve(c, w);
     if (rc) return rc;
   }
-  HB_TRY(hbk::launch_prep(d_params, w, c->mags, c->d_wc, s, nullptr, nullptr, c->d_t, c->plan.n, c->d_ph, nullptr, 0,
-                          acc != nullptr ? acc->ord : nullptr, acc != nullptr ? acc->ebin : nullptr),
-         "hb_prep_kernel");
+  if (prep)
+    HB_TRY(hbk::launch_prep(d_params, w, c->mags, c->d_wc, s, nullptr, nullptr, c->d_t, c->plan.n, c->d_ph, nullptr,
+                            0, c->d_tab_pc),
+           "hb_prep_kernel");
   const EvalPlan& pl = (acc == nullptr && c->has_lat && w < kLatencyW) ? c->lat : c->plan;
   HB_TRY(hbk::launch_eval(pl, c->d_t, c->d_ph, c->d_f, c->d_s, c->d_rows, c->d_wc, w, d_logl, d_tmpl, c->d_scratch,
                           d_tmpl ? 1 : 0, s, acc, c->d_dq),
@@ -345,17 +350,32 @@ static int run_batch(hb_ctx* c, const double* d_params, int w, double* d_logl, d
   return 0;
 }
 
-// internal (device sampler): hb_loglik_batch_dev whose eval waves also run
-// their slot's Hastings test (acc: hbds::AccArgs).  1 when the context's plan
-// has no one-wave path (N > 2048): the caller then launches its own accept.
+// internal (device sampler): the likelihood of w walkers whose records
+// ds_propose already wrote into the context's workspace (hbx_ctx_prep_args),
+// the eval waves also running their slot's Hastings test (acc:
+// hbds::AccArgs).  1 when the context's plan has no one-wave path (N > 2048):
+// the caller then launches the eval (hb_evaluate_dev) and its own accept.
 extern "C" int hbx_loglik_accept_dev(hb_ctx* c, const double* d_params, int w, double* d_logl, const void* acc,
                                      void* stream) {
   if (!c) return set_err_msg("null context");
   if (c->plan.vpt == 0) return 1;
+  if (w > c->cap) return set_err_msg("hbx_loglik_accept_dev: W exceeds the prepared workspace");
   static const bool split = getenv("HB_DS_SPLIT_ACCEPT") != nullptr;  // experiment knob: separate ds_accept
   if (split) return 1;
   return run_batch(c, d_params, w, d_logl, nullptr, (hipStream_t)stream,
-                   static_cast<const hbds::AccArgs*>(acc));
+                   static_cast<const hbds::AccArgs*>(acc), false);
+}
+
+// internal (device sampler): where its propose epilogue writes the walker
+// records (valid until the next hb_reserve that grows the workspace), the
+// magnitude data of the Gaia term, and the device word holding the period of
+// the shared phase table (NaN until a prep launch wrote the table)
+extern "C" int hbx_ctx_prep_args(hb_ctx* c, void** wc, void* mags, double** tab_pc) {
+  if (!c) return set_err_msg("null context");
+  *wc = c->d_wc;
+  memcpy(mags, &c->mags, sizeof(MagArgs));
+  *tab_pc = c->d_tab_pc;
+  return 0;
 }
 
 extern "C" int hb_prepare_dev(hb_ctx* c, const double* d_params, int w, void* stream) {
@@ -367,7 +387,7 @@ extern "C" int hb_prepare_dev(hb_ctx* c, const double* d_params, int w, void* st
     if (rc) return rc;
   }
   HB_TRY(hbk::launch_prep(d_params, w, c->mags, c->d_wc, (hipStream_t)stream, nullptr, nullptr, c->d_t, c->plan.n,
-                          c->d_ph),
+                          c->d_ph, nullptr, 0, c->d_tab_pc),
          "hb_prep_kernel");
   return 0;
 }

@@ -36,20 +36,28 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <math.h>
+
 #include <algorithm>
 #include <chrono>
+#include <condition_variable>
+#include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/hb_sampler.h"
 #include "../../include/hbmi.h"
 #include "hb_accept.hpp"
 #include "hb_glibc_math.hpp"
+#include "hb_lagfib.hpp"
+#include "hb_prep.hpp"
 #include "hb_sampler_view.hpp"
 #include "hb_walls.hpp"
 
 extern "C" int hbx_set_error(const char* msg);
 extern "C" int hbx_ctx_device(const hb_ctx* c);
+extern "C" int hbx_ctx_prep_args(hb_ctx* c, void** wc, void* mags, double** tab_pc);
 extern "C" int hbx_loglik_accept_dev(hb_ctx* c, const double* d_params, int w, double* d_logl, const void* acc,
                                      void* stream);
 
@@ -63,18 +71,16 @@ constexpr double AM = 1.0 / IM1;
 constexpr double RNMX = 1.0 - 1.2e-7;
 constexpr double kSqrt2Pi = 2.5066282746;  // mcmc_wrapper2.h:10
 constexpr int kBlk = 64;                   // slots per workgroup of the gather kernel
-#ifndef HB_DS_ABL  // experiment builds only: timing ablations of ds_propose (results are wrong)
-#define HB_DS_ABL 0
-#endif
 #ifndef HB_DS_KPW
 #define HB_DS_KPW 4
 #endif
 constexpr int kPW = HB_DS_KPW;             // propose waves (one slot each) per workgroup
-#ifndef HB_DS_SWAPT  // experiment knob: ds_swap workgroup size
-#define HB_DS_SWAPT 1024
+#ifndef HB_DS_SEG  // experiment knob: owned slots per swap segment
+#define HB_DS_SEG 256
 #endif
-constexpr int kSwapThreads = HB_DS_SWAPT;
-constexpr int kMaxLevels = 255;            // swap levels staged in LDS (W = 4096 needs ~10)
+constexpr int kSegSlots = HB_DS_SEG;       // owned slots per swap segment (one ds_swap_seg workgroup)
+constexpr int kSegThreads = 256;
+constexpr int kMaxLevels = 64;             // swap dependency levels a schedule buffer holds (W = 65 536: ~13)
 
 // run constants (kernel argument)
 struct Params {
@@ -97,10 +103,22 @@ struct SwapEnt {
   int pad;
   double lnb;
 };
-// schedule buffer: SwapEnt[W] | int off[W + 2] | (8-byte aligned) double beta[W]
-__host__ __device__ inline size_t sched_beta_off(size_t W) {
-  return (sizeof(SwapEnt) * W + sizeof(int) * (W + 2) + 7) & ~(size_t)7;
+// schedule buffer of an iteration with nlv levels over G segments:
+// int soff[G nlv + 1] | (8-B aligned) SwapEnt ent[nent] | double beta[nent];
+// segment g's attempts of level l (0-based) are ent[soff[g nlv + l] ..
+// soff[g nlv + l + 1]) -- an attempt near a segment border is listed for
+// every segment whose cone holds its pair
+__host__ __device__ inline size_t sched_ent_off(size_t G, size_t nlv) {
+  return (sizeof(int) * (G * nlv + 1) + 7) & ~(size_t)7;
 }
+__host__ __device__ inline size_t sched_beta_off(size_t G, size_t nlv, size_t nent) {
+  return sched_ent_off(G, nlv) + sizeof(SwapEnt) * nent;
+}
+__host__ __device__ inline size_t sched_bytes(size_t G, size_t nlv, size_t nent) {
+  return sched_beta_off(G, nlv, nent) + sizeof(double) * nent;
+}
+// first slot of segment g of G over the owned slots [lo, lo + nl)
+__host__ __device__ inline int seg_lo(int lo, int nl, int g, int G) { return lo + (int)((long long)nl * g / G); }
 
 // device state (pointers into one allocation set)
 struct Dev {
@@ -111,10 +129,14 @@ struct Dev {
   double* logL;    // [W] by chain
   double* logP;    // [W] by chain
   int* logP_ok;    // [W] by chain
-  int* idx;        // [W] slot -> chain
+  int* idx;        // [W] slot -> chain (the current iteration's)
+  int* idx_out;    // [W] the other buffer: ds_swap_seg writes the next iteration's index[] there
   int* order;      // [nl] propose wave -> (global) slot, hottest rungs first (dispatch order)
-  int* eord;       // [nl] eval wave -> local slot, by descending e of the proposal (written by the prep launch)
-  unsigned char* ebin;  // [nl] e bin of each proposal (e_bin_desc), the key of eord
+  int* ecnt;       // [kOrdBins] proposals per e bin (AccArgs::ecnt; null: eval waves in slot order)
+  int* elist;      // [kOrdBins][nl] local slots by e bin
+  double* wc;      // [nl] WalkerConst records (the context's workspace; set per launch)
+  hbk::MagArgs ma; // Gaia term data of the context
+  const double* tab_pc;  // period of the context's phase table (NaN: none)
   double* temp;    // [W]
   int* idum;       // [nl] ran2 state by slot
   int* idum2;
@@ -311,7 +333,7 @@ __device__ double gauss_batch(WaveStream& S, int& iset, double& gset, const hbgl
     pos = 1;
     iset = 0;
   }
-  while (pos < kNp && HB_DS_ABL != 3 && HB_DS_ABL < 6) {
+  while (pos < kNp) {
     S.slide();
     const int need = uni((kNp - pos + 1) / 2);          // pairs still to generate
     const int att = uni(min(32, need + need / 2 + 2));  // attempts tested this round (acceptance pi/4)
@@ -363,11 +385,16 @@ __device__ double gauss_batch(WaveStream& S, int& iset, double& gset, const hbgl
 // hot rungs' long wall runs are dispatched first, and a workgroup's waves
 // (spread over its CU's SIMDs) share each SIMD with colder slots of the CU's
 // later workgroups (measured 37.5 -> 35.2 us against order[b + w grid]).
+// Epilogue: the workgroup's four waves become one prep group (hb_prep.hpp)
+// and write the likelihood's per-walker records of their slots, and each
+// slot is filed under its e bin for the eval launch's order -- the likelihood
+// launch follows directly, with no prep launch in between.
 // The iteration's swap schedule (n8 words) is copied from the pinned ring
 // entry into its device ring entry on the way (the coldest slots' waves, which
 // finish first, issue the reads; system-scope loads bypass the GPU caches),
 // so ds_swap depends on nothing outside this stream: a separate copy stream
 // cost an inter-queue event wait of ~10 us per iteration before ds_swap.
+static_assert(kPW == hbk::kPrepRoles, "the propose workgroup is one prep group");
 __global__ __launch_bounds__(64 * kPW) void ds_propose(Dev D, int W, int NPAST, long long iter,
                                                        const unsigned long long* __restrict__ sch_src,
                                                        unsigned long long* __restrict__ sch_dst, long long n8) {
@@ -377,6 +404,8 @@ __global__ __launch_bounds__(64 * kPW) void ds_propose(Dev D, int W, int NPAST, 
   if (sgt < n8) sv = __hip_atomic_load(sch_src + sgt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   __shared__ uint64_t tab_s[hbglibc::kTabWords];  // exp / log / pow tables (divergent lookups)
   __shared__ double gs_s[kPW][32];
+  __shared__ hbk::PrepShared<kPW> PL;
+  __shared__ int jl_s[kPW];
   const Params* P = D.P;
   const hbglibc::Tabs T{tab_s, tab_s + 256, tab_s + 512};
   {
@@ -396,6 +425,7 @@ __global__ __launch_bounds__(64 * kPW) void ds_propose(Dev D, int W, int NPAST, 
   const int j = act ? D.order[k] : D.lo;  // global slot
   const int jl = j - D.lo;                // local slot (arrays by slot)
   double* gs = gs_s[wv];
+  const double pc_tab = *D.tab_pc;
 #ifdef HB_DS_TIMING  // experiment builds only: per-phase shader clocks of two slots at iteration 100
   long long tclk[8], tw0 = wall_clock64();
 #define DS_T(k) tclk[k] = clock64()
@@ -421,115 +451,122 @@ __global__ __launch_bounds__(64 * kPW) void ds_propose(Dev D, int W, int NPAST, 
   if (sgt < n8) sch_dst[sgt] = sv;
   for (long long q = sgt + sgs; q < n8; q += sgs)
     sch_dst[q] = __hip_atomic_load(sch_src + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-#if HB_DS_ABL == 4
-  return;
-#endif
-  if (!act) return;
-  DS_T(1);
-
-  const double a = S.uniform();
-  DS_T(2);
-#if HB_DS_ABL >= 7
-  const double jscale = a;
-#else
-  const double jscale = hbglibc::pow(10., -6. + 6. * a, T);
-#endif
-  int jmp = 0, jt = 0;
-  if ((S.uniform() < 0.5) && (iter > NPAST)) jmp = 1;
-  double yn = xn;
-  // gaussian_proposal_parallel (:1062-1088)
-  auto gaussian_step = [&]() {
-    const double sqtemp = sqrt(temp);
-    const double g = gauss_batch(S, iset, gset, T, gs);
-    if (lane < kNp) yn = xn + g * P->sigma_p[lane] * sqtemp * jscale;
-  };
-  if (jmp == 0) {
-    gaussian_step();
-    jt = 1;
-  }
-  if (jmp == 1) {
-    if (chain == 0 && lane == 0) {
-      D.DEtrial_arr[jl]++;
-      atomicAdd((unsigned long long*)&D.ctr->DEtrial_tot, 1ull);
-    }
-    // differential_evolution_proposal_parallel (:1091-1140) as compiled (see
-    // hb_sampler.cpp de_step: a == 0, the uninitialised c == 0).  The 0.9
-    // draw precedes the per-parameter Gaussians, as in the reference.
-    int ia = (int)(S.uniform() * NPAST);
-    ia = (int)S.uniform();
-    int ib = ia;
-    while (ib == ia) ib = (int)(S.uniform() * NPAST);
-    const double g0 = gauss_pdf(0, 0, 1.e-4, T) - 0.5;
-    const bool scaled = S.uniform() < 0.9;
-    const double gamma = 2.388 / sqrt(2. * kNp);  // GAMMA, mcmc_wrapper2.h:13
-    const double gd = scaled ? gauss_batch(S, iset, gset, T, gs) : 0.0;
-    if (lane < kNp) {
-      const double* hist = &D.hist[(size_t)jl * NPAST * kNp];
-      double dx = hist[(size_t)ib * kNp + lane] - hist[(size_t)ia * kNp + lane];
-      const double eps = dx * g0;
-      if (scaled) dx *= gd * gamma;
-      dx += eps;
-      yn = xn + dx;
-    }
-    jt = 2;
-    double dx_mag = 0;  // summed in coordinate order
-    const double d = xn - yn;
-    for (int i = 0; i < kNp; ++i) {
-      const double di = rld(d, i);
-      dx_mag += di * di;
-    }
-    if (dx_mag < 1e-6) {
+  if (act) {  // wave-uniform; every wave reaches the prep group's barriers below
+    DS_T(1);
+    const double a = S.uniform();
+    DS_T(2);
+    const double jscale = hbglibc::pow(10., -6. + 6. * a, T);
+    int jmp = 0, jt = 0;
+    if ((S.uniform() < 0.5) && (iter > NPAST)) jmp = 1;
+    double yn = xn;
+    // gaussian_proposal_parallel (:1062-1088)
+    auto gaussian_step = [&]() {
+      const double sqtemp = sqrt(temp);
+      const double g = gauss_batch(S, iset, gset, T, gs);
+      if (lane < kNp) yn = xn + g * P->sigma_p[lane] * sqtemp * jscale;
+    };
+    if (jmp == 0) {
       gaussian_step();
       jt = 1;
     }
-  }
-  DS_T(3);
-  DS_T(4);
-  // walls (:440-467), one coordinate per lane
-#if HB_DS_ABL != 1 && HB_DS_ABL < 5
-  if (lane < kNp) yn = hbwall::apply_wall(yn, P->lim_lo[lane], P->lim_hi[lane], P->fl_lo[lane], P->fl_hi[lane]);
-#endif
-  // "order the masses" (:470-475) as written: y[1] = y[0]; period fixed; T0 folded
-  const double y0 = rld(yn, 0), y1 = rld(yn, 1);
-  if (lane == 1 && y1 > y0) yn = y0;
-  if (lane == 2) yn = P->log_lc_period;
-  if (lane == 6) yn = fmod(yn, P->LC_PERIOD);
-  DS_T(5);
-  // prior terms (:444, :477), summed per slot in the reference's order
-  const bool prior = lane < kNp && P->gpflag[lane] == 1 && HB_DS_ABL != 2 && HB_DS_ABL < 5;
-  const double ty = prior ? prior_term(lane, yn, T) : 0.0;
-  const double tx = (needx && prior) ? prior_term(lane, xn, T) : 0.0;
-  double lpy = 0., lpx = 0.;
-  for (int i = 0; i < kNp; ++i) {
-    if (P->gpflag[i] != 1) continue;
-    lpy += rld(ty, i);
-    if (needx) lpx += rld(tx, i);
-  }
-  DS_T(6);
-  // the alpha draw and the retirement of the consumed draws only feed the
-  // stored state, so they follow the walls (off the hot slots' critical path)
-  const double alpha2 = S.uniform();  // drawn after the likelihood calls in the reference; same stream order
-  S.slide();
-  if (lane < kNp) D.y[(size_t)jl * kNp + lane] = yn;
-  if (lane == 3) D.ebin[jl] = (unsigned char)e_bin_desc(yn);  // the eval order's key (hb_prep_kernel)
-  if (lane < NTAB) D.iv[(size_t)jl * NTAB + lane] = S.b_tab;
-  if (lane == 0) {
-    D.logPy[jl] = lpy;
-    if (needx) {
-      D.logP[chain] = lpx;
-      D.logP_ok[chain] = 1;
+    if (jmp == 1) {
+      if (chain == 0 && lane == 0) {
+        D.DEtrial_arr[jl]++;
+        atomicAdd((unsigned long long*)&D.ctr->DEtrial_tot, 1ull);
+      }
+      // differential_evolution_proposal_parallel (:1091-1140) as compiled (see
+      // hb_sampler.cpp de_step: a == 0, the uninitialised c == 0).  The 0.9
+      // draw precedes the per-parameter Gaussians, as in the reference.
+      int ia = (int)(S.uniform() * NPAST);
+      ia = (int)S.uniform();
+      int ib = ia;
+      while (ib == ia) ib = (int)(S.uniform() * NPAST);
+      const double g0 = gauss_pdf(0, 0, 1.e-4, T) - 0.5;
+      const bool scaled = S.uniform() < 0.9;
+      const double gamma = 2.388 / sqrt(2. * kNp);  // GAMMA, mcmc_wrapper2.h:13
+      const double gd = scaled ? gauss_batch(S, iset, gset, T, gs) : 0.0;
+      if (lane < kNp) {
+        const double* hist = &D.hist[(size_t)jl * NPAST * kNp];
+        double dx = hist[(size_t)ib * kNp + lane] - hist[(size_t)ia * kNp + lane];
+        const double eps = dx * g0;
+        if (scaled) dx *= gd * gamma;
+        dx += eps;
+        yn = xn + dx;
+      }
+      jt = 2;
+      double dx_mag = 0;  // summed in coordinate order
+      const double d = xn - yn;
+      for (int i = 0; i < kNp; ++i) {
+        const double di = rld(d, i);
+        dx_mag += di * di;
+      }
+      if (dx_mag < 1e-6) {
+        gaussian_step();
+        jt = 1;
+      }
     }
-    D.jump[jl] = jmp;
-    D.jtype[jl] = jt;
-    D.alpha2[jl] = alpha2;
-    D.idum[jl] = S.b_idum;
-    D.idum2[jl] = S.b_idum2;
-    D.iy[jl] = S.b_iy;
-    D.iset[jl] = iset;
-    D.gset[jl] = gset;
-    D.cts[jl] += S.consumed;
-  DS_T(7);
-  DS_PRINT();
+    DS_T(3);
+    DS_T(4);
+    // walls (:440-467), one coordinate per lane
+    if (lane < kNp) yn = hbwall::apply_wall(yn, P->lim_lo[lane], P->lim_hi[lane], P->fl_lo[lane], P->fl_hi[lane]);
+    // "order the masses" (:470-475) as written: y[1] = y[0]; period fixed; T0 folded
+    const double y0 = rld(yn, 0), y1 = rld(yn, 1);
+    if (lane == 1 && y1 > y0) yn = y0;
+    if (lane == 2) yn = P->log_lc_period;
+    if (lane == 6) yn = fmod(yn, P->LC_PERIOD);
+    DS_T(5);
+    // prior terms (:444, :477), summed per slot in the reference's order
+    const bool prior = lane < kNp && P->gpflag[lane] == 1;
+    const double ty = prior ? prior_term(lane, yn, T) : 0.0;
+    const double tx = (needx && prior) ? prior_term(lane, xn, T) : 0.0;
+    double lpy = 0., lpx = 0.;
+    for (int i = 0; i < kNp; ++i) {
+      if (P->gpflag[i] != 1) continue;
+      lpy += rld(ty, i);
+      if (needx) lpx += rld(tx, i);
+    }
+    DS_T(6);
+    // the alpha draw and the retirement of the consumed draws only feed the
+    // stored state, so they follow the walls (off the hot slots' critical path)
+    const double alpha2 = S.uniform();  // drawn after the likelihood calls in the reference; same stream order
+    S.slide();
+    if (lane < kNp) {
+      D.y[(size_t)jl * kNp + lane] = yn;
+      PL.sp[wv * hbk::kNpars + lane] = yn;
+    }
+    if (lane == 3 && D.ecnt != nullptr) {  // the eval order (hbds::eval_slot_by_e)
+      const int b = e_bin_desc(yn);
+      D.elist[(size_t)b * D.nl + atomicAdd(&D.ecnt[b], 1)] = jl;
+    }
+    if (lane < NTAB) D.iv[(size_t)jl * NTAB + lane] = S.b_tab;
+    if (lane == 0) {
+      jl_s[wv] = jl;
+      D.logPy[jl] = lpy;
+      if (needx) {
+        D.logP[chain] = lpx;
+        D.logP_ok[chain] = 1;
+      }
+      D.jump[jl] = jmp;
+      D.jtype[jl] = jt;
+      D.alpha2[jl] = alpha2;
+      D.idum[jl] = S.b_idum;
+      D.idum2[jl] = S.b_idum2;
+      D.iy[jl] = S.b_iy;
+      D.iset[jl] = iset;
+      D.gset[jl] = gset;
+      D.cts[jl] += S.consumed;
+      DS_T(7);
+      DS_PRINT();
+    }
+  }
+  // the likelihood's per-walker records of the group's slots: every wave
+  // reads the others' proposals from PL.sp
+  const int nb = min(kPW, D.nl - (int)blockIdx.x * kPW);
+  __syncthreads();
+  hbk::prep_records<kPW>(PL, nb, D.ma, nullptr, nullptr, 0, [&](int) { return pc_tab; }, [] {});
+  for (int q = threadIdx.x; q < nb * hbk::kWcDoubles; q += 64 * kPW) {
+    const int w = q / hbk::kWcDoubles, f = q - w * hbk::kWcDoubles;
+    D.wc[(size_t)jl_s[w] * hbk::kWcDoubles + f] = PL.so[q];
   }
 }
 
@@ -609,24 +646,6 @@ __global__ __launch_bounds__(kAccThreads) void ds_accept(Dev D, int W, int NPAST
   }
 }
 
-// index[] accessors: LDS (small W) or device-coherent global (large W)
-template <bool LDS>
-struct IdxRef {
-  int* p;
-  __device__ int ld(int i) const {
-    if (LDS) return p[i];
-    return __hip_atomic_load(p + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  __device__ void st(int i, int v) const {
-    if (LDS) p[i] = v;
-    else __hip_atomic_store(p + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-};
-
-// the W tempering attempts (ptmcmc :768-817) in dependency levels, then the
-// per-iteration bookkeeping of :551-572 / :590 / :639-641
-// LDS mode stages the schedule, logL by chain, the pair factors and index[]
-// (36 W bytes) so that a level costs LDS latency only.
 // Sharded runs: what a rank contributes to the iteration's all-gather
 // (doubles): logL of its slots (padded to m = the largest shard), then K = 2
 // nlv records of kRec doubles {chain, logP, logP_ok, x[21]} -- the chains in
@@ -653,7 +672,7 @@ __global__ __launch_bounds__(kPackThreads) void ds_pack(Dev D, double* __restric
   send[m + r] = v;
 }
 
-// what ds_swap imports in a sharded run (G == nullptr: single process)
+// what ds_swap_seg imports in a sharded run
 struct Gathered {
   const double* G;  // [R][S]: each rank's ds_pack output
   long long S;      // doubles per rank
@@ -661,168 +680,149 @@ struct Gathered {
   int pad;
 };
 
-template <bool LDS>
-__global__ __launch_bounds__(kSwapThreads) void ds_swap(Dev D, int W, const SwapEnt* __restrict__ sched,
-                                                         const int* __restrict__ off, int nlv, long long iter,
-                                                         Gathered X) {
+// the per-iteration bookkeeping after the swaps (:551-572, :590, :622-629)
+// by thread 0 of one workgroup; c0 = the chain now in slot 0 (-1: not this
+// rank's slot).  nswap is added by every segment (atomics).
+__device__ __forceinline__ void swap_tail(const Dev& D, long long iter, int c0) {
+  Counters* C = D.ctr;
+  C->acc += C->acc_it;  // hb_sampler_accept's sums over the slots
+  C->cold_acc += C->acc_it;
+  C->DEacc += C->DEacc_tot;
+  C->DEtrial += C->DEtrial_tot;
+  C->acc_it = 0;
+  C->snap[0] = C->acc;
+  C->snap[1] = C->DEacc;
+  C->snap[2] = C->DEtrial;
+  C->snap[3] = C->atrial;
+  if (c0 >= 0 && D.logL[c0] > C->logLmap) {  // :565-572
+    for (int i = 0; i < kNp; ++i) C->xmap[i] = D.x[(size_t)c0 * kNp + i];
+    C->logLmap = D.logL[c0];
+  }
+  C->atrial++;  // :590 and the 100-step reset of :622-629
+  if (iter % 100 == 0) {
+    C->acc = C->atrial = 0;
+    C->DEacc_tot = C->DEtrial_tot = 0;
+  }
+}
+
+// Tempering swaps (ptmcmc :768-817) and the iteration's bookkeeping, one
+// workgroup per segment [sl, sh) of the owned slots.  A level moves a slot's
+// content by one, so after the nlv levels the chains of [sl, sh) come from the
+// cone [sl - nlv, sh + nlv), and the attempts left out of the cone can disturb
+// only slots within nlv - 1 of its edges, never [sl, sh): the workgroup
+// replays in LDS just the cone's attempts (listed per segment and level by the
+// producer thread) on the cone's (logL, chain) pairs and writes the owned
+// slots' chains into the other index[] buffer, so the neighbouring segments
+// still read the iteration's index[] for their cones.  An attempt with b in
+// [sl, sh) sees exact inputs at every level and counts there (nswap).  No
+// workgroup replays more than kSegSlots + 2 nlv slots, so the swap step is a
+// wide launch instead of one workgroup walking all W attempts.
+// XCHG (sharded runs and the one-rank exchange path): logL by slot comes from
+// the all-gather (the owner rank's block) and the chain ids of other ranks'
+// slots from their edge records, which also carry the state and logL of a
+// chain that moves into an owned slot.
+template <bool XCHG>
+__global__ __launch_bounds__(kSegThreads) void ds_swap_seg(Dev D, int W, const int* __restrict__ soff,
+                                                            const SwapEnt* __restrict__ ent,
+                                                            const double* __restrict__ betas, int nlv, int G,
+                                                            long long iter, Gathered X) {
   extern __shared__ __align__(16) unsigned char smem[];
   __shared__ int nacc_s;
-  __shared__ int off_s[kMaxLevels + 1];
-  __shared__ uint64_t exp_s[256];  // exp table for the divergent lookups of the level loop
-  const int tid = threadIdx.x;
-#ifdef HB_DS_TIMING
-  const long long sstart = clock64();
-#endif
-  for (int q = tid; q < 256; q += kSwapThreads) exp_s[q] = hbglibc::kExpTab[q];
+  __shared__ uint64_t exp_s[256];  // exp table for the divergent lookups of the band case
+  const int tid = threadIdx.x, g = blockIdx.x;
+  const int lo = D.lo, hi = D.lo + D.nl;
+  const int sl = seg_lo(lo, D.nl, g, G), sh = seg_lo(lo, D.nl, g + 1, G);
+  const int clo = max(0, sl - nlv), chi = min(W, sh + nlv), Wc = chi - clo;
+  double* cL = reinterpret_cast<double*>(smem);
+  int* cC = reinterpret_cast<int*>(smem + sizeof(double) * (size_t)Wc);
+  for (int q = tid; q < 256; q += kSegThreads) exp_s[q] = hbglibc::kExpTab[q];
   const hbglibc::Tabs T{exp_s, hbglibc::kLogTab, hbglibc::kPowTab};
-  const bool off_lds = nlv <= kMaxLevels;
-  if (X.G) {
-    // sharded: logL of every slot (by its chain before the swap), then the
-    // other ranks' edge records -- each chain is owned by one rank, so no two
-    // ranks write the same chain (a rank's overlapping edges repeat a record)
-    for (int r = 0; r < X.R; ++r) {
-      const int lo_r = (int)((long long)W * r / X.R), n_r = (int)((long long)W * (r + 1) / X.R) - lo_r;
-      const double* g = X.G + (size_t)r * X.S;
-      for (int i = tid; i < n_r; i += kSwapThreads) D.logL[D.idx[lo_r + i]] = g[i];
+  if (!XCHG) {
+    for (int i = tid; i < Wc; i += kSegThreads) {
+      const int c = D.idx[clo + i];
+      cC[i] = c;
+      cL[i] = D.logL[c];
     }
-    const int nrec = (int)((X.S - X.m) / kRec);
+  } else {
+    auto rlo = [&](int r) { return (int)((long long)W * r / X.R); };
+    for (int i = tid; i < Wc; i += kSegThreads) {
+      const int s = clo + i;
+      int r = (int)(((long long)s * X.R) / W);
+      while (r + 1 < X.R && rlo(r + 1) <= s) ++r;
+      while (r > 0 && rlo(r) > s) --r;
+      cL[i] = X.G[(size_t)r * X.S + (s - rlo(r))];
+      if (s >= lo && s < hi) cC[i] = D.idx[s];
+    }
+    // the other ranks' edge records inside the cone: chain id by slot, and the
+    // chain's record and logL for the case it moves into an owned slot (two
+    // segments whose cones share a record write the same values)
+    const int nrec = (int)((X.S - X.m) / kRec), ke = nrec / 2;
     for (int r = 0; r < X.R; ++r) {
       if (r == X.me) continue;
-      const double* g = X.G + (size_t)r * X.S + X.m;
-      for (int q = tid; q < nrec * kRec; q += kSwapThreads) {
+      const int lo_r = rlo(r), nl_r = rlo(r + 1) - lo_r;
+      if (lo_r >= chi || lo_r + nl_r <= clo) continue;
+      const double* gr = X.G + (size_t)r * X.S + X.m;
+      for (int q = tid; q < nrec * kRec; q += kSegThreads) {
         const int kk = q / kRec, f = q - kk * kRec;
-        const int c = (int)g[(size_t)kk * kRec];
-        if (c < 0 || f == 0) continue;
-        const double v = g[q];
-        if (f == 1) D.logP[c] = v;
-        else if (f == 2) D.logP_ok[c] = (int)v;
-        else D.x[(size_t)c * kNp + (f - 3)] = v;
+        const int c = (int)gr[(size_t)kk * kRec];
+        if (c < 0) continue;
+        const int slot = lo_r + (kk < ke ? kk : nl_r - 2 * ke + kk);
+        if (slot < clo || slot >= chi) continue;
+        const double v = gr[q];
+        if (f == 0) {
+          cC[slot - clo] = c;
+          D.logL[c] = X.G[(size_t)r * X.S + (slot - lo_r)];
+        } else if (f == 1) {
+          D.logP[c] = v;
+        } else if (f == 2) {
+          D.logP_ok[c] = (int)v;
+        } else {
+          D.x[(size_t)c * kNp + (f - 3)] = v;
+        }
+      }
+    }
+  }
+  if (tid == 0) nacc_s = 0;
+  __syncthreads();
+  // the levels.  One attempt (:782-812): exp(x) >= beta decided by x against
+  // ln(beta) outside a band of 1e-12 (1 + |ln beta|), far wider than the ulp
+  // errors of the host log and of exp; inside the band (or beta = 0, NaN x)
+  // the glibc-exact exp is compared with beta itself
+  int nacc = 0;
+  for (int lv = 0; lv < nlv; ++lv) {
+    const int e0 = soff[g * nlv + lv], e1 = soff[g * nlv + lv + 1];
+    for (int q = e0 + tid; q < e1; q += kSegThreads) {
+      const int b = ent[q].b;
+      const double lnb = ent[q].lnb;
+      const int bl = b - clo, al = bl + 1;
+      const double lb = cL[bl], la = cL[al];
+      const double x = (lb - la) * D.hs[b];  // (L[idx b] - L[idx a]) (T_b - T_a)/(T_b T_a), :803
+      bool acc;
+      const double dl = 1e-12 * (1.0 + fabs(lnb));
+      if (lnb > -HUGE_VAL && x >= lnb + dl) acc = true;
+      else if (lnb > -HUGE_VAL && x <= lnb - dl) acc = false;
+      else acc = hbglibc::exp(x, T) >= betas[q];
+      if (acc) {
+        const int ca = cC[al], cb = cC[bl];
+        cL[al] = lb;
+        cL[bl] = la;
+        cC[al] = cb;
+        cC[bl] = ca;
+        if (b >= sl && b < sh) ++nacc;
       }
     }
     __syncthreads();
   }
-  const SwapEnt* S = sched;
-  const double* betas = reinterpret_cast<const double*>(reinterpret_cast<const unsigned char*>(sched) +
-                                                         sched_beta_off((size_t)W));
-  const double* L = D.logL;
-  const double* hs = D.hs;
-  IdxRef<LDS> idx{D.idx};
-  if (off_lds)
-    for (int l = tid; l <= nlv; l += kSwapThreads) off_s[l] = off[l];
-  if (LDS) {
-    SwapEnt* s_l = reinterpret_cast<SwapEnt*>(smem);
-    double* L_l = reinterpret_cast<double*>(smem + sizeof(SwapEnt) * (size_t)W);
-    double* h_l = L_l + W;
-    int* i_l = reinterpret_cast<int*>(h_l + W);
-    const int nent = off[nlv];
-    for (int c = tid; c < W; c += kSwapThreads) {
-      L_l[c] = D.logL[c];
-      h_l[c] = D.hs[c];
-      i_l[c] = D.idx[c];
-    }
-    for (int q = tid; q < nent; q += kSwapThreads) s_l[q] = sched[q];
-    S = s_l;
-    L = L_l;
-    hs = h_l;
-    idx.p = i_l;
-  }
-  if (tid == 0) nacc_s = 0;
-  __syncthreads();
-#ifdef HB_DS_TIMING
-  const long long sw0 = clock64();
-#endif
-  int nacc = 0;
-  // one attempt: exp(x) >= beta (:803-806) decided by x against ln(beta)
-  // outside a band of 1e-12 (1 + |ln beta|), far wider than the ulp errors of
-  // the host log and of exp; inside the band (or beta = 0, NaN x) the
-  // glibc-exact exp is compared with beta itself
-  auto attempt = [&](int s, int b, double lnb, double Hs) {
-    const int a = b + 1;
-    const int olda = idx.ld(a), oldb = idx.ld(b);
-    const double x = (L[oldb] - L[olda]) * Hs;  // Hs = (temp[b] - temp[a]) / (temp[b] temp[a]) (:803)
-    bool acc;
-    const double dl = 1e-12 * (1.0 + fabs(lnb));
-    if (lnb > -HUGE_VAL && x >= lnb + dl) acc = true;
-    else if (lnb > -HUGE_VAL && x <= lnb - dl) acc = false;
-    else acc = hbglibc::exp(x, T) >= betas[s];
-    if (acc) {
-      idx.st(a, oldb);
-      idx.st(b, olda);
-      ++nacc;
-    }
-  };
-  auto offset = [&](int l) { return off_lds ? off_s[l] : off[l]; };
-  // software pipeline: a thread's first attempt of level lv + 1 (pair, ln beta,
-  // pair factor -- none depends on index[]) is loaded while level lv runs, so
-  // a level waits only for its index[] and logL reads
-  int s_cur = nlv > 0 ? offset(0) + tid : 0;
-  int e_cur = nlv > 0 ? offset(1) : 0;
-  int b_cur = 0;
-  double lnb_cur = 0.0, hs_cur = 0.0;
-  if (s_cur < e_cur) {
-    b_cur = S[s_cur].b;
-    lnb_cur = S[s_cur].lnb;
-    hs_cur = hs[b_cur];
-  }
-  for (int lv = 0; lv < nlv; ++lv) {
-    const int e0 = s_cur - tid;
-    const int s_nx = e_cur + tid;
-    const int e_nx = lv + 1 < nlv ? offset(lv + 2) : 0;
-    int b_nx = 0;
-    double lnb_nx = 0.0, hs_nx = 0.0;
-    if (s_nx < e_nx) {
-      b_nx = S[s_nx].b;
-      lnb_nx = S[s_nx].lnb;
-      hs_nx = hs[b_nx];
-    }
-    if (s_cur < e_cur) attempt(s_cur, b_cur, lnb_cur, hs_cur);
-    for (int s = e0 + tid + kSwapThreads; s < e_cur; s += kSwapThreads) attempt(s, S[s].b, S[s].lnb, hs[S[s].b]);
-    __syncthreads();
-    s_cur = s_nx;
-    e_cur = e_nx;
-    b_cur = b_nx;
-    lnb_cur = lnb_nx;
-    hs_cur = hs_nx;
-  }
   if (nacc) atomicAdd(&nacc_s, nacc);
-#ifdef HB_DS_TIMING
-  const long long sw1 = clock64();
-#endif
-  if (LDS) {
-    for (int c = tid; c < W; c += kSwapThreads) D.idx[c] = idx.ld(c);
-    idx.p = D.idx;
-  }
+  for (int s = sl + tid; s < sh; s += kSegThreads) D.idx_out[s] = cC[s - clo];
+  if (iter % 100 == 0)
+    for (int s = sl + tid; s < sh; s += kSegThreads) D.DEacc_arr[s - lo] = D.DEtrial_arr[s - lo] = 0;
+  if (g == 0 && D.ecnt != nullptr && tid < kOrdBins) D.ecnt[tid] = 0;  // the eval launch read them
   __syncthreads();
-  Counters* C = D.ctr;
-  const bool reset = (iter % 100 == 0);
   if (tid == 0) {
-    C->acc += C->acc_it;  // hb_sampler_accept's sums over the slots
-    C->cold_acc += C->acc_it;
-    C->DEacc += C->DEacc_tot;
-    C->DEtrial += C->DEtrial_tot;
-    C->acc_it = 0;
-    C->nswap += nacc_s;
-    C->snap[0] = C->acc;
-    C->snap[1] = C->DEacc;
-    C->snap[2] = C->DEtrial;
-    C->snap[3] = C->atrial;
-    const int c0 = idx.ld(0);  // :565-572
-    if (D.logL[c0] > C->logLmap) {
-      for (int i = 0; i < kNp; ++i) C->xmap[i] = D.x[(size_t)c0 * kNp + i];
-      C->logLmap = D.logL[c0];
-    }
-    C->atrial++;  // :590 and the 100-step reset of :622-629
-    if (reset) {
-      C->acc = C->atrial = 0;
-      C->DEacc_tot = C->DEtrial_tot = 0;
-    }
+    if (nacc_s) atomicAdd((unsigned long long*)&D.ctr->nswap, (unsigned long long)nacc_s);
+    if (g == 0) swap_tail(D, iter, lo == 0 ? cC[0 - clo] : -1);
   }
-  if (reset)
-    for (int c = tid; c < D.nl; c += kSwapThreads) D.DEacc_arr[c] = D.DEtrial_arr[c] = 0;
-#ifdef HB_DS_TIMING
-  if (tid == 0 && iter == 100)
-    printf("swap: start->staged %lld levels(%d) %lld tail %lld\n", sw0 - sstart, nlv, sw1 - sw0, clock64() - sw1);
-#endif
 }
 
 // states and logL of the owned slots, by local slot (writer / verbose / download)
@@ -878,27 +878,41 @@ struct hb_dsampler {
   // one-rank one made by hb_dsampler_create_shard (the exchange path on a
   // single GPU: RCCL world size 1 in tests)
   bool xchg = false;
-  bool lds_swap = true;
   bool no_eord = getenv("HB_DS_NO_EORD") != nullptr;  // experiment knob: eval waves in slot order
-  bool copy_stream = getenv("HB_DS_COPY_STREAM") != nullptr;  // A/B knob: schedule copy on cst (old path)
-  size_t swap_lds = 0;
   std::vector<void*> allocs;
-  // swap schedules: pinned ring -> device ring, copied on their own stream
-  // (they do not depend on GPU results) so the copy overlaps the iteration's
-  // kernels; the swap launch waits on the copy's event
-  static constexpr int R_RING = 4;
-  hipStream_t cst = nullptr;
+  std::vector<int> order;  // owned slots in descending temperature (ds_propose's wave order)
+  // Swap schedules (SwapEnt | off | beta, compact), drawn ahead by producer
+  // threads: the draws and levels of an iteration do not depend on any GPU
+  // result, and hb_lagfib.hpp puts the glibc stream of iteration q at a known
+  // offset (2 W q draws past the stream's state at creation), so the
+  // schedules of several iterations are built in parallel, off the issuing
+  // thread.  Iteration q uses ring slot q % R_RING: pinned -> copied into the
+  // device slot by ds_propose (system-scope loads of the coldest waves).
+  static constexpr int R_RING = 8;
   unsigned char* pin[R_RING] = {};
   unsigned char* d_sched[R_RING] = {};
-  hipEvent_t ev_copy[R_RING] = {};   // copy r done
-  hipEvent_t ev_used[R_RING] = {};   // swap that read ring entry r done
-  bool used[R_RING] = {};
-  int ring = 0;
-  size_t sched_bytes = 0;
-  std::vector<int> b, last, lvl, cnt, order;
-  std::vector<double> beta;
+  hipEvent_t ev_used[R_RING] = {};  // the swap that read ring slot r done
+  struct Slot {
+    long long q = -1;       // iteration it holds (-1: never used)
+    bool ready = false;     // schedule written
+    bool released = false;  // its ds_swap_seg is enqueued and ev_used recorded
+    bool overflow = false;  // more than kMaxLevels levels or sched_cap bytes: the step fails
+    int nent = 0, nlv = 0;
+  };
+  Slot slots[R_RING];
+  std::mutex smu;
+  std::condition_variable scv;
+  std::vector<std::thread> workers;
+  bool stop = false;
+  long long q_prod = 0, q_cons = 0, q_synced = 0;  // produced / consumed / skipped on the host stream
+  uint32_t base_w[31] = {};                         // the swap stream at creation (hb_lagfib.hpp window)
+  size_t sched_cap = 0;                             // bytes per ring slot
+  int nthreads = 0;
+  int nseg = 1;  // swap segments (ds_swap_seg workgroups) over the owned slots
+  // host timers [s]: producer work (all threads), waits for a schedule, issue
+  double t_prod = 0.0, t_wait = 0.0, t_issue = 0.0;
   // the iteration between step_begin and step_end
-  int cur_ring = -1, cur_nlv = 0;
+  int cur_slot = -1;
   long cur_iter = -1;
   long cur_n = 0;
   // staging for gathers / counters / events
@@ -909,18 +923,21 @@ struct hb_dsampler {
   Counters* h_ctr = nullptr;
   Event* h_ev = nullptr;
   ~hb_dsampler() {
+    {
+      std::lock_guard<std::mutex> lk(smu);
+      stop = true;
+    }
+    scv.notify_all();
+    for (std::thread& t : workers) t.join();
     if (st) (void)hipStreamSynchronize(st);
-    if (cst) (void)hipStreamSynchronize(cst);
     for (void* p : allocs) (void)hipFree(p);
     for (int r = 0; r < R_RING; ++r) {
       if (pin[r]) (void)hipHostFree(pin[r]);
-      if (ev_copy[r]) (void)hipEventDestroy(ev_copy[r]);
       if (ev_used[r]) (void)hipEventDestroy(ev_used[r]);
     }
     if (h_ctr) (void)hipHostFree(h_ctr);
     if (h_ev) (void)hipHostFree(h_ev);
     if (st) (void)hipStreamDestroy(st);
-    if (cst) (void)hipStreamDestroy(cst);
   }
   template <class T>
   hipError_t alloc(T** p, size_t n) {
@@ -931,6 +948,145 @@ struct hb_dsampler {
 };
 
 static int ds_upload(hb_dsampler* d, const int* chain_of_slot);
+
+// Builds iteration q's swap schedule into ring slot `slot`: the 2W draws of
+// ptmcmc (:791, :810) from the stream jumped to 2 W q draws past creation,
+// the dependency levels (attempt i follows every earlier attempt touching
+// b_i or b_i + 1), and for each segment g of the owned slots the attempts
+// whose pair lies in its cone [sl_g - nlv, sh_g + nlv) by level
+// (ds_swap_seg).  Per-thread scratch in `sc`.
+struct SchedScratch {
+  std::vector<int> b, lvl, last, cnt;
+  std::vector<double> beta;
+};
+static void sched_build(hb_dsampler* d, long long q, int slot, SchedScratch& sc) {
+  const int W = d->W, G = d->nseg, lo = d->lo, nl = d->nl;
+  hb_dsampler::Slot& sl = d->slots[slot];
+  sc.b.resize(W);
+  sc.lvl.resize(W);
+  sc.last.assign((size_t)W + 1, 0);
+  sc.beta.resize(W);
+  uint32_t w[31], c[31];
+  memcpy(w, d->base_w, sizeof w);
+  hblf::poly_xpow(2ull * (unsigned long long)W * (unsigned long long)q, c);
+  hblf::window_jump(w, c);
+  hblf::Stream gen(w);
+  for (int i = 0; i < W; ++i) {  // ptmcmc :791, :810 (the expressions of hbx_swap_draws)
+    sc.b[i] = (int)(((double)gen.rand() / (RAND_MAX)) * ((double)(W - 1)));
+    sc.beta[i] = ((double)gen.rand() / (RAND_MAX));
+  }
+  int nlv = 0;
+  for (int i = 0; i < W; ++i) {
+    const int b = sc.b[i];
+    if (b < 0 || b + 1 >= W) {  // rand() == RAND_MAX: the reference reads index[NCHAINS]; no swap here
+      sc.lvl[i] = -1;
+      continue;
+    }
+    const int l = std::max(sc.last[b], sc.last[b + 1]) + 1;
+    sc.lvl[i] = l;
+    sc.last[b] = sc.last[b + 1] = l;
+    nlv = std::max(nlv, l);
+  }
+  sl.nlv = nlv;
+  if (nlv > kMaxLevels) {
+    sl.overflow = true;
+    return;
+  }
+  // segments whose cone holds the pair (b, b + 1): sl_g - nlv <= b and
+  // b + 1 < sh_g + nlv -- a contiguous range of g
+  auto seg_of = [&](int s) {  // segment owning slot s (clamped to the owned range)
+    if (s < lo) return 0;
+    if (s >= lo + nl) return G - 1;
+    int g = (int)(((long long)(s - lo) * G) / nl);
+    while (g + 1 < G && seg_lo(lo, nl, g + 1, G) <= s) ++g;
+    while (g > 0 && seg_lo(lo, nl, g, G) > s) --g;
+    return g;
+  };
+  auto seg_range = [&](int b, int& g0, int& g1) {
+    g0 = seg_of(b + 1 - nlv);
+    while (g0 < G && seg_lo(lo, nl, g0 + 1, G) + nlv <= b + 1) ++g0;
+    g1 = seg_of(b + nlv);
+    while (g1 >= 0 && seg_lo(lo, nl, g1, G) - nlv > b) --g1;
+  };
+  sc.cnt.assign((size_t)G * nlv + 1, 0);
+  size_t nent = 0;
+  for (int i = 0; i < W; ++i) {
+    if (sc.lvl[i] <= 0) continue;
+    int g0, g1;
+    seg_range(sc.b[i], g0, g1);
+    for (int g = g0; g <= g1; ++g) {
+      sc.cnt[(size_t)g * nlv + sc.lvl[i] - 1]++;
+      ++nent;
+    }
+  }
+  if (sched_bytes((size_t)G, (size_t)nlv, nent) > d->sched_cap) {
+    sl.overflow = true;
+    return;
+  }
+  unsigned char* buf = d->pin[slot];
+  int* soff = reinterpret_cast<int*>(buf);
+  SwapEnt* ent = reinterpret_cast<SwapEnt*>(buf + sched_ent_off((size_t)G, (size_t)nlv));
+  double* betas = reinterpret_cast<double*>(buf + sched_beta_off((size_t)G, (size_t)nlv, nent));
+  int run = 0;
+  for (size_t k = 0; k < (size_t)G * nlv; ++k) {
+    soff[k] = run;
+    run += sc.cnt[k];
+    sc.cnt[k] = soff[k];  // next free entry of (segment, level)
+  }
+  soff[(size_t)G * nlv] = run;
+  for (int i = 0; i < W; ++i) {
+    if (sc.lvl[i] <= 0) continue;
+    int g0, g1;
+    seg_range(sc.b[i], g0, g1);
+    const double lnb = log(sc.beta[i]);
+    for (int g = g0; g <= g1; ++g) {
+      const int e = sc.cnt[(size_t)g * nlv + sc.lvl[i] - 1]++;
+      ent[e].b = sc.b[i];
+      ent[e].pad = 0;
+      ent[e].lnb = lnb;
+      betas[e] = sc.beta[i];
+    }
+  }
+  sl.nent = (int)nent;
+}
+
+// producer thread: claims the next iteration, waits until its ring slot's
+// previous schedule has been consumed (its ds_swap enqueued, then finished on
+// the GPU), builds the schedule and publishes it
+static void sched_worker(hb_dsampler* d) {
+  (void)hipSetDevice(d->device);
+  SchedScratch sc;
+  constexpr int K = hb_dsampler::R_RING;
+  while (true) {
+    long long q;
+    int slot;
+    bool reused;
+    {
+      std::unique_lock<std::mutex> lk(d->smu);
+      d->scv.wait(lk, [&] {
+        if (d->stop) return true;
+        const hb_dsampler::Slot& sl = d->slots[d->q_prod % K];
+        return sl.q < 0 || (sl.q == d->q_prod - K && sl.released);
+      });
+      if (d->stop) return;
+      q = d->q_prod++;
+      slot = (int)(q % K);
+      reused = d->slots[slot].q >= 0;
+      d->slots[slot] = hb_dsampler::Slot{};
+      d->slots[slot].q = q;
+    }
+    if (reused && hipEventSynchronize(d->ev_used[slot]) != hipSuccess) return;  // the GPU is done with it
+    const double t0 = now_s();
+    sched_build(d, q, slot, sc);
+    const double dt = now_s() - t0;
+    {
+      std::lock_guard<std::mutex> lk(d->smu);
+      d->slots[slot].ready = true;
+      d->t_prod += dt;
+    }
+    d->scv.notify_all();
+  }
+}
 
 // owned slots of rank r of R (hb_mcmc_amd/dist.py shard())
 static inline int shard_lo(int W, int r, int R) { return (int)((long long)W * r / R); }
@@ -991,8 +1147,8 @@ static hb_dsampler* ds_create(hb_sampler* s, hb_ctx* ctx, const int* chain_of_sl
   D.nl = d->nl;
   // by chain / ladder: W entries; by slot: the nl owned slots
   if ((e = d->alloc(&D.x, Wz * kNp)) || (e = d->alloc(&D.logL, Wz)) || (e = d->alloc(&D.logP, Wz)) ||
-      (e = d->alloc(&D.logP_ok, Wz)) || (e = d->alloc(&D.idx, Wz)) || (e = d->alloc(&D.order, Nz)) ||
-      (e = d->alloc(&D.eord, Nz)) || (e = d->alloc(&D.ebin, Nz)) ||
+      (e = d->alloc(&D.logP_ok, Wz)) || (e = d->alloc(&D.idx, Wz)) || (e = d->alloc(&D.idx_out, Wz)) || (e = d->alloc(&D.order, Nz)) ||
+
       (e = d->alloc(&D.temp, Wz)) || (e = d->alloc(&D.idum, Nz)) || (e = d->alloc(&D.idum2, Nz)) ||
       (e = d->alloc(&D.iy, Nz)) || (e = d->alloc(&D.iset, Nz)) || (e = d->alloc(&D.gset, Nz)) ||
       (e = d->alloc(&D.cts, Nz)) || (e = d->alloc(&D.iv, Nz * NTAB)) || (e = d->alloc(&D.y, Nz * kNp)) ||
@@ -1004,29 +1160,27 @@ static hb_dsampler* ds_create(hb_sampler* s, hb_ctx* ctx, const int* chain_of_sl
       (e = d->alloc(&d->d_ok, Nz)) || (e = d->alloc(&D.hs, Wz)) || (e = d->alloc(&d->d_params, 1)))
     return fail("hipMalloc", e);
   D.P = d->d_params;
-  if ((e = hipStreamCreateWithFlags(&d->cst, hipStreamNonBlocking)) != hipSuccess) return fail("stream", e);
-  d->sched_bytes = sched_beta_off(Wz) + sizeof(double) * Wz;
+  // eval order by e bins (AccArgs::ecnt) up to kEvalOrdMax owned slots
+  if (Nz <= (size_t)kEvalOrdMax && !d->no_eord) {
+    if ((e = d->alloc(&D.ecnt, (size_t)kOrdBins)) || (e = d->alloc(&D.elist, (size_t)kOrdBins * Nz)))
+      return fail("hipMalloc", e);
+    if ((e = hipMemsetAsync(D.ecnt, 0, sizeof(int) * kOrdBins, d->st))) return fail("hipMemset", e);
+  }
+  // swap segments of <= kSegSlots owned slots; an attempt is listed for at
+  // most min(G, 3 + 2 kMaxLevels / (smallest segment)) segments
+  d->nseg = std::max(1, (d->nl + kSegSlots - 1) / kSegSlots);
+  {
+    const size_t G = (size_t)d->nseg, segmin = std::max<size_t>(1, (size_t)d->nl / G);
+    const size_t per = std::min(G, 3 + 2 * (size_t)kMaxLevels / segmin);
+    d->sched_cap = sched_bytes(G, (size_t)kMaxLevels, Wz * per);
+  }
   for (int r = 0; r < hb_dsampler::R_RING; ++r) {
-    if ((e = d->alloc(&d->d_sched[r], d->sched_bytes))) return fail("hipMalloc", e);
-    if ((e = hipHostMalloc((void**)&d->pin[r], d->sched_bytes, hipHostMallocDefault))) return fail("pinned", e);
-    if ((e = hipEventCreateWithFlags(&d->ev_copy[r], hipEventDisableTiming))) return fail("event", e);
+    if ((e = d->alloc(&d->d_sched[r], d->sched_cap))) return fail("hipMalloc", e);
+    if ((e = hipHostMalloc((void**)&d->pin[r], d->sched_cap, hipHostMallocDefault))) return fail("pinned", e);
     if ((e = hipEventCreateWithFlags(&d->ev_used[r], hipEventDisableTiming))) return fail("event", e);
   }
   if ((e = hipHostMalloc((void**)&d->h_ctr, sizeof(Counters), hipHostMallocDefault))) return fail("pinned", e);
   if ((e = hipHostMalloc((void**)&d->h_ev, sizeof(Event) * kEvCap, hipHostMallocDefault))) return fail("pinned", e);
-  d->b.resize(W);
-  d->beta.resize(W);
-  d->last.resize(W + 1);
-  d->lvl.resize(W);
-  d->cnt.resize(W + 2);
-  // schedule, logL, pair factors and index[] in LDS when they fit (160 KB per CU on gfx950)
-  d->swap_lds = (sizeof(SwapEnt) + 2 * sizeof(double) + sizeof(int)) * Wz;
-  d->lds_swap = d->swap_lds <= 150 * 1024;  // + ~3 KB of static LDS
-  if (d->lds_swap) {
-    e = hipFuncSetAttribute((const void*)ds_swap<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)d->swap_lds);
-    if (e != hipSuccess) return fail("LDS attribute", e);
-  }
   Params& P = d->P;
   P.W = W;
   P.NPAST = d->NPAST;
@@ -1045,6 +1199,11 @@ static hb_dsampler* ds_create(hb_sampler* s, hb_ctx* ctx, const int* chain_of_sl
     delete d;
     return nullptr;
   }
+  // schedule producers: the swap stream as it stands now is iteration 0's start
+  if (hbx_swap_rng_window(s, d->base_w)) return fail("swap stream", hipErrorInvalidValue);
+  const char* nt = getenv("HB_DS_SCHED_THREADS");
+  d->nthreads = nt ? std::max(1, atoi(nt)) : (W <= 8192 ? 2 : 4);
+  for (int i = 0; i < d->nthreads; ++i) d->workers.emplace_back(sched_worker, d);
   return d;
 }
 
@@ -1200,6 +1359,13 @@ extern "C" int hb_dsampler_download(hb_dsampler* d) {
   *v.atrial = c.atrial;
   *v.cold_acc = c.cold_acc;
   *v.nswap = c.nswap;
+  // the host's swap stream: the draws of the iterations run on the device
+  // since the last download (two per attempt, W attempts each)
+  if (d->q_cons > d->q_synced) {
+    if (hbx_swap_rng_skip(d->s, 2ull * (unsigned long long)d->W * (unsigned long long)(d->q_cons - d->q_synced)))
+      return hbx_set_error("hb_dsampler_download: swap stream");
+    d->q_synced = d->q_cons;
+  }
   return ds_drain_events(d);
 }
 
@@ -1269,71 +1435,70 @@ extern "C" long hb_dsampler_exchange_cap(const hb_dsampler* d) {
 
 extern "C" void* hb_dsampler_stream(hb_dsampler* d) { return d ? (void*)d->st : nullptr; }
 
-// first half of an iteration: the swap schedule (host, into the pinned ring),
-// proposals, likelihood + Hastings test of the owned slots; sharded runs
-// also pack the rank's all-gather contribution into send
+extern "C" int hb_dsampler_host_times(const hb_dsampler* d, double* out4) {
+  if (!d || !out4) return hbx_set_error("hb_dsampler_host_times: null");
+  hb_dsampler* m = const_cast<hb_dsampler*>(d);
+  std::lock_guard<std::mutex> lk(m->smu);
+  out4[0] = d->t_prod;
+  out4[1] = d->t_wait;
+  out4[2] = d->t_issue;
+  out4[3] = d->nthreads;
+  return 0;
+}
+
+// first half of an iteration: the iteration's swap schedule (a producer
+// thread built it into the pinned ring), proposals, likelihood + Hastings
+// test of the owned slots; exchanging samplers also pack the rank's
+// all-gather contribution into send
 static long ds_begin(hb_dsampler* d, long iter, double* send, long cap) {
   const int W = d->W;
   const Dev& D = d->D;
   hipStream_t s = d->st;
   if (d->cur_iter >= 0) return hbx_set_error("hb_dsampler: step_begin twice without step_end");
   DS_TRY(hipSetDevice(d->device), "hipSetDevice");
-  // swap schedule of this iteration (draws in the reference's order)
-  hbx_swap_draws(d->s, d->b.data(), d->beta.data());
-  std::fill(d->last.begin(), d->last.end(), 0);
-  int nlv = 0;
-  for (int i = 0; i < W; ++i) {
-    const int b = d->b[i];
-    if (b < 0 || b + 1 >= W) {  // rand() == RAND_MAX: the reference reads index[NCHAINS]; no swap here
-      d->lvl[i] = -1;
-      continue;
-    }
-    const int l = std::max(d->last[b], d->last[b + 1]) + 1;
-    d->lvl[i] = l;
-    d->last[b] = d->last[b + 1] = l;
-    nlv = std::max(nlv, l);
+  const double tw0 = now_s();
+  const long long q = d->q_cons;
+  const int slot = (int)(q % hb_dsampler::R_RING);
+  hb_dsampler::Slot sl;
+  {
+    std::unique_lock<std::mutex> lk(d->smu);
+    d->scv.wait(lk, [&] { return d->slots[slot].q == q && d->slots[slot].ready; });
+    sl = d->slots[slot];
   }
-  const int r = d->ring;
-  d->ring = (d->ring + 1) % hb_dsampler::R_RING;
-  if (d->used[r]) DS_TRY(hipEventSynchronize(d->ev_used[r]), "schedule ring");  // entry r free again
-  SwapEnt* ent = reinterpret_cast<SwapEnt*>(d->pin[r]);
-  int* off = reinterpret_cast<int*>(d->pin[r] + sizeof(SwapEnt) * (size_t)W);
-  double* betas = reinterpret_cast<double*>(d->pin[r] + sched_beta_off(W));
-  std::fill(d->cnt.begin(), d->cnt.begin() + nlv + 2, 0);
-  for (int i = 0; i < W; ++i)
-    if (d->lvl[i] > 0) d->cnt[d->lvl[i]]++;
-  off[0] = 0;
-  for (int l = 1; l <= nlv; ++l) off[l] = off[l - 1] + d->cnt[l];
-  for (int l = 0; l <= nlv; ++l) d->cnt[l] = off[l];  // next free entry of level l+1 at cnt[l]
-  for (int i = 0; i < W; ++i) {
-    const int l = d->lvl[i];
-    if (l <= 0) continue;
-    const int q = d->cnt[l - 1]++;
-    SwapEnt& e = ent[q];
-    e.b = d->b[i];
-    e.pad = 0;
-    e.lnb = log(d->beta[i]);
-    betas[q] = d->beta[i];
-  }
-  const size_t used_bytes = sched_beta_off(W) + sizeof(double) * (size_t)W;  // a multiple of 8
-  if (d->copy_stream) {
-    DS_TRY(hipMemcpyAsync(d->d_sched[r], d->pin[r], used_bytes, hipMemcpyHostToDevice, d->cst), "schedule upload");
-    DS_TRY(hipEventRecord(d->ev_copy[r], d->cst), "schedule ring");
-  }
-
+  d->q_cons = q + 1;
+  const double tw1 = now_s();
+  if (sl.overflow)
+    return hbx_set_error("hb_dsampler: an iteration's swap schedule exceeds its buffer (more than 64 levels)");
+  const size_t used_bytes = sched_bytes((size_t)d->nseg, (size_t)sl.nlv, (size_t)sl.nent);  // a multiple of 8
   const int NPAST = d->NPAST, nl = d->nl;
+  // proposals, and in their epilogue the likelihood's walker records (the
+  // context's workspace, looked up per launch: another caller may have grown it)
+  Dev Dp = D;
+  {
+    void* wc = nullptr;
+    double* tab_pc = nullptr;
+    const int rc = hbx_ctx_prep_args(d->ctx, &wc, &Dp.ma, &tab_pc);
+    if (rc) return rc;
+    Dp.wc = static_cast<double*>(wc);
+    Dp.tab_pc = tab_pc;
+  }
   ds_propose<<<(nl + kPW - 1) / kPW, 64 * kPW, 0, s>>>(
-      D, W, NPAST, (long long)iter, reinterpret_cast<const unsigned long long*>(d->pin[r]),
-      reinterpret_cast<unsigned long long*>(d->d_sched[r]), d->copy_stream ? 0LL : (long long)(used_bytes / 8));
+      Dp, W, NPAST, (long long)iter, reinterpret_cast<const unsigned long long*>(d->pin[slot]),
+      reinterpret_cast<unsigned long long*>(d->d_sched[slot]), (long long)(used_bytes / 8));
   DS_TRY(hipGetLastError(), "ds_propose");
+  static const bool prep_launch = getenv("HB_DS_PREP_LAUNCH") != nullptr;  // experiment knob: records by hb_prep_kernel
+  if (prep_launch) {
+    const int rc = hb_prepare_dev(d->ctx, D.y, nl, (void*)s);
+    if (rc) return rc;
+  }
   // likelihood with the Hastings test fused into its waves' epilogue
   // (hb_accept.hpp); ds_accept only where the plan has no one-wave kernel
   const AccArgs acc{D.idx, D.logL, D.logP, D.logPy, D.temp, D.alpha2, D.jump, D.jtype, D.x, D.y, D.hist,
                     D.DEacc_arr, D.ctr, D.ev, d->P.log_on, NPAST, (long long)iter, d->lo, 0,
-                    (nl <= kEvalOrdMax && !d->no_eord) ? D.eord : nullptr, D.ebin};
+                    D.ecnt, D.elist, nl, 0};
   int rc = hbx_loglik_accept_dev(d->ctx, D.y, nl, D.logLy, &acc, (void*)s);
   if (rc == 1) {
-    rc = hb_loglik_batch_dev(d->ctx, D.y, nl, D.logLy, (void*)s);
+    rc = hb_evaluate_dev(d->ctx, nl, D.logLy, 0, (void*)s);
     if (rc) return rc;
     ds_accept<<<(nl + 63) / 64, kAccThreads, 0, s>>>(D, W, NPAST, (long long)iter);
     DS_TRY(hipGetLastError(), "ds_accept");
@@ -1342,21 +1507,23 @@ static long ds_begin(hb_dsampler* d, long iter, double* send, long cap) {
   }
   long n = 0;
   if (d->xchg) {
-    const int ke = std::min(nlv, d->nlmin);  // edge window (a level moves a chain by one slot)
+    const int ke = std::min(sl.nlv, d->nlmin);  // edge window (a level moves a chain by one slot)
     n = (long)d->m + 2L * ke * kRec;
     if (!send || n > cap) return hbx_set_error("hb_dsampler_step_begin: send buffer missing or too small");
     const long thr = n;
     ds_pack<<<(unsigned)((thr + kPackThreads - 1) / kPackThreads), kPackThreads, 0, s>>>(D, send, d->m, ke);
     DS_TRY(hipGetLastError(), "ds_pack");
   }
-  d->cur_ring = r;
-  d->cur_nlv = nlv;
+  d->cur_slot = slot;
   d->cur_iter = iter;
   d->cur_n = n;
+  d->t_wait += tw1 - tw0;
+  d->t_issue += now_s() - tw1;
   return n;
 }
 
-// second half: import the all-gather (sharded), tempering swaps, bookkeeping
+// second half: import the all-gather (exchanging samplers), tempering swaps,
+// bookkeeping
 static int ds_end(hb_dsampler* d, long iter, const double* recv, long n) {
   const int W = d->W;
   const Dev& D = d->D;
@@ -1364,20 +1531,35 @@ static int ds_end(hb_dsampler* d, long iter, const double* recv, long n) {
   if (d->cur_iter != iter) return hbx_set_error("hb_dsampler_step_end: no step_begin for this iteration");
   if (d->xchg && (!recv || n != d->cur_n))
     return hbx_set_error("hb_dsampler_step_end: gathered buffer missing or of the wrong size");
-  const int r = d->cur_ring, nlv = d->cur_nlv;
+  const double t0 = now_s();
+  const int slot = d->cur_slot;
+  const hb_dsampler::Slot sl = d->slots[slot];  // written by its producer before the ready flag
   d->cur_iter = -1;
   DS_TRY(hipSetDevice(d->device), "hipSetDevice");
-  const SwapEnt* d_ent = reinterpret_cast<const SwapEnt*>(d->d_sched[r]);
-  const int* d_off = reinterpret_cast<const int*>(d->d_sched[r] + sizeof(SwapEnt) * (size_t)W);
-  const Gathered X{d->xchg ? recv : nullptr, (long long)n, d->R, d->rank, d->m, 0};
-  if (d->copy_stream) DS_TRY(hipStreamWaitEvent(s, d->ev_copy[r], 0), "schedule wait");
-  if (d->lds_swap)
-    ds_swap<true><<<1, kSwapThreads, d->swap_lds, s>>>(D, W, d_ent, d_off, nlv, (long long)iter, X);
-  else
-    ds_swap<false><<<1, kSwapThreads, 0, s>>>(D, W, d_ent, d_off, nlv, (long long)iter, X);
-  DS_TRY(hipGetLastError(), "ds_swap");
-  DS_TRY(hipEventRecord(d->ev_used[r], s), "schedule ring");
-  d->used[r] = true;
+  const int G = d->nseg;
+  const unsigned char* base = d->d_sched[slot];
+  const int* d_soff = reinterpret_cast<const int*>(base);
+  const SwapEnt* d_ent = reinterpret_cast<const SwapEnt*>(base + sched_ent_off((size_t)G, (size_t)sl.nlv));
+  const double* d_beta =
+      reinterpret_cast<const double*>(base + sched_beta_off((size_t)G, (size_t)sl.nlv, (size_t)sl.nent));
+  // LDS: the widest cone's (logL, chain) pairs
+  const size_t lds = (sizeof(double) + sizeof(int)) * ((size_t)(d->nl + G - 1) / G + 2 * (size_t)sl.nlv);
+  if (d->xchg) {
+    const Gathered X{recv, (long long)n, d->R, d->rank, d->m, 0};
+    ds_swap_seg<true><<<G, kSegThreads, lds, s>>>(D, W, d_soff, d_ent, d_beta, sl.nlv, G, (long long)iter, X);
+  } else {
+    const Gathered X{nullptr, 0, 1, 0, 0, 0};
+    ds_swap_seg<false><<<G, kSegThreads, lds, s>>>(D, W, d_soff, d_ent, d_beta, sl.nlv, G, (long long)iter, X);
+  }
+  DS_TRY(hipGetLastError(), "ds_swap_seg");
+  std::swap(d->D.idx, d->D.idx_out);  // the next iteration reads what the swaps wrote
+  DS_TRY(hipEventRecord(d->ev_used[slot], s), "schedule ring");
+  {
+    std::lock_guard<std::mutex> lk(d->smu);
+    d->slots[slot].released = true;
+  }
+  d->scv.notify_all();
+  d->t_issue += now_s() - t0;
   if (d->P.log_on && iter > 10000 && iter % 100 == 0) return ds_drain_events(d);
   return 0;
 }

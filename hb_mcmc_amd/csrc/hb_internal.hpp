@@ -96,7 +96,7 @@ hipError_t preload_code_object();
 hipError_t launch_prep(const double* d_params, int nwalk, const MagArgs& ma, hbdev::WalkerConst* d_wc,
                        hipStream_t s, const TargetDesc* tab = nullptr, const int* wt = nullptr,
                        const double* t = nullptr, long n = 0, double2* ph = nullptr, const int* w0 = nullptr,
-                       int ntargets = 0, int* ord = nullptr, const unsigned char* ebin = nullptr);
+                       int ntargets = 0, double* tab_pc = nullptr);
 // catalog mode: walkers list[0..count) of one size class (cadences per lane
 // vpt), each reading its target's slice through tab[wt[walker]]
 hipError_t launch_eval_multi(int vpt, size_t slab_bytes, const double* t, const double2* ph, const double* f,

@@ -1,6 +1,6 @@
 // hb_kernels.hip -- gfx950 kernels for the HB light-curve log-likelihood.
 //
-//   hb_prep_kernel      one lane per walker: WalkerConst (hb_device.hpp)
+//   hb_prep_kernel      WalkerConst (hb_device.hpp) by prep groups (hb_prep.hpp)
 //   hb_eval_kernel<NW>  one workgroup of NW waves per walker:
 //                         1. model flux for every cadence (t streamed from
 //                            HBM/L2, coalesced), kept in LDS (or an HBM slab
@@ -26,6 +26,7 @@
 #include "hb_accept.hpp"
 #include "hb_device.hpp"
 #include "hb_internal.hpp"
+#include "hb_prep.hpp"
 
 using namespace hbdev;
 
@@ -45,9 +46,6 @@ using namespace hbdev;
 #endif
 #ifndef HB_FULLTILE
 #define HB_FULLTILE 1  // full K*64 tiles store without per-cadence bounds tests
-#endif
-#ifndef HB_PREP_ABL
-#define HB_PREP_ABL 0  // experiment builds only: 1 no Gaia flux, 2 no star_coef, 3 no radius law
 #endif
 #ifndef HB_ABLATE_MODEL
 #define HB_ABLATE_MODEL 0
@@ -100,81 +98,17 @@ __device__ unsigned long long hb_wave_clk[8 * 65536];
 namespace hbk {
 
 // ---------------------------------------------------------------------------
-// kernel 1: per-walker constants.  64 walkers per 256-thread block, lane =
-// walker, four waves with wave-uniform roles: wave s (s = star 0/1) runs the
-// star's radius law and then its photometric coefficients; wave 2 + s runs
-// the star's Teff law and beaming factor, then a star-specific tail (wave 2:
-// Gaia term and sin/cos omega; wave 3: eclipse geometry, Roche test and
-// phase-table rotations).  The block is latency-bound (one wave per SIMD), so
-// splitting the independent chains over four waves shortens the critical
-// path; the formulas and their operand order are those of the 2-wave version
-// (bit-identical records).  Results cross waves through LDS; parameters and
-// records move through LDS so HBM accesses coalesce.
+// kernel 1: per-walker constants (hb_prep.hpp), kPrepWalkers walkers per
+// 256-thread workgroup (a prep group: four role waves, lane = walker), so
+// W = 4096 launches 256 workgroups, one per CU.  Parameters and records move
+// through LDS so the HBM accesses coalesce.  The device sampler computes the
+// same records in ds_propose's epilogue instead (no launch per iteration).
 // ---------------------------------------------------------------------------
 #ifndef HB_PREP_W
-#define HB_PREP_W 64
+#define HB_PREP_W 16
 #endif
-constexpr int kPrepWalkers = HB_PREP_W;  // walkers per prep block (4 lanes each)
-constexpr int kPrepThreads = 4 * kPrepWalkers;
-constexpr int kWcDoubles = (int)(sizeof(WalkerConst) / sizeof(double));
-
-// sin/cos of a phase-table angle: the branch-free reduction for |x| < 2^19,
-// ocml otherwise (never for folded light curves)
-__device__ __forceinline__ void sincos_table(double x, double& sv, double& cv) {
-  if (sincos_fast_ok(x)) {
-    sincos_fast(x, &sv, &cv);
-  } else {
-    const SinCos r = sincos_ocml(x);
-    sv = r.s;
-    cv = r.c;
-  }
-}
-
-// Eval order by descending e, written by one extra prep workgroup (device
-// sampler).  The eval launch is one resident round of waves, four per SIMD,
-// so it lasts as long as the SIMD whose walkers cost most; cost follows e
-// (high e leaves the warm Kepler chains for the cold path).  Waves taking the
-// walkers by descending e give every SIMD walkers from the whole e range
-// (sampler states of a 200-iteration run: 53 us in slot order, 47 us sorted).
-// A counting sort over 64 bins of the bytes ds_propose wrote (contiguous: the
-// one workgroup does not gather the scattered parameter rows): LDS counters,
-// one wave scan, one scatter; the order within a bin is immaterial (each
-// wave's result depends on its walker only).
-__device__ void order_by_e(const unsigned char* __restrict__ ebin, int nwalk, int* __restrict__ ord) {
-  using hbds::kOrdBins;
-  __shared__ int cnt[kOrdBins];
-  const int tid = threadIdx.x;
-  constexpr int T = kPrepThreads, U = (hbds::kEvalOrdMax + T - 1) / T;
-  if (tid < kOrdBins) cnt[tid] = 0;
-  int b[U];
-#pragma unroll
-  for (int u = 0; u < U; ++u) {
-    const int j = tid + u * T;
-    b[u] = j < nwalk ? ebin[j] : 0;
-  }
-  __syncthreads();
-#pragma unroll
-  for (int u = 0; u < U; ++u)
-    if (tid + u * T < nwalk) atomicAdd(&cnt[b[u]], 1);
-  __syncthreads();
-  if (tid < kOrdBins) {  // exclusive scan by wave 0 (lane = bin): first position of each bin
-    const int v = cnt[tid];
-    int incl = v;
-#pragma unroll
-    for (int d = 1; d < kOrdBins; d <<= 1) {
-      const int o = __shfl_up(incl, d);
-      if (tid >= d) incl += o;
-    }
-    cnt[tid] = incl - v;
-  }
-  __syncthreads();
-  int q[U];
-#pragma unroll
-  for (int u = 0; u < U; ++u) q[u] = tid + u * T < nwalk ? atomicAdd(&cnt[b[u]], 1) : 0;
-#pragma unroll
-  for (int u = 0; u < U; ++u)
-    if (tid + u * T < nwalk) ord[q[u]] = tid + u * T;
-}
+constexpr int kPrepWalkers = HB_PREP_W;  // walkers per prep workgroup
+constexpr int kPrepThreads = 64 * kPrepRoles;
 
 __global__ __launch_bounds__(kPrepThreads) void hb_prep_kernel(const double* __restrict__ params,
                                                               int nwalk, MagArgs ma,
@@ -184,32 +118,19 @@ __global__ __launch_bounds__(kPrepThreads) void hb_prep_kernel(const double* __r
                                                               const double* __restrict__ tcad, int ncad,
                                                               double2* __restrict__ ph,
                                                               const int* __restrict__ w0, int ntargets,
-                                                              int* __restrict__ ord,
-                                                              const unsigned char* __restrict__ ebin) {
-  __shared__ double sp[kPrepWalkers * kNpars];
-  __shared__ double so[kPrepWalkers * kWcDoubles];
-  const int G = (int)gridDim.x - (ord != nullptr ? 1 : 0);  // walker blocks; the order block is the last
-  if (ord != nullptr && (int)blockIdx.x == G) {           // workgroup-uniform
-    order_by_e(ebin, nwalk, ord);
-    return;
-  }
-  // per-star results: [star][item][walker]; items 0 m, 1 r, 2 tk, 3 ab, 4..15 star-2 terms
-  __shared__ double xs[2][16][kPrepWalkers];
-  __shared__ double gs[3][kPrepWalkers];  // wave 2's Gaia term and sin/cos omega
+                                                              double* __restrict__ tab_pc_out) {
+  __shared__ PrepShared<kPrepWalkers> L;
+  const int G = (int)gridDim.x;
   const int tid = threadIdx.x;
+  const int lane = tid & 63;
   const int base = blockIdx.x * kPrepWalkers;
   const int nb = min(kPrepWalkers, nwalk - base);
-#ifdef HB_PREP_TIMING  // experiment builds only: phase clocks of block 0 / block 32
-  long long pc[8];
-  pc[0] = clock64();
-#define PT(k) pc[k] = clock64()
-#else
-#define PT(k)
-#endif
-  // wave 2's first phase-table operands (single context), in flight with the parameters
+  // wave 2 writes a single context's shared-period phase table in its slack;
+  // its first operands are in flight with the parameters
+  const bool tabwave = ph != nullptr && tab == nullptr && (tid >> 6) == 2;
   double t_first = 0.0, lp0 = 0.0;
-  if (ph != nullptr && tab == nullptr && tid >= 2 * kPrepWalkers && tid < 3 * kPrepWalkers) {
-    const int i0 = blockIdx.x + G * (tid - 2 * kPrepWalkers);
+  if (tabwave) {
+    const int i0 = blockIdx.x + G * lane;
     if (i0 < ncad) t_first = tcad[i0];
     lp0 = params[2];
   }
@@ -224,212 +145,32 @@ __global__ __launch_bounds__(kPrepThreads) void hb_prep_kernel(const double* __r
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int i = tid + u * kPrepThreads;
-      if (i < nb * kNpars) sp[i] = v[u];
+      if (i < nb * kNpars) L.sp[i] = v[u];
     }
   }
   __syncthreads();
-  PT(1);
-#if HB_PREP_ABL == 4  // experiment builds only: data movement, no math
-  {
-    double* dst = reinterpret_cast<double*>(out) + (size_t)base * kWcDoubles;
-    for (int i = tid; i < nb * kWcDoubles; i += kPrepThreads) dst[i] = sp[i % (nb * kNpars)];
-    return;
-  }
-#endif
-  const int j = tid & (kPrepWalkers - 1);
-  const int wv = tid / kPrepWalkers;  // wave-uniform
-  const int star = wv & 1;
-  const bool chainR = wv < 2;         // radius law + coefficients; else Teff law + tail
-  const bool live = j < nb;
-  const double* p = &sp[(live ? j : 0) * kNpars];
-
-  // ---- this wave's half of the star (calc_radii_and_Teffs + get_alpha_beam) ----
-  const double m = exp10(p[star]);
-  if (chainR) {
-#if HB_PREP_ABL == 3
-    const double r = m + p[7 + star];
-#else
-    const double r = exp10(logradius_of_mass(m) + p[7 + star] * radius_spread_of_logmass(p[star]));
-#endif
-    xs[star][0][j] = m;
-    xs[star][1][j] = r;
-  } else {
-    const double lt = logteff_of_mass(m) + p[17 + star] * teff_spread();
-    xs[star][2][j] = exp10(lt);
-    xs[star][3][j] = beam_coeff(lt) * exp(p[15 + star]);
-  }
-  const double pd = exp10(p[2]);
-  const double e = p[3];
-  PT(2);
-  __syncthreads();
-  PT(3);
-  const int o = star ^ 1;
-  const double r = xs[star][1][j], tk = xs[star][2][j], ab = xs[star][3][j];
-  const double mo = xs[o][0][j], ro = xs[o][1][j], tko = xs[o][2][j];
-  const double lum = sq(r) * sq(sq(tk));
-  const double lumo = sq(ro) * sq(sq(tko));
-  // the same sum in every wave: star-1 luminosity first
-  const double lsum = star ? (lumo + lum) : (lum + lumo);
-  const double m1 = star ? mo : m, m2 = star ? m : mo;
-  const double r1 = star ? ro : r, r2 = star ? r : ro;
-  const double t1 = star ? tko : tk, t2 = star ? tk : tko;
-  double* w = &so[(live ? j : 0) * kWcDoubles];
-  WalkerConst* wc = reinterpret_cast<WalkerConst*>(w);
-  double terms[12];
-  double si = 0.0, ci = 0.0;
-  double aR = 0.0, sq1me2 = 0.0, inv1me2 = 0.0, mA = 0.0;  // wave 0's orbit fields, off the last phase
-  if (chainR) {
-    sincos(p[4], &si, &ci);
-    if (star == 0) {
-      const double mtot_cgs = m1 * kMsun + m2 * kMsun;
-      const double Pc = pd * kDay;
-      aR = cbrt(kG * mtot_cgs * (Pc * Pc) / (kTwoPi * kTwoPi)) / kRsun;
-      sq1me2 = sqrt(1.0 - e * e);
-      inv1me2 = 1.0 / (1.0 - e * e);
-      mA = kTwoPi / Pc;
+  // the table period: walker 0's (single context) or the first walker's of
+  // the walker's target in this batch (catalog)
+  auto tab_pc = [&](int j) -> double {
+    if (ph == nullptr) return __builtin_nan("");
+    return exp10(params[(tab ? (size_t)w0[wt[base + j]] * kNpars : 0) + 2]) * kDay;
+  };
+  // ph[i] = (sin, cos)(t_i DAY 2pi/Pc0) for the period of walker 0, entries
+  // dealt round-robin over the workgroups' wave-2 lanes
+  auto slack = [&]() {
+    if (!tabwave) return;
+    const double Pc0 = exp10(lp0) * kDay;
+    const double mA0 = kTwoPi / Pc0;
+    if (blockIdx.x == 0 && lane == 0 && tab_pc_out != nullptr) *tab_pc_out = Pc0;
+    double ti = t_first;
+    for (int i = blockIdx.x + G * lane; i < ncad; i += G * 64) {
+      double sv, cv;
+      sincos_table((ti * kDay) * mA0, sv, cv);
+      ph[i] = make_double2(sv, cv);
+      if (i + G * 64 < ncad) ti = tcad[i + G * 64];
     }
-    const double nself = lum / lsum;
-#if HB_PREP_ABL == 2
-    StarCoef c;
-    c.kb = pd * m; c.am1 = mo * e; c.am2 = si * r; c.c21 = ro * ab; c.am3 = p[9 + 2 * star]; c.c22 = p[10 + 2 * star];
-    c.c4 = p[13 + star]; c.s1 = pd; c.s3 = m; c.kref = r;
-#else
-    const StarCoef c = star_coef(pd, m, mo, e, si, r, ro, p[9 + 2 * star], p[10 + 2 * star], p[13 + star], ab);
-#endif
-    // star 2 sees u + pi: odd harmonics flip sign
-    const double sg = star ? -1.0 : 1.0;
-    terms[0] = nself * c.am1;
-    terms[1] = nself * c.kb * sg;
-    terms[2] = nself * c.kref;
-    terms[3] = sg * nself * c.kref;
-    terms[4] = nself * c.am2;
-    terms[5] = nself * c.c21;
-    terms[6] = sg * nself * c.s1;
-    terms[7] = sg * nself * c.s3;
-    terms[8] = nself * c.am3;
-    terms[9] = nself * c.c22;
-    terms[10] = nself * c.c4;
-    terms[11] = nself;
-    if (star == 1) {
-#pragma unroll
-      for (int q = 0; q < 12; ++q) xs[1][4 + q][j] = terms[q];
-    }
-  } else if (star == 1) {
-    if (live) {
-      const double mtot_cgs = m1 * kMsun + m2 * kMsun;
-      const double Pc = pd * kDay;
-      const double a_cgs = cbrt(kG * mtot_cgs * (Pc * Pc) / (kTwoPi * kTwoPi));
-      // eclipse geometry
-      wc->r1 = r1;
-      wc->r2 = r2;
-      const double lum1 = star ? lumo : lum, lum2 = star ? lum : lumo;
-      const double n1 = lum1 / lsum, n2 = lum2 / lsum;
-      wc->ecl1 = n1 / (kPi * (r1 * r1));
-      wc->ecl2 = n2 / (kPi * (r2 * r2));
-      wc->rbig = r2 > r1 ? r2 : r1;
-      wc->rsml = r2 > r1 ? r1 : r2;
-      wc->dcrit = sqrt(wc->rbig * wc->rbig - wc->rsml * wc->rsml);
-      wc->rsum = wc->rbig + wc->rsml;
-      wc->rsum2 = wc->rsum * wc->rsum;
-      // Roche overflow (RocheOverflow :953-974)
-      const double q12 = m1 / m2;
-      const double peri = a_cgs * (1.0 - e);
-      const double f1 = (r1 * kRsun) / peri;
-      const double f2 = (r2 * kRsun) / peri;
-      wc->roche = ((lobe_fraction(q12) < f1) || (lobe_fraction(1.0 / q12) < f2)) ? 1.0 : 0.0;
-      // phase-table rotations (WalkerConst::tab); same Pc and mA as wave 0's orbit fields
-      double Pc0 = 0.0;
-      if (ph) Pc0 = exp10(params[(tab ? (size_t)w0[wt[base + j]] * kNpars : 0) + 2]) * kDay;
-      const bool use_tab = (ph != nullptr) && (Pc == Pc0);
-      wc->tab = use_tab ? 1.0 : 0.0;
-      double sv = 0.0, cv = 1.0;
-      if (use_tab) sincos_table((p[6] * kDay) * (kTwoPi / Pc), sv, cv);
-      wc->spsi = sv;
-      wc->cpsi = cv;
-      sincos_table(0.85 * e, sv, cv);
-      wc->sdel = sv;
-      wc->cdel = cv;
-      wc->pad0 = 0.0;
-    }
-  } else {
-    // Gaia G term (loglikelihood :834-848)
-    double dist = ma.mag[0], gobs = ma.mag[1], gerr = ma.magerr[0];
-    if (tab != nullptr && live) {  // catalog mode: this walker's target
-      const TargetDesc& td = tab[wt[base + j]];
-      dist = td.dist;
-      gobs = td.gmag;
-      gerr = td.gerr;
-    }
-#if HB_PREP_ABL == 1
-    const double g = r1 + r2 + t1 + t2 + dist + p[19];
-#else
-    const double g = ab_mag(band_flux(673.0, r1 * kRsun, r2 * kRsun, t1, t2, dist, p[19]));
-#endif
-    double sw_, cw_;
-    sincos(p[5], &sw_, &cw_);
-    gs[0][j] = (g - gobs) / gerr;
-    gs[1][j] = sw_;
-    gs[2][j] = cw_;
-    // Shared-period phase table (WalkerConst::tab) of a single context, in
-    // this wave's slack: ph[i] = (sin, cos)(t_i DAY 2pi/Pc0) for the period of
-    // walker 0, entries dealt round-robin over the blocks (t_i and P0 were
-    // loaded at kernel start)
-    if (ph != nullptr && tab == nullptr) {
-      const double mA0 = kTwoPi / (exp10(lp0) * kDay);
-      double ti = t_first;
-      for (int i = blockIdx.x + G * j; i < ncad; i += G * kPrepWalkers) {
-        double sv, cv;
-        sincos_table((ti * kDay) * mA0, sv, cv);
-        ph[i] = make_double2(sv, cv);
-        if (i + G * kPrepWalkers < ncad) ti = tcad[i + G * kPrepWalkers];
-      }
-    }
-  }
-  PT(4);
-  __syncthreads();  // star-2 terms and the Gaia term are in LDS
-  PT(5);
-  if (wv == 0 && live) {
-    double tt[12];
-#pragma unroll
-    for (int q = 0; q < 12; ++q) tt[q] = terms[q] + xs[1][4 + q][j];  // star-1 term first
-    const double gr = gs[0][j];
-    // orbit
-    wc->Pc = pd * kDay;
-    wc->T0c = p[6] * kDay;
-    wc->e = e;
-    wc->e085 = 0.85 * e;
-    wc->sq1me2 = sq1me2;
-    wc->inv1me2 = inv1me2;
-    wc->sw = gs[1][j];
-    wc->cw = gs[2][j];
-    wc->ci = ci;
-    wc->si = si;
-    wc->ci2 = ci * ci;
-    wc->swq = gs[1][j] * sq1me2;
-    wc->cwq = gs[2][j] * sq1me2;
-    wc->aR = aR;
-    wc->aR2 = aR * aR;
-    wc->mA = mA;
-    wc->mB = -wc->T0c;
-    // polynomial coefficients
-    const double s2 = si * si;
-    wc->kconst = tt[11] + tt[0];
-    wc->kb = tt[1];
-    wc->kr0 = tt[2] * (0.64 + 0.18 * s2);
-    wc->kr2 = -tt[2] * (0.18 * s2);
-    wc->krs = -tt[3] * si;
-    wc->kam2 = tt[4];
-    wc->kc21 = tt[5];
-    wc->ks1 = tt[6];
-    wc->ks3 = tt[7];
-    wc->kam3 = tt[8];
-    wc->kc22 = tt[9];
-    wc->kc4 = tt[10];
-    wc->blend = p[19];
-    wc->tune = p[20];
-    wc->chi2_extra = gr * gr;
-  }
-  __syncthreads();
+  };
+  prep_records<kPrepWalkers>(L, nb, ma, tab, wt, base, tab_pc, slack);
   {
     double* dst = reinterpret_cast<double*>(out) + (size_t)base * kWcDoubles;
     constexpr int U = (kPrepWalkers * kWcDoubles + kPrepThreads - 1) / kPrepThreads;
@@ -437,7 +178,7 @@ __global__ __launch_bounds__(kPrepThreads) void hb_prep_kernel(const double* __r
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int i = tid + u * kPrepThreads;
-      v[u] = i < nb * kWcDoubles ? so[i] : 0.0;
+      v[u] = i < nb * kWcDoubles ? L.so[i] : 0.0;
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -445,33 +186,23 @@ __global__ __launch_bounds__(kPrepThreads) void hb_prep_kernel(const double* __r
       if (i < nb * kWcDoubles) dst[i] = v[u];
     }
   }
-  PT(6);
   // Catalog phase table (WalkerConst::tab), written after the walker records
   // so its latency overlaps their stores: per target k, for the period of its
   // first walker w0[k] in this batch (-1: no walkers), ph[i] = (sin, cos)(t_i
   // DAY 2pi/Pc0) over its slice of the concatenated arrays.  (A single
   // context's table is written by wave 2 above.)
   if (ph && tab != nullptr) {
-    {
-      for (int k = blockIdx.x; k < ntargets; k += G) {
-        if (w0[k] < 0) continue;
-        const double mA0 = kTwoPi / (exp10(params[(size_t)w0[k] * kNpars + 2]) * kDay);
-        const long off = tab[k].off;
-        for (int i = tid; i < (int)tab[k].n; i += blockDim.x) {
-          double sv, cv;
-          sincos_table((tcad[off + i] * kDay) * mA0, sv, cv);
-          ph[off + i] = make_double2(sv, cv);
-        }
+    for (int k = blockIdx.x; k < ntargets; k += G) {
+      if (w0[k] < 0) continue;
+      const double mA0 = kTwoPi / (exp10(params[(size_t)w0[k] * kNpars + 2]) * kDay);
+      const long off = tab[k].off;
+      for (int i = tid; i < (int)tab[k].n; i += blockDim.x) {
+        double sv, cv;
+        sincos_table((tcad[off + i] * kDay) * mA0, sv, cv);
+        ph[off + i] = make_double2(sv, cv);
       }
     }
   }
-#ifdef HB_PREP_TIMING
-  PT(7);
-  if ((blockIdx.x == 0 || blockIdx.x == 32) && (tid == 0 || tid == kPrepWalkers))
-    printf("prep blk %d star %d: load %lld chain %lld sync %lld coef %lld sync2 %lld store %lld table %lld total %lld\n",
-           blockIdx.x, tid / kPrepWalkers, pc[1] - pc[0], pc[2] - pc[1], pc[3] - pc[2], pc[4] - pc[3], pc[5] - pc[4],
-           pc[6] - pc[5], pc[7] - pc[6], pc[7] - pc[0]);
-#endif
 }
 
 // ---------------------------------------------------------------------------
@@ -1685,7 +1416,7 @@ __global__ __launch_bounds__(64 * WPB) HB_WPE_ATTR void hb_eval_wave_kernel(
   const bool valid = WPB == 1 || slot < count;
   unsigned char* smem = smem_all + (size_t)wib * (size_t)lds_per;
   int wv = slot;
-  if (ACC && hst.ord != nullptr && valid) wv = hst.ord[slot];  // device sampler: slots by descending e (ds_propose)
+  if (ACC && hst.ecnt != nullptr && valid) wv = hbds::eval_slot_by_e(hst, slot, lane);  // device sampler
   if (MULTI && valid) {
     wv = list[slot];
     const TargetDesc& td = tab[wt[wv]];
@@ -2263,13 +1994,12 @@ __global__ __launch_bounds__(1024) void hb_sort_step_kernel(uint64_t* __restrict
 // ---------------------------------------------------------------------------
 hipError_t launch_prep(const double* d_params, int nwalk, const MagArgs& ma, WalkerConst* d_wc,
                        hipStream_t s, const TargetDesc* tab, const int* wt, const double* t, long n,
-                       double2* ph, const int* w0, int ntargets, int* ord, const unsigned char* ebin) {
+                       double2* ph, const int* w0, int ntargets, double* tab_pc) {
   if (nwalk <= 0) return hipSuccess;
   if (t == nullptr || (tab != nullptr && w0 == nullptr) || !HB_PHASE_TAB) ph = nullptr;
-  if (nwalk > hbds::kEvalOrdMax || ebin == nullptr) ord = nullptr;
   const int nb = (nwalk + kPrepWalkers - 1) / kPrepWalkers;
-  hipLaunchKernelGGL(hb_prep_kernel, dim3(nb + (ord != nullptr ? 1 : 0)), dim3(kPrepThreads), 0, s,
-                     d_params, nwalk, ma, d_wc, tab, wt, t, (int)n, ph, w0, ntargets, ord, ebin);
+  hipLaunchKernelGGL(hb_prep_kernel, dim3(nb), dim3(kPrepThreads), 0, s, d_params, nwalk, ma, d_wc, tab, wt, t,
+                     (int)n, ph, w0, ntargets, tab_pc);
   return hipGetLastError();
 }
 

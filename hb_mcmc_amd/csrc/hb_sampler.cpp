@@ -31,6 +31,7 @@
 
 #include "../../include/hb_sampler.h"
 #include "../../include/hbmi.h"
+#include "hb_lagfib.hpp"
 #include "hb_sampler_view.hpp"
 #include "hb_walls.hpp"
 
@@ -190,6 +191,21 @@ class GlibcRand {
     for (int i = 0; i < 310; ++i) next();
   }
   int rand() { return (int)(next() >> 1); }
+  // the last 31 outputs r[k-31 .. k-1] (the generator's whole state)
+  void window(uint32_t* w) const {
+    for (int i = 0; i < 31; ++i) w[i] = r_[(k_ - 31 + i) % 34];
+  }
+  // skip n outputs (hb_lagfib.hpp jump-ahead; the device sampler's schedule
+  // producers consume the stream from a copy)
+  void skip(unsigned long long n) {
+    if (n == 0) return;
+    uint32_t w[31], c[31];
+    window(w);
+    hblf::poly_xpow(n, c);
+    hblf::window_jump(w, c);
+    k_ += (long)n;
+    for (int i = 0; i < 31; ++i) r_[(k_ - 31 + i) % 34] = w[i];
+  }
 
  private:
   uint32_t next() {  // ring of 34: r[k-31] = r[(k+3) % 34], r[k-3] = r[(k+31) % 34]
@@ -350,6 +366,14 @@ extern "C" double hb_ran2_parallel(long* idum, void* st) { return ran2p(idum, (R
 extern "C" double hb_gasdev2_parallel(long* idum, void* st) { return gasdevp(idum, (RNG_Vars*)st); }
 extern "C" int hb_rand_stream(unsigned seed, int n, int* out) {
   GlibcRand g(seed);
+  for (int i = 0; i < n; ++i) out[i] = g.rand();
+  return 0;
+}
+
+// the same stream after jumping `skip` draws ahead (hb_lagfib.hpp)
+extern "C" int hb_rand_stream_jump(unsigned seed, unsigned long long skip, int n, int* out) {
+  GlibcRand g(seed);
+  g.skip(skip);
   for (int i = 0; i < n; ++i) out[i] = g.rand();
   return 0;
 }
@@ -788,6 +812,18 @@ extern "C" int hbx_sampler_view(hb_sampler* s, HbSamplerView* v) {
   v->cold_acc = &s->cold_acc;
   v->nswap = &s->nswap;
   v->log = s->log;
+  return 0;
+}
+
+// the swap stream's state (hb_lagfib.hpp window) and a jump of n draws
+extern "C" int hbx_swap_rng_window(const hb_sampler* s, uint32_t* w31) {
+  if (!s || !w31) return -1;
+  s->rng.window(w31);
+  return 0;
+}
+extern "C" int hbx_swap_rng_skip(hb_sampler* s, unsigned long long n) {
+  if (!s) return -1;
+  s->rng.skip(n);
   return 0;
 }
 

@@ -3,6 +3,7 @@
 // plain pointers into a hb_sampler's state, so a device run can start from a
 // host sampler and hand the exact state back.  Not part of the public ABI.
 #pragma once
+#include <stdint.h>
 #include "../../include/hb_sampler.h"
 #include "../../include/hbmi.h"
 
@@ -41,6 +42,10 @@ int hbx_sampler_view(hb_sampler* s, HbSamplerView* v);
 // reference's ptmcmc consumes them (mcmc_wrapper2.c:791, :810): per attempt
 // i, b[i] = (int)(rand()/RAND_MAX * (W-1)) and beta[i] = rand()/RAND_MAX
 int hbx_swap_draws(hb_sampler* s, int* b, double* beta);
+// the swap stream's state as the window of its last 31 outputs
+// (hb_lagfib.hpp), and a jump-ahead of n draws
+int hbx_swap_rng_window(const hb_sampler* s, uint32_t* w31);
+int hbx_swap_rng_skip(hb_sampler* s, unsigned long long n);
 void hbx_log_big_jump(hb_writer* w, long iter, int chain_id, double H, double alpha, double tmp, double lx,
                       double ly, double px, double py, const double* xo, const double* xn, int jump_type);
 }

@@ -274,9 +274,10 @@ def run_sharded_device(t, flux, sigma, niter, run_id, log10_period, run=0, nchai
             writer.light_curve(t, flux, np.asarray(model(xmap), dtype=np.float64))
             writer.pars(True, x_all[0])
         st = S.stats()
-        cold_acc = comm.allreduce_sum([st["cold_acc"]])[0]
+        # a swap counts on the rank owning its lower slot (ds_swap_cone)
+        cold_acc, nswap = comm.allreduce_sum([st["cold_acc"], st["nswap"]])
         return {"xmap": xmap if r == 0 else None, "logLmap": logLmap if r == 0 else None,
-                "accepted": int(cold_acc), "swaps": st["nswap"], "seconds_total": seconds,
+                "accepted": int(cold_acc), "swaps": int(nswap), "seconds_total": seconds,
                 "loglik_evals": W * (int(niter) + 1), "slots": (lo, hi),
                 "exchanged_doubles_per_iter": D.exchanged_doubles / max(1, int(niter))}
     finally:

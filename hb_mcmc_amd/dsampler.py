@@ -72,6 +72,13 @@ class DeviceSampler:
     def download(self):
         self._check(self.lib.hb_dsampler_download(self._h), "hb_dsampler_download")
 
+    def host_times(self):
+        """Host seconds since creation: schedule building (all producer
+        threads), waits for a schedule, kernel issue; and the thread count."""
+        out = np.zeros(4)
+        self._check(self.lib.hb_dsampler_host_times(self._h, _pd(out)), "hb_dsampler_host_times")
+        return {"sched_build": out[0], "sched_wait": out[1], "issue": out[2], "threads": int(out[3])}
+
 
 def run_mcmc_device(t, flux, sigma, niter, run_id, log10_period, run=0, nchains=50, npast=500, ladder=0,
                     verbose=False, out_root=None, mag_data=None, magerr=None, device=0):
@@ -96,8 +103,9 @@ class ShardedDeviceSampler:
     this rank's GPU proposes, evaluates and tests the slots [W r/R, W (r+1)/R)
     of the ladder; per iteration ONE all-gather carries every rank's logL by
     slot and the records of the chains near its shard's edges, then every rank
-    replays the same tempering swaps on its copy of index[] (SURVEY.md 8(e),
-    mcmc_wrapper2.c:554-563).  The collective runs device to device on the
+    replays the tempering swaps inside its cone [lo - nlv, hi + nlv) (nlv = the
+    iteration's dependency levels: no chain moves farther) on the cone's
+    slice of index[] (mcmc_wrapper2.c:554-563).  The collective runs device to device on the
     sampler's own HIP stream under RCCL (backend "nccl"); under gloo (ranks
     sharing a GPU, rehearsal) it is staged through host memory.
 
@@ -228,3 +236,10 @@ class ShardedDeviceSampler:
 
     def download(self):
         self._check(self.lib.hb_dsampler_download(self._h), "hb_dsampler_download")
+
+    def host_times(self):
+        """Host seconds since creation: schedule building (all producer
+        threads), waits for a schedule, kernel issue; and the thread count."""
+        out = np.zeros(4)
+        self._check(self.lib.hb_dsampler_host_times(self._h, _pd(out)), "hb_dsampler_host_times")
+        return {"sched_build": out[0], "sched_wait": out[1], "issue": out[2], "threads": int(out[3])}

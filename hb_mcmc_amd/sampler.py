@@ -72,6 +72,8 @@ def _declare(lib):
             ("hb_dsampler_step_end", C.c_int, [vp, C.c_long, vp, C.c_long]),
             ("hb_dsampler_exchange_cap", C.c_long, [vp]),
             ("hb_dsampler_stream", vp, [vp]),
+            ("hb_dsampler_host_times", C.c_int, [vp, pd]),
+            ("hb_rand_stream_jump", C.c_int, [C.c_uint, C.c_ulonglong, C.c_int, C.POINTER(C.c_int)]),
             ("hb_mcmc_run_device", C.c_int, [C.POINTER(MCMCConfig), vp, pd, pd, C.c_long, C.POINTER(MCMCResult)]),
             ("hb_glibc_eval", C.c_int, [C.c_int, pd, pd, C.c_long, pd]),
             ("hb_writer_open", vp, [C.c_char_p, C.c_char_p, C.c_int, C.c_int]),

@@ -135,10 +135,12 @@ int hb_dsampler_download(hb_dsampler *d);
  *       sampler's stream (hb_dsampler_stream) or ordered after it
  *   hb_dsampler_step_end(d, it, recv, n)
  *       imports the other ranks' logL and records, replays the iteration's
- *       tempering swaps (identical on every rank) and the bookkeeping.
+ *       tempering swaps inside the rank's cone [lo - nlv, hi + nlv) (nlv =
+ *       the iteration's dependency levels) and the bookkeeping.
  * Gather/download/init_logl act on the owned slots; the MAP tracker
  * (xmap, logLmap) is meaningful on the rank owning slot 0; counters are the
- * owned slots' (sum acc/DEacc/DEtrial/cold_acc over ranks). */
+ * owned slots' (sum acc/DEacc/DEtrial/cold_acc/nswap over ranks; a swap
+ * counts on the rank owning its lower slot b). */
 hb_dsampler *hb_dsampler_create_shard(hb_sampler *s, struct hb_ctx *ctx, const int *chain_of_slot, int nranks,
                                       int rank);
 long hb_dsampler_step_begin(hb_dsampler *d, long iter, double *send, long cap);
@@ -147,6 +149,10 @@ int hb_dsampler_step_end(hb_dsampler *d, long iter, const double *recv, long n);
 long hb_dsampler_exchange_cap(const hb_dsampler *d);
 /* the hipStream_t every kernel of the sampler runs on */
 void *hb_dsampler_stream(hb_dsampler *d);
+/* host-side time [s] since creation: out[0] building swap schedules (summed
+ * over the producer threads), out[1] step_begin waiting for a schedule,
+ * out[2] enqueueing kernels; out[3] = producer thread count */
+int hb_dsampler_host_times(const hb_dsampler *d, double *out4);
 
 /* hb_mcmc_run with the device-resident loop; the light curve and magnitude
  * data come from ctx (t, flux: host copies for the .out file) */
@@ -160,6 +166,9 @@ double hb_ran2_parallel(long *idum, void *rng_state /* struct RNG_Vars */);
 double hb_gasdev2_parallel(long *idum, void *rng_state);
 /* n draws of glibc's rand() after srand(seed), from the sampler's private copy */
 int hb_rand_stream(unsigned seed, int n, int *out);
+/* the same stream after `skip` draws, by jump-ahead (the device sampler draws
+ * iteration q's swap schedule 2*W*q draws past its start) */
+int hb_rand_stream_jump(unsigned seed, unsigned long long skip, int n, int *out);
 
 #ifdef __cplusplus
 }

@@ -55,7 +55,7 @@ def main():
             seeds = D._gather_rows(arrs["seeds"].astype(np.float64), D.counts)
             hist = D._gather_rows(arrs["history"].reshape(S.nl, -1), D.counts)
             st = S.stats()
-            sums = np.array([st[k] for k in ("acc", "DEacc", "DEtrial", "cold_acc")], dtype=np.float64)
+            sums = np.array([st[k] for k in ("acc", "DEacc", "DEtrial", "cold_acc", "nswap")], dtype=np.float64)
             tot = torch.from_numpy(sums)
             if backend == "nccl":
                 tot = tot.cuda()
@@ -63,7 +63,7 @@ def main():
             exch = D.exchanged_doubles
         if r == 0:
             np.savez(out, x=x, logl=ll, cid=cid_all, xmap=xmap, logLmap=lmap, seeds=seeds, hist=hist,
-                     sums=tot.cpu().numpy(), atrial=st["atrial"], nswap=st["nswap"], exchanged=exch)
+                     sums=tot.cpu().numpy(), atrial=st["atrial"], exchanged=exch)
         S.close()
         L.close()
     finally:

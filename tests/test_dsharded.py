@@ -63,7 +63,7 @@ def test_sharded_symbols_exported():
 
     lib = sampler._declare(_lib.lib())
     for name in ("hb_dsampler_create_shard", "hb_dsampler_step_begin", "hb_dsampler_step_end",
-                 "hb_dsampler_exchange_cap", "hb_dsampler_stream"):
+                 "hb_dsampler_exchange_cap", "hb_dsampler_stream", "hb_dsampler_host_times"):
         assert hasattr(lib, name)
 
 
@@ -123,8 +123,8 @@ def _compare(a, b):
     assert np.array_equal(a["hist"], b["hist"]), "history"
     assert np.array_equal(a["xmap"], b["xmap"]) and float(a["logLmap"]) == b["logLmap"], "MAP"
     st = b["st"]
-    assert list(a["sums"].astype(np.int64)) == [st["acc"], st["DEacc"], st["DEtrial"], st["cold_acc"]]
-    assert int(a["atrial"]) == st["atrial"] and int(a["nswap"]) == st["nswap"]
+    assert list(a["sums"].astype(np.int64)) == [st["acc"], st["DEacc"], st["DEtrial"], st["cold_acc"], st["nswap"]]
+    assert int(a["atrial"]) == st["atrial"]
     assert st["nswap"] > 0
 
 

@@ -69,6 +69,24 @@ def test_private_rand_is_glibc_rand():
         assert list(got) == want, seed
 
 
+@pytest.mark.parametrize("skip", [0, 1, 30, 31, 34, 1000, 2 * 4096 * 7 + 3, 10**6])
+def test_rand_jump_ahead_equals_sequential(skip):
+    """hb_lagfib.hpp: jumping the glibc stream `skip` draws ahead (x^J mod the
+    trinomial) gives the same draws as drawing them one by one -- the swap
+    schedule of iteration q is built from the stream 2 W q draws on."""
+    import ctypes as C
+
+    from hb_mcmc_amd import _lib, sampler
+
+    lib = sampler._declare(_lib.lib())
+    for seed in (1, 1200, 2**31 + 5):
+        seq = (C.c_int * (skip + 500))()
+        lib.hb_rand_stream(seed, skip + 500, seq)
+        got = (C.c_int * 500)()
+        assert lib.hb_rand_stream_jump(seed, skip, 500, got) == 0
+        assert list(got) == list(seq)[skip:], (seed, skip)
+
+
 @pytest.mark.slow
 def test_sampler_bookkeeping_bit_exact_with_oracle_likelihood(oracle, tmp_path):
     from hb_mcmc_amd.sampler import run_mcmc
