@@ -38,11 +38,34 @@ struct Event {  // LogSuspiciousJumps (:520-528) arguments
 // j - lo), arrays "by chain" and idx/temp keep all W entries.
 constexpr int kEvalOrdMax = 8192;  // walkers the eval launch takes by e (AccArgs::ecnt)
 constexpr int kOrdBins = 64;       // one per lane (eval_slot_by_e)
+#ifndef HB_EBIN_STRIDE
+#define HB_EBIN_STRIDE 32  // ints between two bins' counters: one 128-B line each (1: packed, measured 3.6 us slower per iteration)
+#endif
+constexpr int kEbinStride = HB_EBIN_STRIDE;
 // e bin of a proposal, descending e -> ascending bin (NaN -> last)
 __device__ __forceinline__ int e_bin_desc(double e) {
   const double q = e * kOrdBins;
   const int b = q >= 0.0 ? (q < (double)kOrdBins ? (int)q : kOrdBins - 1) : 0;
   return kOrdBins - 1 - b;
+}
+
+// one tempering attempt of the level schedule: pair (b, b+1) and ln(beta) of
+// its acceptance draw (beta itself is kept in a global-only array beside it)
+struct SwapEnt {
+  int b;
+  int pad;
+  double lnb;
+};
+// first slot of segment g of G over the owned slots [lo, lo + nl)
+__host__ __device__ inline int seg_lo(int lo, int nl, int g, int G) { return lo + (int)((long long)nl * g / G); }
+// segment holding slot x of [0, nl) (x clamped into the range)
+__host__ __device__ inline int seg_of(int x, int nl, int G) {
+  if (x < 0) x = 0;
+  if (x > nl - 1) x = nl - 1;
+  int g = (int)(((long long)x * G) / nl);
+  while (g + 1 < G && seg_lo(0, nl, g + 1, G) <= x) ++g;
+  while (g > 0 && seg_lo(0, nl, g, G) > x) --g;
+  return g;
 }
 
 struct AccArgs {
@@ -81,7 +104,7 @@ struct AccArgs {
 // The order within a bin is immaterial: a wave's result depends on its
 // walker only.  One load and a wave scan over the 64 bin counts.
 __device__ __forceinline__ int eval_slot_by_e(const AccArgs& A, int s, int lane) {
-  const int c = A.ecnt[lane];
+  const int c = A.ecnt[lane * kEbinStride];
   int incl = c;
 #pragma unroll
   for (int d = 1; d < kOrdBins; d <<= 1) {
@@ -102,7 +125,8 @@ struct AccPre {
   int jg, chain;
   double lx, temp, dlp, alpha, xo, yn;
 };
-__device__ inline AccPre accept_prefetch(const AccArgs& A, int j, int lane) {
+// the wave-uniform operands only (the per-lane rows: accept_prefetch_rows)
+__device__ inline AccPre accept_prefetch_uniform(const AccArgs& A, int j) {
   AccPre p;
   p.jg = j + A.lo;
   p.chain = A.idx[p.jg];
@@ -112,10 +136,17 @@ __device__ inline AccPre accept_prefetch(const AccArgs& A, int j, int lane) {
   p.alpha = A.alpha2[j];
   p.xo = 0.0;
   p.yn = 0.0;
+  return p;
+}
+__device__ inline void accept_prefetch_rows(const AccArgs& A, int j, int lane, AccPre& p) {
   if (lane < kNp) {
     p.xo = A.x[(size_t)p.chain * kNp + lane];
     p.yn = A.y[(size_t)j * kNp + lane];
   }
+}
+__device__ inline AccPre accept_prefetch(const AccArgs& A, int j, int lane) {
+  AccPre p = accept_prefetch_uniform(A, j);
+  accept_prefetch_rows(A, j, lane, p);
   return p;
 }
 

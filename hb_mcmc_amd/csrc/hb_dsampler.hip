@@ -76,7 +76,7 @@ constexpr int kBlk = 64;                   // slots per workgroup of the gather 
 #endif
 constexpr int kPW = HB_DS_KPW;             // propose waves (one slot each) per workgroup
 #ifndef HB_DS_SEG  // experiment knob: owned slots per swap segment
-#define HB_DS_SEG 256
+#define HB_DS_SEG 128
 #endif
 constexpr int kSegSlots = HB_DS_SEG;       // owned slots per swap segment (one ds_swap_seg workgroup)
 constexpr int kSegThreads = 256;
@@ -98,11 +98,6 @@ struct Params {
 
 // one tempering attempt of the level schedule: pair (b, b+1) and ln(beta) of
 // its acceptance draw (beta itself is kept in a global-only array beside it)
-struct SwapEnt {
-  int b;
-  int pad;
-  double lnb;
-};
 // schedule buffer of an iteration with nlv levels over G segments:
 // int soff[G nlv + 1] | (8-B aligned) SwapEnt ent[nent] | double beta[nent];
 // segment g's attempts of level l (0-based) are ent[soff[g nlv + l] ..
@@ -117,8 +112,7 @@ __host__ __device__ inline size_t sched_beta_off(size_t G, size_t nlv, size_t ne
 __host__ __device__ inline size_t sched_bytes(size_t G, size_t nlv, size_t nent) {
   return sched_beta_off(G, nlv, nent) + sizeof(double) * nent;
 }
-// first slot of segment g of G over the owned slots [lo, lo + nl)
-__host__ __device__ inline int seg_lo(int lo, int nl, int g, int G) { return lo + (int)((long long)nl * g / G); }
+
 
 // device state (pointers into one allocation set)
 struct Dev {
@@ -394,8 +388,21 @@ __device__ double gauss_batch(WaveStream& S, int& iset, double& gset, const hbgl
 // finish first, issue the reads; system-scope loads bypass the GPU caches),
 // so ds_swap depends on nothing outside this stream: a separate copy stream
 // cost an inter-queue event wait of ~10 us per iteration before ds_swap.
+// PREP = false (more slots than one resident round of 4 waves per SIMD): the
+// epilogue's ~100 VGPRs would halve the kernel's occupancy (64 VGPRs, 7 waves
+// per SIMD without it), so the records come from a separate hb_prep_kernel
+// launch instead.
 static_assert(kPW == hbk::kPrepRoles, "the propose workgroup is one prep group");
-__global__ __launch_bounds__(64 * kPW) void ds_propose(Dev D, int W, int NPAST, long long iter,
+#ifndef HB_DS_PROPOSE_WPE
+#define HB_DS_PROPOSE_WPE 0  // > 0: minimum waves per SIMD for ds_propose (experiment builds)
+#endif
+#if HB_DS_PROPOSE_WPE > 0
+#define HB_DS_PROPOSE_ATTR __attribute__((amdgpu_waves_per_eu(HB_DS_PROPOSE_WPE)))
+#else
+#define HB_DS_PROPOSE_ATTR
+#endif
+template <bool PREP>
+__global__ __launch_bounds__(64 * kPW) HB_DS_PROPOSE_ATTR void ds_propose(Dev D, int W, int NPAST, long long iter,
                                                        const unsigned long long* __restrict__ sch_src,
                                                        unsigned long long* __restrict__ sch_dst, long long n8) {
   const long long sgt = (long long)(gridDim.x - 1 - blockIdx.x) * blockDim.x + threadIdx.x;
@@ -425,7 +432,7 @@ __global__ __launch_bounds__(64 * kPW) void ds_propose(Dev D, int W, int NPAST, 
   const int j = act ? D.order[k] : D.lo;  // global slot
   const int jl = j - D.lo;                // local slot (arrays by slot)
   double* gs = gs_s[wv];
-  const double pc_tab = *D.tab_pc;
+  const double pc_tab = PREP ? *D.tab_pc : 0.0;
 #ifdef HB_DS_TIMING  // experiment builds only: per-phase shader clocks of two slots at iteration 100
   long long tclk[8], tw0 = wall_clock64();
 #define DS_T(k) tclk[k] = clock64()
@@ -532,11 +539,11 @@ __global__ __launch_bounds__(64 * kPW) void ds_propose(Dev D, int W, int NPAST, 
     S.slide();
     if (lane < kNp) {
       D.y[(size_t)jl * kNp + lane] = yn;
-      PL.sp[wv * hbk::kNpars + lane] = yn;
+      if (PREP) PL.sp[wv * hbk::kNpars + lane] = yn;
     }
     if (lane == 3 && D.ecnt != nullptr) {  // the eval order (hbds::eval_slot_by_e)
       const int b = e_bin_desc(yn);
-      D.elist[(size_t)b * D.nl + atomicAdd(&D.ecnt[b], 1)] = jl;
+      D.elist[(size_t)b * D.nl + atomicAdd(&D.ecnt[b * kEbinStride], 1)] = jl;
     }
     if (lane < NTAB) D.iv[(size_t)jl * NTAB + lane] = S.b_tab;
     if (lane == 0) {
@@ -559,6 +566,7 @@ __global__ __launch_bounds__(64 * kPW) void ds_propose(Dev D, int W, int NPAST, 
       DS_PRINT();
     }
   }
+  if (!PREP) return;
   // the likelihood's per-walker records of the group's slots: every wave
   // reads the others' proposals from PL.sp
   const int nb = min(kPW, D.nl - (int)blockIdx.x * kPW);
@@ -733,9 +741,17 @@ __global__ __launch_bounds__(kSegThreads) void ds_swap_seg(Dev D, int W, const i
   const int lo = D.lo, hi = D.lo + D.nl;
   const int sl = seg_lo(lo, D.nl, g, G), sh = seg_lo(lo, D.nl, g + 1, G);
   const int clo = max(0, sl - nlv), chi = min(W, sh + nlv), Wc = chi - clo;
-  double* cL = reinterpret_cast<double*>(smem);
-  int* cC = reinterpret_cast<int*>(smem + sizeof(double) * (size_t)Wc);
+  // LDS: the segment's attempts (all levels), then the cone's logL, pair
+  // factors and chain ids -- staged with every load in flight, so a level
+  // costs LDS round trips only
+  const int eb = soff[g * nlv], ne = soff[g * nlv + nlv] - eb;
+  SwapEnt* sE = reinterpret_cast<SwapEnt*>(smem);
+  double* cL = reinterpret_cast<double*>(smem + sizeof(SwapEnt) * (size_t)ne);
+  double* cH = cL + Wc;
+  int* cC = reinterpret_cast<int*>(cH + Wc);
   for (int q = tid; q < 256; q += kSegThreads) exp_s[q] = hbglibc::kExpTab[q];
+  for (int q = tid; q < ne; q += kSegThreads) sE[q] = ent[eb + q];
+  for (int i = tid; i < Wc; i += kSegThreads) cH[i] = D.hs[clo + i];
   const hbglibc::Tabs T{exp_s, hbglibc::kLogTab, hbglibc::kPowTab};
   if (!XCHG) {
     for (int i = tid; i < Wc; i += kSegThreads) {
@@ -790,18 +806,18 @@ __global__ __launch_bounds__(kSegThreads) void ds_swap_seg(Dev D, int W, const i
   // the glibc-exact exp is compared with beta itself
   int nacc = 0;
   for (int lv = 0; lv < nlv; ++lv) {
-    const int e0 = soff[g * nlv + lv], e1 = soff[g * nlv + lv + 1];
+    const int e0 = soff[g * nlv + lv] - eb, e1 = soff[g * nlv + lv + 1] - eb;
     for (int q = e0 + tid; q < e1; q += kSegThreads) {
-      const int b = ent[q].b;
-      const double lnb = ent[q].lnb;
+      const int b = sE[q].b;
+      const double lnb = sE[q].lnb;
       const int bl = b - clo, al = bl + 1;
       const double lb = cL[bl], la = cL[al];
-      const double x = (lb - la) * D.hs[b];  // (L[idx b] - L[idx a]) (T_b - T_a)/(T_b T_a), :803
+      const double x = (lb - la) * cH[bl];  // (L[idx b] - L[idx a]) (T_b - T_a)/(T_b T_a), :803
       bool acc;
       const double dl = 1e-12 * (1.0 + fabs(lnb));
       if (lnb > -HUGE_VAL && x >= lnb + dl) acc = true;
       else if (lnb > -HUGE_VAL && x <= lnb - dl) acc = false;
-      else acc = hbglibc::exp(x, T) >= betas[q];
+      else acc = hbglibc::exp(x, T) >= betas[eb + q];
       if (acc) {
         const int ca = cC[al], cb = cC[bl];
         cL[al] = lb;
@@ -817,7 +833,7 @@ __global__ __launch_bounds__(kSegThreads) void ds_swap_seg(Dev D, int W, const i
   for (int s = sl + tid; s < sh; s += kSegThreads) D.idx_out[s] = cC[s - clo];
   if (iter % 100 == 0)
     for (int s = sl + tid; s < sh; s += kSegThreads) D.DEacc_arr[s - lo] = D.DEtrial_arr[s - lo] = 0;
-  if (g == 0 && D.ecnt != nullptr && tid < kOrdBins) D.ecnt[tid] = 0;  // the eval launch read them
+  if (g == 0 && D.ecnt != nullptr && tid < kOrdBins) D.ecnt[tid * kEbinStride] = 0;  // the eval launch read them
   __syncthreads();
   if (tid == 0) {
     if (nacc_s) atomicAdd((unsigned long long*)&D.ctr->nswap, (unsigned long long)nacc_s);
@@ -891,13 +907,19 @@ struct hb_dsampler {
   static constexpr int R_RING = 8;
   unsigned char* pin[R_RING] = {};
   unsigned char* d_sched[R_RING] = {};
-  hipEvent_t ev_used[R_RING] = {};  // the swap that read ring slot r done
+  hipEvent_t ev_used[R_RING] = {};  // recorded after the swaps of every ev_every-th iteration (slot r)
+  // an event after every swap launch costs a cache-flushing barrier packet
+  // (~5 us of idle GPU before the next ds_propose, rocprof timeline); every
+  // fourth iteration suffices for the producers' slot reuse
+  int ev_every = 4;
+  long long q_issued = 0;  // iterations whose swaps are enqueued
   struct Slot {
     long long q = -1;       // iteration it holds (-1: never used)
     bool ready = false;     // schedule written
     bool released = false;  // its ds_swap_seg is enqueued and ev_used recorded
     bool overflow = false;  // more than kMaxLevels levels or sched_cap bytes: the step fails
     int nent = 0, nlv = 0;
+    int maxent = 0;         // most attempts of one segment (ds_swap_seg stages them in LDS)
   };
   Slot slots[R_RING];
   std::mutex smu;
@@ -909,6 +931,7 @@ struct hb_dsampler {
   size_t sched_cap = 0;                             // bytes per ring slot
   int nthreads = 0;
   int nseg = 1;  // swap segments (ds_swap_seg workgroups) over the owned slots
+  bool fused_prep = true;  // walker records in ds_propose's epilogue (else an hb_prep_kernel launch)
   // host timers [s]: producer work (all threads), waits for a schedule, issue
   double t_prod = 0.0, t_wait = 0.0, t_issue = 0.0;
   // the iteration between step_begin and step_end
@@ -955,6 +978,22 @@ static int ds_upload(hb_dsampler* d, const int* chain_of_slot);
 // b_i or b_i + 1), and for each segment g of the owned slots the attempts
 // whose pair lies in its cone [sl_g - nlv, sh_g + nlv) by level
 // (ds_swap_seg).  Per-thread scratch in `sc`.
+// the segments g of the owned slots [lo, lo + nl) whose cone
+// [sl_g - nlv, sh_g + nlv) holds the pair (b, b + 1): sl_g - nlv <= b and
+// b + 1 < sh_g + nlv, a contiguous range g0 .. g1 (empty: g0 > g1)
+static void pair_segments(int b, int nlv, int lo, int nl, int G, int& g0, int& g1) {
+  g0 = seg_of(b + 1 - nlv - lo, nl, G);
+  while (g0 < G && seg_lo(lo, nl, g0 + 1, G) + nlv <= b + 1) ++g0;
+  g1 = seg_of(b + nlv - lo, nl, G);
+  while (g1 >= 0 && seg_lo(lo, nl, g1, G) - nlv > b) --g1;
+}
+
+// test hook (tests/test_dsampler.py): the producer's segment ranges
+extern "C" int hbx_pair_segments(int b, int nlv, int lo, int nl, int G, int* g0, int* g1) {
+  pair_segments(b, nlv, lo, nl, G, *g0, *g1);
+  return 0;
+}
+
 struct SchedScratch {
   std::vector<int> b, lvl, last, cnt;
   std::vector<double> beta;
@@ -994,20 +1033,7 @@ static void sched_build(hb_dsampler* d, long long q, int slot, SchedScratch& sc)
   }
   // segments whose cone holds the pair (b, b + 1): sl_g - nlv <= b and
   // b + 1 < sh_g + nlv -- a contiguous range of g
-  auto seg_of = [&](int s) {  // segment owning slot s (clamped to the owned range)
-    if (s < lo) return 0;
-    if (s >= lo + nl) return G - 1;
-    int g = (int)(((long long)(s - lo) * G) / nl);
-    while (g + 1 < G && seg_lo(lo, nl, g + 1, G) <= s) ++g;
-    while (g > 0 && seg_lo(lo, nl, g, G) > s) --g;
-    return g;
-  };
-  auto seg_range = [&](int b, int& g0, int& g1) {
-    g0 = seg_of(b + 1 - nlv);
-    while (g0 < G && seg_lo(lo, nl, g0 + 1, G) + nlv <= b + 1) ++g0;
-    g1 = seg_of(b + nlv);
-    while (g1 >= 0 && seg_lo(lo, nl, g1, G) - nlv > b) --g1;
-  };
+  auto seg_range = [&](int b, int& g0, int& g1) { pair_segments(b, nlv, lo, nl, G, g0, g1); };
   sc.cnt.assign((size_t)G * nlv + 1, 0);
   size_t nent = 0;
   for (int i = 0; i < W; ++i) {
@@ -1034,6 +1060,9 @@ static void sched_build(hb_dsampler* d, long long q, int slot, SchedScratch& sc)
     sc.cnt[k] = soff[k];  // next free entry of (segment, level)
   }
   soff[(size_t)G * nlv] = run;
+  int maxent = 0;
+  for (int g = 0; g < G; ++g) maxent = std::max(maxent, soff[(size_t)(g + 1) * nlv] - soff[(size_t)g * nlv]);
+  sl.maxent = maxent;
   for (int i = 0; i < W; ++i) {
     if (sc.lvl[i] <= 0) continue;
     int g0, g1;
@@ -1059,23 +1088,26 @@ static void sched_worker(hb_dsampler* d) {
   constexpr int K = hb_dsampler::R_RING;
   while (true) {
     long long q;
-    int slot;
+    int slot, ev_slot = 0;
     bool reused;
     {
       std::unique_lock<std::mutex> lk(d->smu);
       d->scv.wait(lk, [&] {
         if (d->stop) return true;
         const hb_dsampler::Slot& sl = d->slots[d->q_prod % K];
-        return sl.q < 0 || (sl.q == d->q_prod - K && sl.released);
+        if (sl.q < 0) return true;
+        const long long q_rec = (sl.q / d->ev_every) * d->ev_every + d->ev_every - 1;  // next recorded event
+        return sl.q == d->q_prod - K && sl.released && d->q_issued > q_rec;
       });
       if (d->stop) return;
       q = d->q_prod++;
       slot = (int)(q % K);
       reused = d->slots[slot].q >= 0;
+      if (reused) ev_slot = (int)(((d->slots[slot].q / d->ev_every) * d->ev_every + d->ev_every - 1) % K);
       d->slots[slot] = hb_dsampler::Slot{};
       d->slots[slot].q = q;
     }
-    if (reused && hipEventSynchronize(d->ev_used[slot]) != hipSuccess) return;  // the GPU is done with it
+    if (reused && hipEventSynchronize(d->ev_used[ev_slot]) != hipSuccess) return;  // the GPU is done with it
     const double t0 = now_s();
     sched_build(d, q, slot, sc);
     const double dt = now_s() - t0;
@@ -1162,10 +1194,20 @@ static hb_dsampler* ds_create(hb_sampler* s, hb_ctx* ctx, const int* chain_of_sl
   D.P = d->d_params;
   // eval order by e bins (AccArgs::ecnt) up to kEvalOrdMax owned slots
   if (Nz <= (size_t)kEvalOrdMax && !d->no_eord) {
-    if ((e = d->alloc(&D.ecnt, (size_t)kOrdBins)) || (e = d->alloc(&D.elist, (size_t)kOrdBins * Nz)))
+    if ((e = d->alloc(&D.ecnt, (size_t)kOrdBins * kEbinStride)) || (e = d->alloc(&D.elist, (size_t)kOrdBins * Nz)))
       return fail("hipMalloc", e);
-    if ((e = hipMemsetAsync(D.ecnt, 0, sizeof(int) * kOrdBins, d->st))) return fail("hipMemset", e);
+    if ((e = hipMemsetAsync(D.ecnt, 0, sizeof(int) * kOrdBins * kEbinStride, d->st))) return fail("hipMemset", e);
   }
+  // records in ds_propose's epilogue while the slots fit one resident round
+  // of its waves at that occupancy (4 per SIMD, 16 per CU); HB_DS_FUSED_PREP=0/1 forces
+  {
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, d->device) != hipSuccess || cus <= 0)
+      cus = 256;
+    const char* fp = getenv("HB_DS_FUSED_PREP");
+    d->fused_prep = fp ? atoi(fp) != 0 : d->nl <= 16 * cus;
+  }
+  if (const char* ee = getenv("HB_DS_EV_EVERY")) d->ev_every = std::max(1, atoi(ee));  // experiment knob
   // swap segments of <= kSegSlots owned slots; an attempt is listed for at
   // most min(G, 3 + 2 kMaxLevels / (smallest segment)) segments
   d->nseg = std::max(1, (d->nl + kSegSlots - 1) / kSegSlots);
@@ -1274,6 +1316,7 @@ static int ds_upload(hb_dsampler* d, const int* chain_of_slot) {
   DS_TRY(hipMemcpyAsync(D.logP, Pp.data(), sizeof(double) * Wz, hipMemcpyHostToDevice, s), "upload");
   DS_TRY(hipMemcpyAsync(D.logP_ok, ok.data(), sizeof(int) * Wz, hipMemcpyHostToDevice, s), "upload");
   DS_TRY(hipMemcpyAsync(D.idx, idx.data(), sizeof(int) * Wz, hipMemcpyHostToDevice, s), "upload");
+  DS_TRY(hipMemcpyAsync(D.idx_out, idx.data(), sizeof(int) * Wz, hipMemcpyHostToDevice, s), "upload");
   DS_TRY(hipMemcpyAsync(D.temp, v.temp, sizeof(double) * Wz, hipMemcpyHostToDevice, s), "upload");
   // propose waves in descending temperature: the hot rungs' long wall runs
   // are dispatched first (ds_propose lasts as long as its latest-finishing
@@ -1482,12 +1525,15 @@ static long ds_begin(hb_dsampler* d, long iter, double* send, long cap) {
     Dp.wc = static_cast<double*>(wc);
     Dp.tab_pc = tab_pc;
   }
-  ds_propose<<<(nl + kPW - 1) / kPW, 64 * kPW, 0, s>>>(
-      Dp, W, NPAST, (long long)iter, reinterpret_cast<const unsigned long long*>(d->pin[slot]),
-      reinterpret_cast<unsigned long long*>(d->d_sched[slot]), (long long)(used_bytes / 8));
+  auto* sch_src = reinterpret_cast<const unsigned long long*>(d->pin[slot]);
+  auto* sch_dst = reinterpret_cast<unsigned long long*>(d->d_sched[slot]);
+  const long long n8 = (long long)(used_bytes / 8);
+  if (d->fused_prep)
+    ds_propose<true><<<(nl + kPW - 1) / kPW, 64 * kPW, 0, s>>>(Dp, W, NPAST, (long long)iter, sch_src, sch_dst, n8);
+  else
+    ds_propose<false><<<(nl + kPW - 1) / kPW, 64 * kPW, 0, s>>>(Dp, W, NPAST, (long long)iter, sch_src, sch_dst, n8);
   DS_TRY(hipGetLastError(), "ds_propose");
-  static const bool prep_launch = getenv("HB_DS_PREP_LAUNCH") != nullptr;  // experiment knob: records by hb_prep_kernel
-  if (prep_launch) {
+  if (!d->fused_prep) {
     const int rc = hb_prepare_dev(d->ctx, D.y, nl, (void*)s);
     if (rc) return rc;
   }
@@ -1542,21 +1588,25 @@ static int ds_end(hb_dsampler* d, long iter, const double* recv, long n) {
   const SwapEnt* d_ent = reinterpret_cast<const SwapEnt*>(base + sched_ent_off((size_t)G, (size_t)sl.nlv));
   const double* d_beta =
       reinterpret_cast<const double*>(base + sched_beta_off((size_t)G, (size_t)sl.nlv, (size_t)sl.nent));
-  // LDS: the widest cone's (logL, chain) pairs
-  const size_t lds = (sizeof(double) + sizeof(int)) * ((size_t)(d->nl + G - 1) / G + 2 * (size_t)sl.nlv);
+  // LDS: the widest cone's (logL, chain, pair factor) and the largest
+  // segment's attempts
+  const size_t wc_max = (size_t)(d->nl + G - 1) / G + 2 * (size_t)sl.nlv;
+  const size_t lds = sizeof(SwapEnt) * (size_t)sl.maxent + (2 * sizeof(double) + sizeof(int)) * wc_max;
   if (d->xchg) {
     const Gathered X{recv, (long long)n, d->R, d->rank, d->m, 0};
     ds_swap_seg<true><<<G, kSegThreads, lds, s>>>(D, W, d_soff, d_ent, d_beta, sl.nlv, G, (long long)iter, X);
+    DS_TRY(hipGetLastError(), "ds_swap_seg");
   } else {
     const Gathered X{nullptr, 0, 1, 0, 0, 0};
     ds_swap_seg<false><<<G, kSegThreads, lds, s>>>(D, W, d_soff, d_ent, d_beta, sl.nlv, G, (long long)iter, X);
+    DS_TRY(hipGetLastError(), "ds_swap_seg");
   }
-  DS_TRY(hipGetLastError(), "ds_swap_seg");
   std::swap(d->D.idx, d->D.idx_out);  // the next iteration reads what the swaps wrote
-  DS_TRY(hipEventRecord(d->ev_used[slot], s), "schedule ring");
+  if ((sl.q + 1) % d->ev_every == 0) DS_TRY(hipEventRecord(d->ev_used[slot], s), "schedule ring");
   {
     std::lock_guard<std::mutex> lk(d->smu);
     d->slots[slot].released = true;
+    d->q_issued = sl.q + 1;
   }
   d->scv.notify_all();
   d->t_issue += now_s() - t0;

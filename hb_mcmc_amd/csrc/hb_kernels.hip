@@ -53,6 +53,9 @@ using namespace hbdev;
 #ifndef HB_ABLATE_SELECT
 #define HB_ABLATE_SELECT 0
 #endif
+#ifndef HB_ACC_PRE
+#define HB_ACC_PRE 1  // fused Hastings test: operands loaded at wave start (see hb_eval_wave_kernel)
+#endif
 #ifndef HB_PRIO
 #define HB_PRIO 1  // wave pacing (Pacer): 0 off, 1 by own quartile, 2 by lead over the SIMD's slowest wave
 #endif
@@ -612,8 +615,10 @@ __device__ __forceinline__ void model_pass_chain(const double* __restrict__ tT, 
   const int last = n - 1;
   const int base = lane * rw.rc;
   const int rs = lane * rw.stride, lsw = HB_ODD_STRIDE ? 0 : (lane & rw.swz);  // slab_pos = rs + (c ^ lsw)
+#if !HB_GQ
   const uint64_t lt_mask = (1ull << lane) - 1ull;
   int qn = 0;  // queued eclipse cadences (wave-uniform)
+#endif
   ChainState<KC> st;
   double tk[KC];
 #pragma unroll
@@ -1455,11 +1460,19 @@ __global__ __launch_bounds__(64 * WPB) HB_WPE_ATTR void hb_eval_wave_kernel(
 #endif
   if (!valid) return;
   // the Hastings test's operands are loaded now, not after the likelihood
+  // HB_ACC_PRE 1: all of it (uniform values and the 21-coordinate rows);
+  // 2: the uniform values only, the rows when the test runs; 0: nothing
   hbds::AccPre apre{};
-  if (ACC) apre = hbds::accept_prefetch(hst, wv, lane);
+  if (ACC && HB_ACC_PRE == 1) apre = hbds::accept_prefetch(hst, wv, lane);
+  if (ACC && HB_ACC_PRE == 2) apre = hbds::accept_prefetch_uniform(hst, wv);
+  auto acc_tail = [&](double ly) {
+    if (HB_ACC_PRE == 0) apre = hbds::accept_prefetch(hst, wv, lane);
+    if (HB_ACC_PRE == 2) hbds::accept_prefetch_rows(hst, wv, lane, apre);
+    hbds::accept_slot_wave_pre(hst, wv, ly, lane, apre);
+  };
   if (roche_exit) {  // likelihood3.c:866-869, see hb_eval_kernel
     if (lane == 0) logl[wv] = -kBig / 2.0;
-    if (ACC) hbds::accept_slot_wave_pre(hst, wv, -kBig / 2.0, lane, apre);
+    if (ACC) acc_tail(-kBig / 2.0);
     HB_CLK_END(wv);
     return;
   }
@@ -1536,7 +1549,7 @@ __global__ __launch_bounds__(64 * WPB) HB_WPE_ATTR void hb_eval_wave_kernel(
     double c = chi2 + w.chi2_extra;
     if (w.roche != 0.0) c = kBig;
     if (lane == 0) logl[wv] = -c / 2.0;
-    if (ACC) hbds::accept_slot_wave_pre(hst, wv, -c / 2.0, lane, apre);  // c is wave-uniform (readlanes)
+    if (ACC) acc_tail(-c / 2.0);  // c is wave-uniform (readlanes)
     HB_CLK_END(wv);
     return;
   }
@@ -1631,7 +1644,7 @@ __global__ __launch_bounds__(64 * WPB) HB_WPE_ATTR void hb_eval_wave_kernel(
   if (ACC) {
     double c = chi2 + w.chi2_extra;  // wave-uniform (the DPP sum ends in readlanes)
     if (w.roche != 0.0) c = kBig;
-    hbds::accept_slot_wave_pre(hst, wv, __shfl(-c / 2.0, 0), lane, apre);
+    acc_tail(__shfl(-c / 2.0, 0));
   }
   HB_CLK_END(wv);
 }

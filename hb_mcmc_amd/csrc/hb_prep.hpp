@@ -101,7 +101,6 @@ __device__ __forceinline__ void prep_records(PrepShared<NW>& L, int nb, const Ma
   const double r1 = star ? ro : r, r2 = star ? r : ro;
   const double t1 = star ? tko : tk, t2 = star ? tk : tko;
   WalkerConst* wc = reinterpret_cast<WalkerConst*>(&L.so[jc * kWcDoubles]);
-  double terms[12];
   double si = 0.0, ci = 0.0;
   double aR = 0.0, sq1me2 = 0.0, inv1me2 = 0.0, mA = 0.0;  // wave 0's orbit fields, off the last phase
   if (chainR) {
@@ -118,6 +117,7 @@ __device__ __forceinline__ void prep_records(PrepShared<NW>& L, int nb, const Ma
     const StarCoef c = star_coef(pd, m, mo, e, si, r, ro, p[9 + 2 * star], p[10 + 2 * star], p[13 + star], ab);
     // star 2 sees u + pi: odd harmonics flip sign
     const double sg = star ? -1.0 : 1.0;
+    double terms[12];
     terms[0] = nself * c.am1;
     terms[1] = nself * c.kb * sg;
     terms[2] = nself * c.kref;
@@ -130,9 +130,9 @@ __device__ __forceinline__ void prep_records(PrepShared<NW>& L, int nb, const Ma
     terms[9] = nself * c.c22;
     terms[10] = nself * c.c4;
     terms[11] = nself;
-    if (star == 1 && live) {
+    if (live) {  // both stars' terms through LDS (no 12 registers held across the barrier)
 #pragma unroll
-      for (int q = 0; q < 12; ++q) L.xs[1][4 + q][j] = terms[q];
+      for (int q = 0; q < 12; ++q) L.xs[star][4 + q][j] = terms[q];
     }
   } else if (star == 1) {
     if (live) {
@@ -192,7 +192,7 @@ __device__ __forceinline__ void prep_records(PrepShared<NW>& L, int nb, const Ma
   if (wv == 0 && live) {
     double tt[12];
 #pragma unroll
-    for (int q = 0; q < 12; ++q) tt[q] = terms[q] + L.xs[1][4 + q][j];  // star-1 term first
+    for (int q = 0; q < 12; ++q) tt[q] = L.xs[0][4 + q][j] + L.xs[1][4 + q][j];  // star-1 term first
     const double gr = L.gs[0][j];
     // orbit
     wc->Pc = pd * kDay;

@@ -40,7 +40,8 @@ def main(d):
         pr = res["per_rank"]
         ms = max(p["ms_per_iter"] for p in pr)
         print(f"== {name}: W={W} ranks={R} ({W // R} walkers a rank), tree={os.path.basename(res['tree'])}")
-        print(f"   wall ms/iter (max over ranks, gloo exchange staged through host): {ms:.3f}")
+        print(f"   wall ms/iter (max over ranks{', gloo exchange staged through host' if R > 1 else ''}): {ms:.3f}")
+        print("   host ms/iter inside step(): " + " ".join(f"{p.get('host_step_ms', float('nan')):.3f}" for p in pr))
         if "sched_build" in pr[0]:
             for k in ("sched_build", "sched_wait", "issue"):
                 print(f"   host {k:12s} ms/iter: " + " ".join(f"{p[k]:.3f}" for p in pr))

@@ -3,9 +3,10 @@
 #   gpurun -- bash scripts/gpu_dsp.sh TAG [TREE_OLD]
 # 1. the sharded / device-sampler GPU tests of this tree;
 # 2. scripts/ds_shard_profile.py under rocprofv3 --kernel-trace --stats for
-#    this tree and (optionally) an older build's worktree, at the C4 rank
-#    shape (W = 65 536 over 8 gloo ranks = 8 192 walkers a rank) and at
-#    W = 16 384 over 2 ranks.  Output: gpurun_out/dsp_TAG/.
+#    this tree and (optionally) an older build's worktree at W = 65 536 (C4's
+#    ensemble): one process, 2 gloo ranks, and 8 gloo ranks (8 192 walkers a
+#    rank, C4's rank shape), all sharing the box's GPU.
+#    Output: gpurun_out/dsp_TAG/.
 set -o pipefail
 TAG=${1:-x}
 OLD=${2:-}
@@ -20,16 +21,22 @@ if [ -z "$SKIP_TESTS" ]; then
   tail -3 "$OUT/tests.log"
 fi
 cd /tmp && export TMPDIR=/tmp
-run() {  # name tree R W
-  local name=$1 tree=$2 R=$3 W=$4
+run() {  # name tree R W [serial]
+  local name=$1 tree=$2 R=$3 W=$4 mode=${5:-}
   HB_TREE=$tree timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$name/%pid%" -o run -- \
     python3 -m torch.distributed.run --nnodes=1 --nproc-per-node "$R" --master-addr 127.0.0.1 \
-    --master-port $((29500 + RANDOM % 1000)) "$ROOT/scripts/ds_shard_profile.py" "$OUT/$name.json" "$W" 100 20 \
+    --master-port $((29500 + RANDOM % 1000)) "$ROOT/scripts/ds_shard_profile.py" "$OUT/$name.json" "$W" 100 20 1024 $mode \
     > "$OUT/$name.log" 2>&1 || { tail -30 "$OUT/$name.log"; return 1; }
   tail -1 "$OUT/$name.log"
 }
-run new_r8 "$ROOT" 8 65536 && run new_r2 "$ROOT" 2 16384 || exit 1
-if [ -n "$OLD" ]; then
-  run old_r8 "$ROOT/$OLD" 8 65536 && run old_r2 "$ROOT/$OLD" 2 16384 || exit 1
-fi
+# concurrent ranks (wall time, host split), then ranks taking turns on the
+# GPU (kernel durations of one rank alone: "s" runs)
+for R in 1 2 8; do
+  run new_r$R "$ROOT" $R 65536 || exit 1
+  if [ -n "$OLD" ]; then run old_r$R "$ROOT/$OLD" $R 65536 || exit 1; fi
+done
+for R in 2 8; do
+  run new_s$R "$ROOT" $R 65536 serial || exit 1
+  if [ -n "$OLD" ]; then run old_s$R "$ROOT/$OLD" $R 65536 serial || exit 1; fi
+done
 python3 "$ROOT/scripts/dsp_summary.py" "$OUT" > "$OUT/summary.txt" && cat "$OUT/summary.txt"

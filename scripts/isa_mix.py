@@ -8,7 +8,7 @@ path, sym = sys.argv[1], sys.argv[2]
 top = int(sys.argv[3]) if len(sys.argv) > 3 else 12
 lines = open(path).read().splitlines()
 start = next(i for i, l in enumerate(lines) if l.startswith(sym + ":"))
-end = next(i for i in range(start, len(lines)) if "s_endpgm" in lines[i])
+end = next(i for i in range(start, len(lines)) if lines[i].startswith(".Lfunc_end"))
 blocks, cur, name = [], [], "entry"
 for l in lines[start + 1:end + 1]:
     s = l.strip()

@@ -82,6 +82,32 @@ def test_level_count_is_small():
     assert lv.max() <= 20
 
 
+def _seg_lo(lo, nl, g, G):
+    return lo + (nl * g) // G
+
+
+@pytest.mark.parametrize("nl,G,nlv", [(50, 1, 7), (4096, 32, 10), (4096, 32, 0), (1000, 8, 200), (300, 3, 1),
+                                      (7, 2, 5), (65536, 512, 14)])
+def test_segment_ranges_are_exactly_the_cones(nl, G, nlv):
+    """The producer's per-segment attempt lists (hb_dsampler.hip
+    pair_segments): for every pair (b, b+1) the returned segments are exactly
+    those whose cone [sl - nlv, sh + nlv) holds the pair -- for one process
+    and for a rank owning [lo, lo + nl) of a larger ladder."""
+    import ctypes as C
+
+    from hb_mcmc_amd import _lib
+
+    lib = _lib.lib()
+    g0, g1 = C.c_int(), C.c_int()
+    for lo, Wt in ((0, nl), (nl // 3, 3 * nl)):
+        sl = np.array([_seg_lo(lo, nl, g, G) for g in range(G + 1)])
+        for b in (range(Wt - 1) if Wt <= 5000 else list(range(0, Wt - 1, 5)) + [Wt - 2]):
+            want = {g for g in range(G) if sl[g] - nlv <= b and b + 1 < sl[g + 1] + nlv}
+            lib.hbx_pair_segments(b, nlv, lo, nl, G, C.byref(g0), C.byref(g1))
+            got = set(range(g0.value, g1.value + 1))
+            assert want == got, (lo, b, want, got)
+
+
 def test_device_sampler_symbols_exported():
     from hb_mcmc_amd import _lib, sampler
 
@@ -151,11 +177,13 @@ def _host_vs_device(W, niter, ladder, seed_run=0, n=256):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("W,niter,ladder,n", [(50, 60, 0, 256), (4096, 30, 1, 256), (6000, 24, 1, 256),
-                                              (100, 30, 0, 2500)])
+                                              (100, 30, 0, 2500), (1000, 40, 1, 1024)])
 def test_device_sampler_state_equals_host_sampler(W, niter, ladder, n):
     """n = 2500 takes the multi-wave likelihood plan, where the Hastings test
     runs as its own ds_accept launch instead of the eval kernel's epilogue;
-    W = 100 leaves the last workgroup partly filled (36 of 64 slots)."""
+    W = 100 leaves the last workgroup partly filled (36 of 64 slots);
+    W = 1000 at n = 1024: 8 swap segments of 125 slots, the records written by
+    ds_propose's epilogue."""
     ((hx, hl, hc, hs, ha), (dx, dl, dc, ds, da)), x0 = _host_vs_device(W, niter, ladder, n=n)
     assert np.array_equal(hc, dc), "chain ids by slot"
     assert np.array_equal(hx, dx), "states"
