@@ -45,7 +45,7 @@ def is_eval(r):
     return "hb_eval_wave_kernel<" in k and ", true," in k
 
 
-prep_grid = ((walkers + 63) // 64) * 256
+prep_grid = ((walkers + 15) // 16) * 256  # hb_prep_kernel: 16 walkers per 256-thread workgroup (HB_PREP_W)
 ev = collections.defaultdict(float)
 calls = collections.Counter()
 disp = collections.defaultdict(set)
