@@ -366,6 +366,14 @@ extern "C" int hbx_loglik_accept_dev(hb_ctx* c, const double* d_params, int w, d
                    static_cast<const hbds::AccArgs*>(acc), false);
 }
 
+// internal (device sampler): LDS bytes each wave of the fused likelihood +
+// Hastings launch owns (the swap tail restages its segment there); 0 when the
+// plan has no one-wave path
+extern "C" long hbx_ctx_wave_lds(const hb_ctx* c) {
+  if (!c || c->plan.vpt == 0) return 0;
+  return (long)hbk::wave_lds_bytes(c->plan.slab_bytes, c->plan.vpt);
+}
+
 // internal (device sampler): where its propose epilogue writes the walker
 // records (valid until the next hb_reserve that grows the workspace), the
 // magnitude data of the Gaia term, and the device word holding the period of

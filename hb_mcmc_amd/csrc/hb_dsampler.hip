@@ -60,6 +60,8 @@ extern "C" int hbx_ctx_device(const hb_ctx* c);
 extern "C" int hbx_ctx_prep_args(hb_ctx* c, void** wc, void* mags, double** tab_pc);
 extern "C" int hbx_loglik_accept_dev(hb_ctx* c, const double* d_params, int w, double* d_logl, const void* acc,
                                      void* stream);
+extern "C" long hbx_ctx_wave_lds(const hb_ctx* c);
+extern "C" int hbx_swap_tail_compiled(void);
 
 namespace hbds {
 
@@ -733,7 +735,7 @@ template <bool XCHG>
 __global__ __launch_bounds__(kSegThreads) void ds_swap_seg(Dev D, int W, const int* __restrict__ soff,
                                                             const SwapEnt* __restrict__ ent,
                                                             const double* __restrict__ betas, int nlv, int G,
-                                                            long long iter, Gathered X) {
+                                                            long long iter, Gathered X, const double* __restrict__ Ls) {
   extern __shared__ __align__(16) unsigned char smem[];
   __shared__ int nacc_s;
   __shared__ uint64_t exp_s[256];  // exp table for the divergent lookups of the band case
@@ -757,7 +759,7 @@ __global__ __launch_bounds__(kSegThreads) void ds_swap_seg(Dev D, int W, const i
     for (int i = tid; i < Wc; i += kSegThreads) {
       const int c = D.idx[clo + i];
       cC[i] = c;
-      cL[i] = D.logL[c];
+      cL[i] = Ls != nullptr ? Ls[clo + i] : D.logL[c];  // Ls: by slot, written by the fused Hastings test
     }
   } else {
     auto rlo = [&](int r) { return (int)((long long)W * r / X.R); };
@@ -932,6 +934,14 @@ struct hb_dsampler {
   int nthreads = 0;
   int nseg = 1;  // swap segments (ds_swap_seg workgroups) over the owned slots
   bool fused_prep = true;  // walker records in ds_propose's epilogue (else an hb_prep_kernel launch)
+  // tempering swaps at the tail of the likelihood launch (hb_accept.hpp
+  // swap_tail_wave) instead of a ds_swap_seg launch: one-process samplers
+  // whose eval waves' LDS holds a segment (checked per iteration)
+  bool tail_ok = false;
+  bool tail_now = false;  // this iteration's swaps ran in the likelihood launch
+  int* d_tcnt = nullptr;     // [nseg + 2] the tail's counters (zero between launches)
+  double* d_lslot = nullptr; // [W + 1] logL by slot after the Hastings test (one-process samplers)
+  bool lslot_now = false;    // this iteration's fused Hastings test wrote d_lslot
   // host timers [s]: producer work (all threads), waits for a schedule, issue
   double t_prod = 0.0, t_wait = 0.0, t_issue = 0.0;
   // the iteration between step_begin and step_end
@@ -1211,6 +1221,18 @@ static hb_dsampler* ds_create(hb_sampler* s, hb_ctx* ctx, const int* chain_of_sl
   // swap segments of <= kSegSlots owned slots; an attempt is listed for at
   // most min(G, 3 + 2 kMaxLevels / (smallest segment)) segments
   d->nseg = std::max(1, (d->nl + kSegSlots - 1) / kSegSlots);
+  {
+    // the tail counts a slot in the cones of at most 64 segments (one per lane)
+    // experiment (measured slower): HB_DS_TAIL=1 with a library built with -DHB_SWAP_TAIL=1
+    const char* tl = getenv("HB_DS_TAIL");
+    const bool one = !d->xchg && d->lo == 0 && d->nl == W;
+    d->tail_ok = one && d->nl / d->nseg >= 8 && tl && atoi(tl) != 0 && hbx_swap_tail_compiled();
+    if (one && (e = d->alloc(&d->d_lslot, Wz + 1))) return fail("hipMalloc", e);
+    if (d->tail_ok) {
+      if ((e = d->alloc(&d->d_tcnt, (size_t)d->nseg + 2))) return fail("hipMalloc", e);
+      if ((e = hipMemsetAsync(d->d_tcnt, 0, sizeof(int) * ((size_t)d->nseg + 2), d->st))) return fail("hipMemset", e);
+    }
+  }
   {
     const size_t G = (size_t)d->nseg, segmin = std::max<size_t>(1, (size_t)d->nl / G);
     const size_t per = std::min(G, 3 + 2 * (size_t)kMaxLevels / segmin);
@@ -1539,10 +1561,33 @@ static long ds_begin(hb_dsampler* d, long iter, double* send, long cap) {
   }
   // likelihood with the Hastings test fused into its waves' epilogue
   // (hb_accept.hpp); ds_accept only where the plan has no one-wave kernel
-  const AccArgs acc{D.idx, D.logL, D.logP, D.logPy, D.temp, D.alpha2, D.jump, D.jtype, D.x, D.y, D.hist,
-                    D.DEacc_arr, D.ctr, D.ev, d->P.log_on, NPAST, (long long)iter, d->lo, 0,
-                    D.ecnt, D.elist, nl, 0};
+  AccArgs acc{D.idx, D.logL, D.logP, D.logPy, D.temp, D.alpha2, D.jump, D.jtype, D.x, D.y, D.hist,
+              D.DEacc_arr, D.ctr, D.ev, d->P.log_on, NPAST, (long long)iter, d->lo, 0,
+              D.ecnt, D.elist, nl, 0};
+  d->tail_now = false;
+  acc.Lslot = d->d_lslot;  // null for exchanging samplers
+  if (d->tail_ok) {  // the swaps at the launch's tail when a wave's LDS holds the largest segment
+    const int G = d->nseg;
+    const size_t wc_max = (size_t)(nl + G - 1) / G + 2 * (size_t)sl.nlv;
+    if ((long)tail_lds_bytes((size_t)sl.maxent, wc_max) <= hbx_ctx_wave_lds(d->ctx)) {
+      const unsigned char* base = d->d_sched[slot];
+      acc.tcnt = d->d_tcnt;
+      acc.soff = reinterpret_cast<const int*>(base);
+      acc.ent = reinterpret_cast<const SwapEnt*>(base + sched_ent_off((size_t)G, (size_t)sl.nlv));
+      acc.betas = reinterpret_cast<const double*>(base + sched_beta_off((size_t)G, (size_t)sl.nlv, (size_t)sl.nent));
+      acc.hs = D.hs;
+      acc.idx_out = D.idx_out;
+      acc.DEtrial_arr = D.DEtrial_arr;
+      acc.ecnt_w = D.ecnt;
+      acc.W = W;
+      acc.nlv = sl.nlv;
+      acc.G = G;
+      acc.nl = nl;
+    }
+  }
   int rc = hbx_loglik_accept_dev(d->ctx, D.y, nl, D.logLy, &acc, (void*)s);
+  if (rc == 0 && acc.tcnt != nullptr) d->tail_now = true;
+  d->lslot_now = rc == 0 && acc.Lslot != nullptr;
   if (rc == 1) {
     rc = hb_evaluate_dev(d->ctx, nl, D.logLy, 0, (void*)s);
     if (rc) return rc;
@@ -1592,13 +1637,16 @@ static int ds_end(hb_dsampler* d, long iter, const double* recv, long n) {
   // segment's attempts
   const size_t wc_max = (size_t)(d->nl + G - 1) / G + 2 * (size_t)sl.nlv;
   const size_t lds = sizeof(SwapEnt) * (size_t)sl.maxent + (2 * sizeof(double) + sizeof(int)) * wc_max;
-  if (d->xchg) {
+  if (d->tail_now) {
+    // the likelihood launch's waves ran the swaps and the bookkeeping
+  } else if (d->xchg) {
     const Gathered X{recv, (long long)n, d->R, d->rank, d->m, 0};
-    ds_swap_seg<true><<<G, kSegThreads, lds, s>>>(D, W, d_soff, d_ent, d_beta, sl.nlv, G, (long long)iter, X);
+    ds_swap_seg<true><<<G, kSegThreads, lds, s>>>(D, W, d_soff, d_ent, d_beta, sl.nlv, G, (long long)iter, X, nullptr);
     DS_TRY(hipGetLastError(), "ds_swap_seg");
   } else {
     const Gathered X{nullptr, 0, 1, 0, 0, 0};
-    ds_swap_seg<false><<<G, kSegThreads, lds, s>>>(D, W, d_soff, d_ent, d_beta, sl.nlv, G, (long long)iter, X);
+    ds_swap_seg<false><<<G, kSegThreads, lds, s>>>(D, W, d_soff, d_ent, d_beta, sl.nlv, G, (long long)iter, X,
+                                                   d->lslot_now ? d->d_lslot : nullptr);
     DS_TRY(hipGetLastError(), "ds_swap_seg");
   }
   std::swap(d->D.idx, d->D.idx_out);  // the next iteration reads what the swaps wrote

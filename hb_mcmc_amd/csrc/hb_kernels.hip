@@ -98,6 +98,9 @@ __device__ unsigned long long hb_wave_clk[8 * 65536];
 #define HB_CLK_END(wv) do { } while (0)
 #endif
 
+// whether this build of the eval kernel carries the swap tail (hb_accept.hpp)
+extern "C" int hbx_swap_tail_compiled(void) { return HB_SWAP_TAIL; }
+
 namespace hbk {
 
 // ---------------------------------------------------------------------------
@@ -1468,7 +1471,13 @@ __global__ __launch_bounds__(64 * WPB) HB_WPE_ATTR void hb_eval_wave_kernel(
   auto acc_tail = [&](double ly) {
     if (HB_ACC_PRE == 0) apre = hbds::accept_prefetch(hst, wv, lane);
     if (HB_ACC_PRE == 2) hbds::accept_prefetch_rows(hst, wv, lane, apre);
-    hbds::accept_slot_wave_pre(hst, wv, ly, lane, apre);
+    const bool took = hbds::accept_slot_wave_pre(hst, wv, ly, lane, apre);
+#if HB_SWAP_TAIL
+    if (hst.tcnt != nullptr)  // tempering swaps (hb_accept.hpp), on the logL the test left in the slot
+      hbds::swap_tail_wave(hst, wv, took ? ly : apre.lx, lane, smem);
+#else
+    (void)took;
+#endif
   };
   if (roche_exit) {  // likelihood3.c:866-869, see hb_eval_kernel
     if (lane == 0) logl[wv] = -kBig / 2.0;
