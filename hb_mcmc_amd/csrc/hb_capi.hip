@@ -207,7 +207,7 @@ extern "C" int hb_reserve(hb_ctx* c, int max_walkers) {
   if (!c->plan.lds)
     HB_TRY(hipMalloc(&c->d_scratch, sizeof(double) * (size_t)max_walkers * (size_t)c->plan.n),
            "hipMalloc(template scratch)");
-  const size_t qb = c->plan.vpt > 0 ? hbk::wave_queue_bytes(c->plan.vpt, max_walkers) : 0;
+  const size_t qb = c->plan.vpt > 0 ? hbk::wave_queue_bytes(c->plan.vpt, max_walkers, c->plan.wpw) : 0;
   if (qb) HB_TRY(hipMalloc(&c->d_dq, qb), "hipMalloc(deferred cadence queue)");
   c->cap = max_walkers;
   return 0;
@@ -358,7 +358,7 @@ static int run_batch(hb_ctx* c, const double* d_params, int w, double* d_logl, d
 extern "C" int hbx_loglik_accept_dev(hb_ctx* c, const double* d_params, int w, double* d_logl, const void* acc,
                                      void* stream) {
   if (!c) return set_err_msg("null context");
-  if (c->plan.vpt == 0) return 1;
+  if (c->plan.vpt == 0 || c->plan.wpw != 1) return 1;  // no fused epilogue: multi-wave or pair plans
   if (w > c->cap) return set_err_msg("hbx_loglik_accept_dev: W exceeds the prepared workspace");
   static const bool split = getenv("HB_DS_SPLIT_ACCEPT") != nullptr;  // experiment knob: separate ds_accept
   if (split) return 1;
@@ -371,7 +371,7 @@ extern "C" int hbx_loglik_accept_dev(hb_ctx* c, const double* d_params, int w, d
 // plan has no one-wave path
 extern "C" long hbx_ctx_wave_lds(const hb_ctx* c) {
   if (!c || c->plan.vpt == 0) return 0;
-  return (long)hbk::wave_lds_bytes(c->plan.slab_bytes, c->plan.vpt);
+  return (long)hbk::wave_lds_bytes(c->plan.slab_bytes, c->plan.vpt, c->plan.wpw);
 }
 
 // internal (device sampler): where its propose epilogue writes the walker
@@ -451,8 +451,10 @@ static int host_batch(hb_ctx* c, const double* params, int w, double* out, void*
 // quarters of each range, for smaller LDS slabs) measured slower: 0.424 ms on
 // one stream, 0.322-0.341 on 2-4 (launch tails dominate).
 // ---------------------------------------------------------------------------
-static constexpr int kCatClasses = 6;
-static constexpr int kCatRcHi[kCatClasses] = {1, 2, 4, 8, 16, 32};
+// class 6: N > 1280, a pair of waves per walker (hbk::wave_nr_for); its queue
+// and slab sizes are those of 32 cadences per lane of one wave
+static constexpr int kCatClasses = 7;
+static constexpr int kCatRcHi[kCatClasses] = {1, 2, 4, 8, 16, 32, 32};
 static constexpr int kCatStreams = 4;  // the caller's + 3 forked
 // experiment knob (A/B only): HB_CAT_STREAMS = streams used (1..4)
 static int cat_env(const char* k, int def) {
@@ -460,6 +462,7 @@ static int cat_env(const char* k, int def) {
   return v ? atoi(v) : def;
 }
 static int catalog_class_of(long n) {
+  if (hbk::wave_nr_for(n) == 128) return kCatClasses - 1;
   const int rc = (int)((n + 63) / 64);
   for (int c = 0; c < kCatClasses; ++c)
     if (rc <= kCatRcHi[c]) return c;
@@ -740,10 +743,15 @@ static int catalog_run(hb_catalog* c, const double* d_params, double* d_logl, hi
     const int cnt = c->class_off[cl + 1] - c->class_off[cl];
     int vpt = 1;
     while (vpt < kCatRcHi[cl]) vpt <<= 1;
+    int wpw = 1;
+    if (cl == kCatClasses - 1) {  // a pair of waves of <= 16 cadences per lane
+      vpt = 16;
+      wpw = 2;
+    }
     hipStream_t sj = (j % ns == 0) ? s : c->aux[j % ns - 1];
     HB_TRY(hbk::launch_eval_multi(vpt, c->class_slab[cl], c->d_t, c->d_ph, c->d_f, c->d_s, c->d_rows, c->d_tab, c->d_wt,
                                   c->d_list + c->class_off[cl], cnt, c->d_wc, d_logl, sj,
-                                  reinterpret_cast<double*>(reinterpret_cast<unsigned char*>(c->d_dq) + c->class_dq[cl])),
+                                  reinterpret_cast<double*>(reinterpret_cast<unsigned char*>(c->d_dq) + c->class_dq[cl]), wpw),
            "eval launch");
   }
   for (int i = 0; i < ns - 1; ++i) {

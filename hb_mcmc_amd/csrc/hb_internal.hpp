@@ -37,6 +37,7 @@ struct EvalPlan {
   long kth = 0;        // 0-based rank of the subtracted "median"
   int nw = 1;          // waves per walker
   int vpt = 0;         // >0: one-wave path, cadences per lane (register keys)
+  int wpw = 1;         // one-wave path: waves per walker (2: a pair, 1024 < n <= 2048)
   int bvpt = 0;        // >0: NW-wave path with register keys, cadences per thread
   size_t slab_bytes = 0;  // template slab / histogram bytes (one-wave path)
   bool lds = true;     // template in LDS (else HBM scratch slab)
@@ -99,17 +100,19 @@ hipError_t launch_prep(const double* d_params, int nwalk, const MagArgs& ma, hbd
                        int ntargets = 0, double* tab_pc = nullptr);
 // catalog mode: walkers list[0..count) of one size class (cadences per lane
 // vpt), each reading its target's slice through tab[wt[walker]]
+// (wpw = 2: a pair of waves per walker, vpt the cadences per lane of 128 rows)
 hipError_t launch_eval_multi(int vpt, size_t slab_bytes, const double* t, const double2* ph, const double* f,
                              const double* sg, const double* rows,
                              const TargetDesc* tab, const int* wt, const int* list, int count,
-                             const hbdev::WalkerConst* wc, double* logl, hipStream_t s, double* dq);
-int wave_vpt_for(long n);
+                             const hbdev::WalkerConst* wc, double* logl, hipStream_t s, double* dq, int wpw = 1);
+int wave_vpt_for(long n);  // cadences per lane of the one-wave path, 0 if n > 2048
+int wave_nr_for(long n);   // lane rows per walker: 64, or 128 (a pair of waves) for 1024 < n <= 2048
 // device bytes of the one-wave kernel's deferred cadence queue for `count`
 // walkers at `vpt` cadences per lane (the dq argument of launch_eval*)
-size_t wave_queue_bytes(int vpt, long count);  // cadences per lane of the one-wave path, 0 if n > 2048
+size_t wave_queue_bytes(int vpt, long count, int wpw = 1);
 size_t wave_slab_bytes(long n);
-size_t wave_lds_bytes(size_t slab, int vpt);
-// t, f, 1/sigma in the one-wave kernel's lane-row order (3 x 64 x ceil(n/64) doubles)
+size_t wave_lds_bytes(size_t slab, int vpt, int wpw = 1);
+// t, f, 1/sigma in the one-wave kernel's lane-row order (3 x nr x ceil(n/nr) doubles)
 long wave_rows_doubles(long n);
 void build_rows(const double* t, const double* f, const double* isg, long n, double* out);
 // acc (device sampler, one-wave path only): each wave also runs its slot's

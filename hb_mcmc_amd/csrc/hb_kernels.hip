@@ -359,9 +359,10 @@ struct Rows {
 __host__ __device__ __forceinline__ int rows_stride(int rc) {
   return (HB_ODD_STRIDE || (rc & (rc - 1)) != 0) ? (rc | 1) : rc;
 }
-__device__ __forceinline__ Rows make_rows(int n) {
+// nr lane rows per walker: 64 (one wave) or 128 (a pair of waves, WPW = 2)
+__device__ __forceinline__ Rows make_rows(int n, int nr = 64) {
   Rows r;
-  r.rc = (n + 63) >> 6;
+  r.rc = (n + nr - 1) / nr;
   r.stride = rows_stride(r.rc);
   r.swz = (!HB_ODD_STRIDE && (r.rc & (r.rc - 1)) == 0) ? r.rc - 1 : 0;
   r.rcp = 1.0f / (float)r.rc;
@@ -551,21 +552,23 @@ struct Pacer {
 // lanes of an iteration are neighbours in phase and the inline eclipse term
 // runs only on the few iterations that cross an eclipse.  Values are stored
 // at the lane-row slab positions (slab_pos_of) that the key load reads.
+// NT threads per walker (64, or 128 for a pair of waves), thread tid
+template <int NT = 64>
 __device__ __forceinline__ void model_pass_cold(const double* __restrict__ t, const double2* __restrict__ ph,
                                                 int n, const Rows& rw, const WalkerConst& w, double* vals,
                                                 int lane, Pacer pc, DeferQ& dq) {
   constexpr int K = HB_K;
   const bool tab = (ph != nullptr) && (w.tab != 0.0);  // walker-uniform
   const int last = n - 1;
-  const int nit = (n + K * 64 - 1) / (K * 64);
+  const int nit = (n + K * NT - 1) / (K * NT);
   pc.begin(nit);
-  for (int base = 0, it = 0; base < n; base += K * 64, ++it) {
+  for (int base = 0, it = 0; base < n; base += K * NT, ++it) {
     pc.step(it, nit);
     double tk[K], v[K];
     double2 pk[K];
 #pragma unroll
     for (int k = 0; k < K; ++k) {
-      const int i = min(base + k * 64 + lane, last);
+      const int i = min(base + k * NT + lane, last);
       tk[k] = t[i];
       pk[k] = tab ? ph[i] : make_double2(0.0, 1.0);
     }
@@ -578,7 +581,7 @@ __device__ __forceinline__ void model_pass_cold(const double* __restrict__ t, co
     hb_cadence_poly_k<K>(tk, pk, tab, w, v, dd, zz, bad);
 #pragma unroll
     for (int k = 0; k < K; ++k) {
-      const int i = base + k * 64 + lane;
+      const int i = base + k * NT + lane;
       const int sp = slab_pos_of(rw, i);
       if (i < n) vals[sp] = v[k];
       const bool need = (!bad) & eclipse_lane(w, dd[k], zz[k]);
@@ -594,7 +597,7 @@ __device__ __forceinline__ void model_pass_cold(const double* __restrict__ t, co
     }
 #pragma unroll
     for (int k = 0; k < K; ++k) {
-      const int i = base + k * 64 + lane;
+      const int i = base + k * NT + lane;
       if (i < n) vals[slab_pos_of(rw, i)] = v[k];
     }
 #endif
@@ -604,10 +607,12 @@ __device__ __forceinline__ void model_pass_cold(const double* __restrict__ t, co
 // tT: the light curve's times in lane-row order (tT[c * 64 + l] = t[l * rc + c],
 // build_rows), so the step-c loads of the 64 lanes are one coalesced 512-B
 // request instead of 64 strided ones
-template <int VPT>
+// NR: lane rows of the walker (the arrays' pitch: 64, or 128 for a pair of
+// waves, each passing tT offset by its first row); row: this lane's row
+template <int VPT, int NR = 64>
 __device__ __forceinline__ void model_pass_chain(const double* __restrict__ tT, const double2* __restrict__ ph,
                                                  int n, const Rows& rw, const WalkerConst& w, double* vals,
-                                                 double* eq_dr, int* eq_code, int lane, Pacer pc, DeferQ& dq
+                                                 double* eq_dr, int* eq_code, int lane, int row, Pacer pc, DeferQ& dq
 #ifdef HB_CLK_STEP0
                                                  , unsigned long long& clk_step0
 #endif
@@ -616,8 +621,8 @@ __device__ __forceinline__ void model_pass_chain(const double* __restrict__ tT, 
   const int lc = (rw.rc + KC - 1) / KC;  // chain length (wave-uniform)
   const bool tab = (ph != nullptr) && (w.tab != 0.0);  // walker-uniform
   const int last = n - 1;
-  const int base = lane * rw.rc;
-  const int rs = lane * rw.stride, lsw = HB_ODD_STRIDE ? 0 : (lane & rw.swz);  // slab_pos = rs + (c ^ lsw)
+  const int base = row * rw.rc;
+  const int rs = row * rw.stride, lsw = HB_ODD_STRIDE ? 0 : (row & rw.swz);  // slab_pos = rs + (c ^ lsw)
 #if !HB_GQ
   const uint64_t lt_mask = (1ull << lane) - 1ull;
   int qn = 0;  // queued eclipse cadences (wave-uniform)
@@ -625,7 +630,7 @@ __device__ __forceinline__ void model_pass_chain(const double* __restrict__ tT, 
   ChainState<KC> st;
   double tk[KC];
 #pragma unroll
-  for (int k = 0; k < KC; ++k) tk[k] = tT[min(k * lc, rw.rc - 1) * 64 + lane];
+  for (int k = 0; k < KC; ++k) tk[k] = tT[min(k * lc, rw.rc - 1) * NR + lane];
   pc.begin(lc);
   for (int j = 0; j < lc; ++j) {
     pc.step(j, lc);
@@ -647,7 +652,7 @@ __device__ __forceinline__ void model_pass_chain(const double* __restrict__ tT, 
 #endif
     double tn[KC];
 #pragma unroll
-    for (int k = 0; k < KC; ++k) tn[k] = tT[min(k * lc + j + 1, rw.rc - 1) * 64 + lane];
+    for (int k = 0; k < KC; ++k) tn[k] = tT[min(k * lc + j + 1, rw.rc - 1) * NR + lane];
     double v[KC], dd[KC], zz[KC];
     bool bad;
 #if HB_SPLIT_LIVE
@@ -1320,6 +1325,103 @@ __device__ __forceinline__ double wave_select3(const uint64_t (&key)[VPT], uint3
   const int who = __builtin_amdgcn_readfirstlane(__ffsll((long long)hit) - 1);
   return oval(readlane_u64(mine, who));
 }
+// ---------------------------------------------------------------------------
+// A pair of waves per walker (WPW = 2: N = 1025..2048).  One wave per walker
+// would need 32 cadences per lane, whose 17-KB slab leaves LDS for 9 waves per
+// CU; two waves of 16 cadences per lane each hold half of the walker's rows.
+// The model pass, the deferred eclipse terms and the key loads stay per wave
+// (each lane owns its row); the select's histograms, the survivors and the
+// chi^2 halves are shared through LDS with workgroup barriers.  Both waves
+// run the same bin picks on the same histogram, so every decision is uniform
+// over the pair.
+// ---------------------------------------------------------------------------
+struct PairShared {
+  uint32_t hmn[2], hmx[2];  // per wave: min / max key high words
+  double chi[2];            // per wave: chi^2 partial
+  uint32_t ncand;           // survivor counter
+  uint32_t pad[3];
+};
+static_assert(sizeof(PairShared) % 16 == 0, "LDS carve must stay 16-B aligned");
+
+template <int VPT, int B, bool TEST>
+__device__ __forceinline__ void pair_pass(const uint64_t (&key)[VPT], uint32_t* hist, int lane, int& hi,
+                                          int& pshift, uint64_t& prefix, uint32_t& kk, uint32_t& cnt) {
+  static_assert(!TEST || (4 << B) + 256 <= (4 << kSelBits), "the TEST pass dummies fit in the slab");
+  constexpr int PER = (1 << B) / 64, Q = PER / 4;
+  const int width = hi + 1 < B ? hi + 1 : B;
+  const int shift = hi + 1 - width;
+  const uint32_t dm = (1u << width) - 1u;
+  uint4* h4 = reinterpret_cast<uint4*>(hist);
+  if (threadIdx.x < 64) {  // wave 0 clears, wave 1 waits at the barrier
+#pragma unroll
+    for (int q = 0; q < Q; ++q) h4[lane * Q + q] = make_uint4(0u, 0u, 0u, 0u);
+  }
+  __syncthreads();
+  const uint32_t dummy = (1u << B) + (uint32_t)lane;
+  if (shift >= 32) select3_hist<VPT, TEST, true, true>(key, hist, pshift, prefix, shift, dm, dummy);
+  else if (!TEST || pshift >= 32) select3_hist<VPT, TEST, true, false>(key, hist, pshift, prefix, shift, dm, dummy);
+  else select3_hist<VPT, TEST, false, false>(key, hist, pshift, prefix, shift, dm, dummy);
+  __syncthreads();
+  uint32_t bin, before;
+  wave_pick_bin<B>(hist, lane, kk, bin, before, cnt);  // both waves: the same pick
+  kk -= before;
+  prefix |= (uint64_t)bin << shift;
+  pshift = shift;
+  hi = shift - 1;
+  __syncthreads();  // histogram reads done before the next clear
+}
+template <int VPT, bool HT>
+__device__ __forceinline__ void pair_compact(const uint64_t (&key)[VPT], uint64_t* cand, PairShared* ps, int pshift,
+                                             uint64_t prefix) {
+  uint32_t mine = 0;
+#pragma unroll
+  for (int v = 0; v < VPT; ++v) mine += key_match<HT>(key[v], pshift, prefix) ? 1u : 0u;
+  uint32_t tot = mine;  // the wave's survivors, then one LDS atomic for its base
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) tot += (uint32_t)__shfl_xor((int)tot, off, 64);
+  uint32_t basec = 0;
+  if ((threadIdx.x & 63) == 0) basec = atomicAdd(&ps->ncand, tot);
+  basec = (uint32_t)__builtin_amdgcn_readfirstlane((int)__shfl((int)basec, 0, 64));
+#pragma unroll
+  for (int v = 0; v < VPT; ++v) {
+    const bool m = key_match<HT>(key[v], pshift, prefix);
+    const unsigned long long bal = wave_ballot(m);
+    if (m) {
+      const uint32_t pos = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, basec));
+      cand[pos] = key[v];
+    }
+    basec += (uint32_t)__popcll(bal);
+  }
+}
+// k-th smallest key (0-based) over the pair; hmin/hmax: the pair's min / max
+// high words.  ps->ncand is zero on entry (set before the caller's barrier).
+template <int VPT>
+__device__ __forceinline__ double pair_select3(const uint64_t (&key)[VPT], uint32_t kth, uint32_t hmin, uint32_t hmax,
+                                               uint32_t* hist, uint64_t* cand, PairShared* ps) {
+  const int lane = threadIdx.x & 63;
+  const uint64_t kmin = (uint64_t)hmin << 32, kmax = ((uint64_t)hmax << 32) | 0xffffffffull;
+  int hi = 63 - __builtin_clzll(kmin ^ kmax);  // >= 31
+  uint64_t prefix = hi == 63 ? 0ull : (kmin & ~((2ull << hi) - 1ull));
+  int pshift = hi + 1;
+  uint32_t kk = kth, cnt = 0;
+  pair_pass<VPT, kSelBits, false>(key, hist, lane, hi, pshift, prefix, kk, cnt);
+  while (cnt > (uint32_t)kCandMax && hi >= 0) pair_pass<VPT, kSelBits2, true>(key, hist, lane, hi, pshift, prefix, kk, cnt);
+  if (hi < 0) return oval(prefix);
+  if (pshift >= 32) pair_compact<VPT, true>(key, cand, ps, pshift, prefix);
+  else pair_compact<VPT, false>(key, cand, ps, pshift, prefix);
+  __syncthreads();
+  const uint32_t nc = cnt;  // == ps->ncand
+  const uint64_t mine = (uint32_t)lane < nc ? cand[lane] : ~0ull;
+  uint32_t r = 0;
+  for (uint32_t j = 0; j < nc; ++j) {
+    const uint64_t o = cand[j];
+    r += (o < mine) | ((o == mine) & (j < (uint32_t)lane));
+  }
+  const unsigned long long hit = wave_ballot((uint32_t)lane < nc && r == kk);
+  const int who = __builtin_amdgcn_readfirstlane(__ffsll((long long)hit) - 1);
+  return oval(readlane_u64(mine, who));
+}
+
 // keys of this lane's row (slot v: cadence lane rc + v; slots v >= lim are
 // padding ~0) and the lane's min / max key high words over its live slots
 template <int VPT, bool FULL>
@@ -1353,7 +1455,7 @@ __device__ __forceinline__ void load_keys3(const double* vals, const Rows& rw, i
 }
 // chi^2 partial of this lane (the reference's per-cadence operations,
 // likelihood3.c:679-685 and :822-832) or, mode 1, the template values
-template <int VPT, bool FULL>
+template <int VPT, bool FULL, int NR = 64>
 __device__ __forceinline__ double chi2_keys3(const uint64_t (&key)[VPT], double med, const WalkerConst& w,
                                              const double* __restrict__ fT, const double* __restrict__ iT,
                                              const Rows& rw, int lane, int lim) {
@@ -1366,8 +1468,8 @@ __device__ __forceinline__ double chi2_keys3(const uint64_t (&key)[VPT], double 
 #pragma unroll
     for (int u = 0; u < kCh; ++u) {  // row block vc (wave-uniform) + lane: scalar base, lane offset
       const int vc = FULL ? v0 + u : (v0 + u < rw.rc ? v0 + u : rw.rc - 1);
-      fv[u] = (fT + vc * 64)[lane];
-      iv[u] = (iT + vc * 64)[lane];
+      fv[u] = (fT + vc * NR)[lane];
+      iv[u] = (iT + vc * NR)[lane];
     }
 #pragma unroll
     for (int u = 0; u < kCh; ++u) {
@@ -1409,16 +1511,23 @@ __device__ __forceinline__ bool key_live(const Rows& r, int v, int lane, long n)
 // WPB > 1: WPB walkers (one wave each) per workgroup; a wave's LDS is its
 // lds_per-byte slice.  The waves only meet at the progress-word barrier of
 // the pacer (HB_PRIO == 2); everything else syncs per wave (HB_WSYNC).
-template <int VPT, bool MULTI, bool ACC = false, int WPB = 1>
-__global__ __launch_bounds__(64 * WPB) HB_WPE_ATTR void hb_eval_wave_kernel(
+// WPW = 2: a pair of waves per walker (N = 1025..2048, see PairShared): wave h
+// owns lane rows 64 h .. 64 h + 63 of 128; VPT is then the cadences per lane
+// of the pair's rows (<= 16).
+template <int VPT, bool MULTI, bool ACC = false, int WPB = 1, int WPW = 1>
+__global__ __launch_bounds__(64 * WPB * WPW) HB_WPE_ATTR void hb_eval_wave_kernel(
     const double* __restrict__ t, const double2* __restrict__ ph, const double* __restrict__ f,
     const double* __restrict__ isg, const double* __restrict__ rows,
     long n, long kth, const WalkerConst* __restrict__ wcs, double* __restrict__ logl,
     double* __restrict__ tmpl_out, int mode, int slab_bytes, double gap, const TargetDesc* __restrict__ tab,
     const int* __restrict__ wt, const int* __restrict__ list, hbds::AccArgs hst, int count, int lds_per,
     double* __restrict__ dqbuf) {
+  static_assert(WPW == 1 || (WPW == 2 && WPB == 1 && !ACC && HB_SEL_V == 3 && HB_GQ), "pair: plain batched path");
+  constexpr int NR = 64 * WPW;  // lane rows per walker
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_all[];
   const int lane = threadIdx.x & 63;
+  const int h = WPW > 1 ? __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) : 0;  // wave of the pair
+  const int row = h * 64 + lane;
   const int wib = WPB > 1 ? __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) : 0;
   const int slot = (int)blockIdx.x * WPB + wib;
   const bool valid = WPB == 1 || slot < count;
@@ -1480,7 +1589,7 @@ __global__ __launch_bounds__(64 * WPB) HB_WPE_ATTR void hb_eval_wave_kernel(
 #endif
   };
   if (roche_exit) {  // likelihood3.c:866-869, see hb_eval_kernel
-    if (lane == 0) logl[wv] = -kBig / 2.0;
+    if (row == 0) logl[wv] = -kBig / 2.0;
     if (ACC) acc_tail(-kBig / 2.0);
     HB_CLK_END(wv);
     return;
@@ -1488,12 +1597,15 @@ __global__ __launch_bounds__(64 * WPB) HB_WPE_ATTR void hb_eval_wave_kernel(
 
   uint64_t kmn, kmx;
   uint64_t key[VPT];
-  const Rows rw = make_rows((int)n);
-  const double* __restrict__ fT = rows + 64 * rw.rc;   // f and 1/sigma in lane-row order
-  const double* __restrict__ iT = rows + 128 * rw.rc;
+  const Rows rw = make_rows((int)n, NR);
+  // t, f and 1/sigma in lane-row order (pitch NR), from this wave's first row
+  const double* __restrict__ tT = rows + h * 64;
+  const double* __restrict__ fT = rows + NR * rw.rc + h * 64;
+  const double* __restrict__ iT = rows + 2 * NR * rw.rc + h * 64;
+  PairShared* ps = reinterpret_cast<PairShared*>(smem + slab_bytes + 8 * kCandMax);  // WPW == 2 only
   DeferQ dq{nullptr, 0};
   if (HB_GQ) {  // this wave's region of the deferred queue (64 VPT entries of 16 B)
-    dq.e = reinterpret_cast<char*>(dqbuf) + (size_t)slot * (size_t)(64 * VPT * 16);
+    dq.e = reinterpret_cast<char*>(dqbuf) + ((size_t)slot * WPW + (size_t)h) * (size_t)(64 * VPT * 16);
     __asm__ volatile("" : "+v"(dq.e));  // a VGPR pair, not one more scalar to spill
   }
   {
@@ -1501,13 +1613,13 @@ __global__ __launch_bounds__(64 * WPB) HB_WPE_ATTR void hb_eval_wave_kernel(
       // the eclipse queue shares the select's candidate area (dead until the select)
       double* eq_dr = reinterpret_cast<double*>(smem + slab_bytes);
       int* eq_code = reinterpret_cast<int*>(eq_dr + kEclQ + 1);
-      model_pass_chain<VPT>(rows, ph, (int)n, rw, w, vals, eq_dr, eq_code, lane, pc, dq
+      model_pass_chain<VPT, NR>(tT, ph, (int)n, rw, w, vals, eq_dr, eq_code, lane, row, pc, dq
 #ifdef HB_CLK_STEP0
                             , clkm_[3]
 #endif
                             );
     } else {
-      model_pass_cold(t, ph, (int)n, rw, w, vals, lane, pc, dq);
+      model_pass_cold<NR>(t, ph, (int)n, rw, w, vals, row, pc, dq);
     }
   }
 #if HB_GQ
@@ -1515,7 +1627,11 @@ __global__ __launch_bounds__(64 * WPB) HB_WPE_ATTR void hb_eval_wave_kernel(
   HB_CLK_MARK(3);
 #endif
   HB_WSYNC();  // the slab values of every lane are in place
+  // a pair's cold pass writes cadences of either wave's rows, and its queued
+  // eclipse terms land there too: the pair meets before and after them
+  if (WPW > 1) __syncthreads();
   dq_apply(w, vals, dq, t, rw, (int)n, lane);
+  if (WPW > 1) __syncthreads();
 #endif
   HB_CLK_MARK(0);
 #if HB_PRIO == 2
@@ -1528,16 +1644,27 @@ __global__ __launch_bounds__(64 * WPB) HB_WPE_ATTR void hb_eval_wave_kernel(
 #if HB_SEL_V == 3
   {
     // live key slots of this lane; a light curve of 64 VPT cadences fills every row
-    const int lim = min(rw.rc, max(0, (int)n - lane * rw.rc));
-    const bool full = (rw.rc == VPT) && (n == 64L * VPT);  // wave-uniform
+    const int lim = min(rw.rc, max(0, (int)n - row * rw.rc));
+    const bool full = (rw.rc == VPT) && (n == (long)NR * VPT);  // wave-uniform
     uint32_t hmn, hmx;
-    if (full) load_keys3<VPT, true>(vals, rw, lane, lim, key, hmn, hmx);
-    else load_keys3<VPT, false>(vals, rw, lane, lim, key, hmn, hmx);
+    if (full) load_keys3<VPT, true>(vals, rw, row, lim, key, hmn, hmx);
+    else load_keys3<VPT, false>(vals, rw, row, lim, key, hmn, hmx);
     hmn = wave_reduce_u32(hmn, OpMinU32());
     hmx = wave_reduce_u32(hmx, OpMaxU32());
+    if (WPW > 1) {  // the pair's bracket; both waves' keys are loaded before the slab turns histogram
+      if (lane == 0) {
+        ps->hmn[h] = hmn;
+        ps->hmx[h] = hmx;
+        if (h == 0) ps->ncand = 0u;
+      }
+      __syncthreads();
+      hmn = min(ps->hmn[0], ps->hmn[1]);
+      hmx = max(ps->hmx[0], ps->hmx[1]);
+    }
     HB_CLK_MARK(1);
     HB_WSYNC();  // the slab becomes the histogram
-    const double med = wave_select3<VPT>(key, (uint32_t)kth, hmn, hmx, hist, cand);
+    const double med = WPW > 1 ? pair_select3<VPT>(key, (uint32_t)kth, hmn, hmx, hist, cand, ps)
+                               : wave_select3<VPT>(key, (uint32_t)kth, hmn, hmx, hist, cand);
     HB_CLK_MARK(2);
     if (mode == 1) {
       const double blend = w.blend, one_m_blend = 1.0 - w.blend, tune = w.tune;
@@ -1546,18 +1673,23 @@ __global__ __launch_bounds__(64 * WPB) HB_WPE_ATTR void hb_eval_wave_kernel(
       for (int v = 0; v < VPT; ++v) {
         if (v < lim) {
           const double m = (oval(key[v]) - med) + 1.0;
-          o[key_index(rw, v, lane)] = (blend + m * one_m_blend) * tune;
+          o[key_index(rw, v, row)] = (blend + m * one_m_blend) * tune;
         }
       }
       HB_CLK_END(wv);
       return;
     }
-    const double acc = full ? chi2_keys3<VPT, true>(key, med, w, fT, iT, rw, lane, lim)
-                            : chi2_keys3<VPT, false>(key, med, w, fT, iT, rw, lane, lim);
-    const double chi2 = wave_sum_dpp(acc);
+    const double acc = full ? chi2_keys3<VPT, true, NR>(key, med, w, fT, iT, rw, lane, lim)
+                            : chi2_keys3<VPT, false, NR>(key, med, w, fT, iT, rw, lane, lim);
+    double chi2 = wave_sum_dpp(acc);
+    if (WPW > 1) {  // the halves in a fixed order
+      if (lane == 0) ps->chi[h] = chi2;
+      __syncthreads();
+      chi2 = ps->chi[0] + ps->chi[1];
+    }
     double c = chi2 + w.chi2_extra;
     if (w.roche != 0.0) c = kBig;
-    if (lane == 0) logl[wv] = -c / 2.0;
+    if (row == 0) logl[wv] = -c / 2.0;
     if (ACC) acc_tail(-c / 2.0);  // c is wave-uniform (readlanes)
     HB_CLK_END(wv);
     return;
@@ -2074,13 +2206,13 @@ int wave_wpb(int count, size_t lds_per) {
   return wpb < 1 ? 1 : wpb;
 }
 
-template <int VPT, bool MULTI, bool ACC, int WPB>
+template <int VPT, bool MULTI, bool ACC, int WPB, int WPW = 1>
 static hipError_t launch_wave_g(size_t lds_per, int count, hipStream_t s, const double* t, const double2* ph,
                                 const double* f, const double* sg, const double* rows, long n, long kth, const WalkerConst* wc,
                                 double* logl, double* tmpl, int mode, size_t slab, double gap,
                                 const TargetDesc* tab, const int* wt, const int* list,
                                 const hbds::AccArgs& acc, double* dq) {
-  auto kern = hb_eval_wave_kernel<VPT, MULTI, ACC, WPB>;
+  auto kern = hb_eval_wave_kernel<VPT, MULTI, ACC, WPB, WPW>;
   const size_t lds = (size_t)WPB * lds_per + (WPB > 1 ? 64 : 0);
   static bool attr_set = false;  // per instantiation; benign race (idempotent)
   if (!attr_set && lds > 65536) {
@@ -2089,17 +2221,20 @@ static hipError_t launch_wave_g(size_t lds_per, int count, hipStream_t s, const 
     if (e != hipSuccess) return e;
     attr_set = true;
   }
-  hipLaunchKernelGGL(kern, dim3((count + WPB - 1) / WPB), dim3(64 * WPB), lds, s, t, ph, f, sg, rows, n, kth, wc, logl,
+  hipLaunchKernelGGL(kern, dim3((count + WPB - 1) / WPB), dim3(64 * WPB * WPW), lds, s, t, ph, f, sg, rows, n, kth, wc, logl,
                      tmpl, mode, (int)slab, gap, tab, wt, list, acc, count, (int)lds_per, dq);
   return hipGetLastError();
 }
 
-template <int VPT, bool MULTI, bool ACC>
+template <int VPT, bool MULTI, bool ACC, int WPW = 1>
 static hipError_t launch_wave_w(size_t slab, int count, hipStream_t s, const double* t, const double2* ph,
                                 const double* f, const double* sg, const double* rows, long n, long kth, const WalkerConst* wc,
                                 double* logl, double* tmpl, int mode, double gap, const TargetDesc* tab,
                                 const int* wt, const int* list, const hbds::AccArgs& acc, double* dq) {
-  const size_t per = wave_lds_bytes(slab, VPT);
+  const size_t per = wave_lds_bytes(slab, VPT, WPW);
+  if constexpr (WPW > 1)  // a pair of waves per walker: one walker per workgroup
+    return launch_wave_g<VPT, MULTI, ACC, 1, WPW>(per, count, s, t, ph, f, sg, rows, n, kth, wc, logl, tmpl, mode,
+                                                  slab, gap, tab, wt, list, acc, dq);
   switch (wave_wpb(count, per)) {
 #if HB_WPB_MAX >= 16
     case 16:
@@ -2122,6 +2257,10 @@ static hipError_t launch_wave_t(const EvalPlan& pl, const double* t, const doubl
                                 const double* sg, const double* rows,
                                 const WalkerConst* wc, int nwalk, double* logl, double* tmpl, int mode,
                                 hipStream_t s, double* dq) {
+  if constexpr (VPT == 16)
+    if (pl.wpw == 2)
+      return launch_wave_w<VPT, false, false, 2>(pl.slab_bytes, nwalk, s, t, ph, f, sg, rows, pl.n, pl.kth, wc, logl,
+                                                 tmpl, mode, pl.gap, nullptr, nullptr, nullptr, hbds::AccArgs{}, dq);
   return launch_wave_w<VPT, false, false>(pl.slab_bytes, nwalk, s, t, ph, f, sg, rows, pl.n, pl.kth, wc, logl, tmpl,
                                           mode, pl.gap, nullptr, nullptr, nullptr, hbds::AccArgs{}, dq);
 }
@@ -2138,7 +2277,12 @@ template <int VPT>
 static hipError_t launch_multi_t(size_t slab, const double* t, const double2* ph, const double* f,
                                  const double* sg, const double* rows,
                                  const TargetDesc* tab, const int* wt, const int* list, int count,
-                                 const WalkerConst* wc, double* logl, hipStream_t s, double* dq) {
+                                 const WalkerConst* wc, double* logl, hipStream_t s, double* dq, int wpw) {
+  if constexpr (VPT == 16)
+    if (wpw == 2)
+      return launch_wave_w<VPT, true, false, 2>(slab, count, s, t, ph, f, sg, rows, 0L, 0L, wc, logl, nullptr, 0, 0.0,
+                                                tab, wt, list, hbds::AccArgs{}, dq);
+  if (wpw != 1) return hipErrorInvalidValue;
   return launch_wave_w<VPT, true, false>(slab, count, s, t, ph, f, sg, rows, 0L, 0L, wc, logl, nullptr, 0, 0.0, tab, wt,
                                          list, hbds::AccArgs{}, dq);
 }
@@ -2146,15 +2290,15 @@ static hipError_t launch_multi_t(size_t slab, const double* t, const double2* ph
 hipError_t launch_eval_multi(int vpt, size_t slab, const double* t, const double2* ph, const double* f,
                              const double* sg, const double* rows,
                              const TargetDesc* tab, const int* wt, const int* list, int count,
-                             const WalkerConst* wc, double* logl, hipStream_t s, double* dq) {
+                             const WalkerConst* wc, double* logl, hipStream_t s, double* dq, int wpw) {
   if (count <= 0) return hipSuccess;
   switch (vpt) {
-    case 1: return launch_multi_t<1>(slab, t, ph, f, sg, rows, tab, wt, list, count, wc, logl, s, dq);
-    case 2: return launch_multi_t<2>(slab, t, ph, f, sg, rows, tab, wt, list, count, wc, logl, s, dq);
-    case 4: return launch_multi_t<4>(slab, t, ph, f, sg, rows, tab, wt, list, count, wc, logl, s, dq);
-    case 8: return launch_multi_t<8>(slab, t, ph, f, sg, rows, tab, wt, list, count, wc, logl, s, dq);
-    case 16: return launch_multi_t<16>(slab, t, ph, f, sg, rows, tab, wt, list, count, wc, logl, s, dq);
-    case 32: return launch_multi_t<32>(slab, t, ph, f, sg, rows, tab, wt, list, count, wc, logl, s, dq);
+    case 1: return launch_multi_t<1>(slab, t, ph, f, sg, rows, tab, wt, list, count, wc, logl, s, dq, wpw);
+    case 2: return launch_multi_t<2>(slab, t, ph, f, sg, rows, tab, wt, list, count, wc, logl, s, dq, wpw);
+    case 4: return launch_multi_t<4>(slab, t, ph, f, sg, rows, tab, wt, list, count, wc, logl, s, dq, wpw);
+    case 8: return launch_multi_t<8>(slab, t, ph, f, sg, rows, tab, wt, list, count, wc, logl, s, dq, wpw);
+    case 16: return launch_multi_t<16>(slab, t, ph, f, sg, rows, tab, wt, list, count, wc, logl, s, dq, wpw);
+    case 32: return launch_multi_t<32>(slab, t, ph, f, sg, rows, tab, wt, list, count, wc, logl, s, dq, wpw);
     default: return hipErrorInvalidValue;
   }
 }
@@ -2166,6 +2310,7 @@ hipError_t launch_eval(const EvalPlan& pl, const double* t, const double2* ph, c
   if (pl.vpt > 0 && HB_GQ && dq == nullptr) return hipErrorInvalidValue;  // the one-wave path's deferred queue
   if (acc != nullptr) {  // fused Hastings epilogue: one-wave path only
     if (mode != 0) return hipErrorInvalidValue;
+    if (pl.wpw != 1) return hipErrorNotSupported;
     switch (pl.vpt) {
       case 1: return launch_wave_acc_t<1>(pl, t, ph, f, sg, rows, wc, nwalk, logl, s, *acc, dq);
       case 2: return launch_wave_acc_t<2>(pl, t, ph, f, sg, rows, wc, nwalk, logl, s, *acc, dq);
@@ -2261,46 +2406,66 @@ hipError_t preload_code_object() {
   return hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&hb_prep_kernel));
 }
 
+// lane rows per walker: 128 (a pair of waves, WPW = 2) for 1280 < n <= 2048,
+// else 64.  At 4096 walkers the pair takes N = 1500 / 1861 / 2048 in 64 / 72 /
+// 73 us instead of 72 / 88 / 88, and loses at N = 1100 (61 vs 55 us: chains
+// of 5 cadences per lane), so short rows stay one wave.  HB_NO_PAIR=1 (A/B
+// knob): one wave of 32 cadences per lane up to 2048.
+constexpr long kPairNmin = 64 * 20 + 1;
+int wave_nr_for(long n) {
+  static const bool no_pair = getenv("HB_NO_PAIR") != nullptr && atoi(getenv("HB_NO_PAIR")) != 0;
+  return (n >= kPairNmin && n <= 64 * 32 && !no_pair) ? 128 : 64;
+}
+
+// cadences per lane (a power of two) of the one-wave path, 0 if n > 2048
 int wave_vpt_for(long n) {
   if (n > 64 * 32) return 0;
+  const long nr = wave_nr_for(n);
   int vpt = 1;
-  while ((long)vpt * 64 < n) vpt <<= 1;
+  while ((long)vpt * nr < n) vpt <<= 1;
   return vpt;
 }
 
-// the template slab (64 lane rows of VPT doubles) doubles as the
+// the template slab (nr lane rows of VPT doubles) doubles as the
 // 2^kSelBits-bin histogram of the select
 size_t wave_slab_bytes(long n) {
-  const size_t vals = (size_t)64 * rows_stride((int)((n + 63) / 64)) * 8;
+  const long nr = wave_nr_for(n);
+  const size_t vals = (size_t)nr * rows_stride((int)((n + nr - 1) / nr)) * 8;
   const size_t slab = vals > (size_t)(4u << kSelBits) ? vals : (size_t)(4u << kSelBits);
   return (slab + 15) & ~(size_t)15;
 }
 
-// bytes of the one-wave kernel's deferred queue for `count` waves (HB_GQ)
-size_t wave_queue_bytes(int vpt, long count) {
-  return HB_GQ ? (size_t)count * (size_t)64 * (size_t)vpt * 16 : 0;
+// bytes of the one-wave kernel's deferred queue for `count` walkers of wpw
+// waves (HB_GQ)
+size_t wave_queue_bytes(int vpt, long count, int wpw) {
+  return HB_GQ ? (size_t)count * (size_t)wpw * (size_t)64 * (size_t)vpt * 16 : 0;
 }
 
-// slab | select candidates | eclipse queue (chain model pass only)
-size_t wave_lds_bytes(size_t slab, int vpt) {
+// slab | select candidates | eclipse queue (chain model pass only) | the
+// pair's shared words (wpw = 2)
+size_t wave_lds_bytes(size_t slab, int vpt, int wpw) {
   const bool chain = vpt >= HB_CHAIN_VPT_MIN && vpt <= HB_CHAIN_VPT_MAX;
   const size_t q = (chain && !HB_GQ) ? (size_t)(kEclQ + 1) * (8 + 4) : 0;  // eclipse queue aliases the candidates
   const size_t cb = 8 * (size_t)kCandMax;
-  return (slab + (q > cb ? q : cb) + 15) & ~(size_t)15;
+  return (slab + (q > cb ? q : cb) + (wpw > 1 ? sizeof(PairShared) : 0) + 15) & ~(size_t)15;
 }
 
 // t, f and 1/sigma in the one-wave kernel's lane-row order: row block c holds
-// cadence l * rc + c for lanes l = 0..63 (rc = ceil(n / 64); cadences past the
-// end repeat the last one and are never used)
-long wave_rows_doubles(long n) { return 3L * 64L * ((n + 63) / 64); }
+// cadence l * rc + c for lane rows l = 0..nr-1 (nr = wave_nr_for(n), rc =
+// ceil(n / nr); cadences past the end repeat the last one and are never used)
+long wave_rows_doubles(long n) {
+  const long nr = wave_nr_for(n);
+  return 3L * nr * ((n + nr - 1) / nr);
+}
 void build_rows(const double* t, const double* f, const double* isg, long n, double* out) {
-  const long rc = (n + 63) / 64;
+  const long nr = wave_nr_for(n);
+  const long rc = (n + nr - 1) / nr;
   for (long c = 0; c < rc; ++c)
-    for (long l = 0; l < 64; ++l) {
+    for (long l = 0; l < nr; ++l) {
       const long i = std::min(l * rc + c, n - 1);
-      out[c * 64 + l] = t[i];
-      out[64 * rc + c * 64 + l] = f[i];
-      out[128 * rc + c * 64 + l] = isg[i];
+      out[c * nr + l] = t[i];
+      out[nr * rc + c * nr + l] = f[i];
+      out[2 * nr * rc + c * nr + l] = isg[i];
     }
 }
 
@@ -2319,12 +2484,13 @@ EvalPlan make_plan(long n) {
   pl.n = n;
   pl.kth = (n % 2 == 0) ? n / 2 : n / 2 + 1;  // likelihood3.c:97-99
   static const long wave_max = getenv("HB_WAVE_NMAX") ? atol(getenv("HB_WAVE_NMAX")) : 64 * 32;  // A/B knob
-  if (n <= wave_max && n <= 64 * 32) {  // one wave per walker, keys in registers
+  if (n <= wave_max && n <= 64 * 32) {  // one wave (or a pair) per walker, keys in registers
     pl.vpt = wave_vpt_for(n);
+    pl.wpw = wave_nr_for(n) / 64;
     pl.nw = 1;
     pl.lds = true;
     pl.slab_bytes = wave_slab_bytes(n);
-    pl.lds_bytes = wave_lds_bytes(pl.slab_bytes, pl.vpt);
+    pl.lds_bytes = wave_lds_bytes(pl.slab_bytes, pl.vpt, pl.wpw);
     return pl;
   }
   return make_block_plan(n);
