@@ -195,6 +195,31 @@ def test_block_kernel_sizes(hbmi, oracle, n):
     assert (np.abs(tm - ref) <= tol).all()
 
 
+@pytest.mark.parametrize("n", [1280, 1281, 1500, 2047, 2048])
+def test_pair_plan_sizes(hbmi, oracle, n):
+    """N = 1281..2048 runs a pair of waves per walker (1280 is
+    the last one-wave size): templates and logL against the oracle, with
+    walkers on the cold Kepler path (e = 0.9: the pair's cold pass writes
+    cadences of either wave's rows) and Roche walkers; and every walker's logL
+    bit-identical when the batch is evaluated again in reversed order (the
+    pair's LDS hand-overs are race-free)."""
+    from hb_mcmc_amd import synth
+    from hb_mcmc_amd.likelihood import HBLikelihood
+
+    t, f, s = synth.dataset(n, oracle.light_curve)
+    P = synth.walkers(64, seed=n)
+    P[::4, 3] = 0.9  # cold path
+    with HBLikelihood(t, f, s) as L:
+        assert L.eval_kernel == "hb_eval_wave_kernel"
+        ll = L.loglike(P)
+        rev = L.loglike(P[::-1].copy())[::-1]
+        tm = L.light_curve(P)
+    assert np.array_equal(ll, rev, equal_nan=True)
+    close_logl(ll, oracle.loglike_batch(t, f, s, P, synth.MAG_DEFAULT, synth.MAGERR_DEFAULT, 8))
+    ref = oracle.light_curve_batch(t, P, 8)
+    assert (np.abs(tm - ref) <= lc_tol(P[:, 3], ref)).all()
+
+
 @pytest.mark.parametrize("latency", [True, False], ids=["small-batch-plan", "one-wave-plan"])
 @pytest.mark.parametrize("n", [1024, 6001])
 def test_phase_table_and_direct_paths(hbmi, oracle, n, latency):
