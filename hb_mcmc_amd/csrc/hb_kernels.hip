@@ -347,6 +347,9 @@ __device__ __forceinline__ void model_pass(const double* __restrict__ t, const d
 #ifndef HB_KC
 #define HB_KC 2  // chains per lane
 #endif
+#ifndef HB_PAIR_KC
+#define HB_PAIR_KC HB_KC  // experiment knob: Kepler chains per lane in the pair kernel
+#endif
 #ifndef HB_ODD_STRIDE
 #define HB_ODD_STRIDE 1  // 0: power-of-two rows stored at c ^ (lane mod rc) (stride rc)
 #endif
@@ -617,7 +620,8 @@ __device__ __forceinline__ void model_pass_chain(const double* __restrict__ tT, 
                                                  , unsigned long long& clk_step0
 #endif
                                                  ) {
-  constexpr int KC = VPT < HB_KC ? VPT : HB_KC;
+  constexpr int KCM = NR > 64 ? HB_PAIR_KC : HB_KC;
+  constexpr int KC = VPT < KCM ? VPT : KCM;
   const int lc = (rw.rc + KC - 1) / KC;  // chain length (wave-uniform)
   const bool tab = (ph != nullptr) && (w.tab != 0.0);  // walker-uniform
   const int last = n - 1;
@@ -2257,7 +2261,7 @@ static hipError_t launch_wave_t(const EvalPlan& pl, const double* t, const doubl
                                 const double* sg, const double* rows,
                                 const WalkerConst* wc, int nwalk, double* logl, double* tmpl, int mode,
                                 hipStream_t s, double* dq) {
-  if constexpr (VPT == 16)
+  if constexpr (VPT == 16 || VPT == 8)
     if (pl.wpw == 2)
       return launch_wave_w<VPT, false, false, 2>(pl.slab_bytes, nwalk, s, t, ph, f, sg, rows, pl.n, pl.kth, wc, logl,
                                                  tmpl, mode, pl.gap, nullptr, nullptr, nullptr, hbds::AccArgs{}, dq);
@@ -2278,7 +2282,7 @@ static hipError_t launch_multi_t(size_t slab, const double* t, const double2* ph
                                  const double* sg, const double* rows,
                                  const TargetDesc* tab, const int* wt, const int* list, int count,
                                  const WalkerConst* wc, double* logl, hipStream_t s, double* dq, int wpw) {
-  if constexpr (VPT == 16)
+  if constexpr (VPT == 16 || VPT == 8)
     if (wpw == 2)
       return launch_wave_w<VPT, true, false, 2>(slab, count, s, t, ph, f, sg, rows, 0L, 0L, wc, logl, nullptr, 0, 0.0,
                                                 tab, wt, list, hbds::AccArgs{}, dq);
@@ -2411,7 +2415,10 @@ hipError_t preload_code_object() {
 // 73 us instead of 72 / 88 / 88, and loses at N = 1100 (61 vs 55 us: chains
 // of 5 cadences per lane), so short rows stay one wave.  HB_NO_PAIR=1 (A/B
 // knob): one wave of 32 cadences per lane up to 2048.
-constexpr long kPairNmin = 64 * 20 + 1;
+#ifndef HB_PAIR_NMIN
+#define HB_PAIR_NMIN (64 * 20 + 1)  // experiment knob: smallest N of the pair plan
+#endif
+constexpr long kPairNmin = HB_PAIR_NMIN;
 int wave_nr_for(long n) {
   static const bool no_pair = getenv("HB_NO_PAIR") != nullptr && atoi(getenv("HB_NO_PAIR")) != 0;
   return (n >= kPairNmin && n <= 64 * 32 && !no_pair) ? 128 : 64;
