@@ -113,9 +113,12 @@ namespace hbk {
 #ifndef HB_PREP_W
 #define HB_PREP_W 16
 #endif
-constexpr int kPrepWalkers = HB_PREP_W;  // walkers per prep workgroup
+constexpr int kPrepWalkers = HB_PREP_W;  // walkers per prep workgroup (small batches)
 constexpr int kPrepThreads = 64 * kPrepRoles;
 
+// NW walkers per workgroup: kPrepWalkers, or 32 / 64 for batches that still
+// fill 256 workgroups with them (C4, C5: one round instead of two or four)
+template <int NW>
 __global__ __launch_bounds__(kPrepThreads) void hb_prep_kernel(const double* __restrict__ params,
                                                               int nwalk, MagArgs ma,
                                                               WalkerConst* __restrict__ out,
@@ -125,6 +128,7 @@ __global__ __launch_bounds__(kPrepThreads) void hb_prep_kernel(const double* __r
                                                               double2* __restrict__ ph,
                                                               const int* __restrict__ w0, int ntargets,
                                                               double* __restrict__ tab_pc_out) {
+  constexpr int kPrepWalkers = NW;
   __shared__ PrepShared<kPrepWalkers> L;
   const int G = (int)gridDim.x;
   const int tid = threadIdx.x;
@@ -2155,8 +2159,12 @@ hipError_t launch_prep(const double* d_params, int nwalk, const MagArgs& ma, Wal
                        double2* ph, const int* w0, int ntargets, double* tab_pc) {
   if (nwalk <= 0) return hipSuccess;
   if (t == nullptr || (tab != nullptr && w0 == nullptr) || !HB_PHASE_TAB) ph = nullptr;
-  const int nb = (nwalk + kPrepWalkers - 1) / kPrepWalkers;
-  hipLaunchKernelGGL(hb_prep_kernel, dim3(nb), dim3(kPrepThreads), 0, s, d_params, nwalk, ma, d_wc, tab, wt, t,
+  // the most walkers per workgroup that still leave >= 256 workgroups (one per CU)
+  static const int wmax = getenv("HB_PREP_WMAX") ? atoi(getenv("HB_PREP_WMAX")) : 64;  // A/B knob
+  const int nw = (wmax >= 64 && nwalk >= 256 * 64) ? 64 : (wmax >= 32 && nwalk >= 256 * 32) ? 32 : kPrepWalkers;
+  const int nb = (nwalk + nw - 1) / nw;
+  auto kern = nw == 64 ? hb_prep_kernel<64> : nw == 32 ? hb_prep_kernel<32> : hb_prep_kernel<kPrepWalkers>;
+  hipLaunchKernelGGL(kern, dim3(nb), dim3(kPrepThreads), 0, s, d_params, nwalk, ma, d_wc, tab, wt, t,
                      (int)n, ph, w0, ntargets, tab_pc);
   return hipGetLastError();
 }
@@ -2407,7 +2415,7 @@ hipError_t launch_median(double* d_a, long n, long kth, hipStream_t s) {
 // Choose waves-per-walker and template storage for N cadences.
 hipError_t preload_code_object() {
   hipFuncAttributes a;
-  return hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&hb_prep_kernel));
+  return hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&hb_prep_kernel<kPrepWalkers>));
 }
 
 // lane rows per walker: 128 (a pair of waves, WPW = 2) for 1280 < n <= 2048,

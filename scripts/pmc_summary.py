@@ -45,7 +45,9 @@ def is_eval(r):
     return "hb_eval_wave_kernel<" in k and ", true," in k
 
 
-prep_grid = ((walkers + 15) // 16) * 256  # hb_prep_kernel: 16 walkers per 256-thread workgroup (HB_PREP_W)
+# hb_prep_kernel: 64 / 32 / 16 walkers per 256-thread workgroup (hbk::launch_prep: the most that leave >= 256 groups)
+_pw = 64 if walkers >= 256 * 64 else 32 if walkers >= 256 * 32 else 16
+prep_grid = ((walkers + _pw - 1) // _pw) * 256
 ev = collections.defaultdict(float)
 calls = collections.Counter()
 disp = collections.defaultdict(set)
