@@ -19,7 +19,7 @@ i.e. 8192 walkers per GPU (weak scaling: 8192 x N global).
 
 Rank 0 prints ONE JSON line.  `value` = evals over all ranks / max-over-ranks
 wall time of the K timed steps.  `roofline` prices the dominant kernel
-(hb_eval_wave_kernel at N <= 2048, else hb_eval_block_kernel) with algorithmic bytes B(N) = 24 N + 176 per eval (SURVEY.md
+(hb_eval_wave_kernel: one wave per walker at N <= 1280, 2 / 4 waves of lane rows up to 4096; else hb_eval_block_kernel) with algorithmic bytes B(N) = 24 N + 176 per eval (SURVEY.md
 8(d)) over its HIP-event-timed duration; `cpu_baseline` times the reference
 likelihood3.c (oracle/_ref, else the oracle port) on the host cores on a
 bounded sample of the same workload.

@@ -362,7 +362,9 @@ struct Rows {
   int stride;  // row stride [doubles]
   int swz;     // XOR swizzle mask (HB_ODD_STRIDE == 0, power-of-two rc: rc - 1; else 0)
   float rcp;   // 1 / rc (row of cadence i, i < 2^11: exact after rounding)
+  int live;    // rows holding cadences: ceil(n / rc) (the rows kernel stores no others)
 };
+constexpr long kRowsLdsCap = 163840 - 2048;  // the rows kernel's slab, below its candidates and shared words
 __host__ __device__ __forceinline__ int rows_stride(int rc) {
   return (HB_ODD_STRIDE || (rc & (rc - 1)) != 0) ? (rc | 1) : rc;
 }
@@ -371,6 +373,9 @@ __device__ __forceinline__ Rows make_rows(int n, int nr = 64) {
   Rows r;
   r.rc = (n + nr - 1) / nr;
   r.stride = rows_stride(r.rc);
+  r.live = (n + r.rc - 1) / r.rc;
+  // many rows (the rows kernel, nr > 128): the odd pad only while the live rows fit the LDS
+  if (nr > 128 && (long)r.live * r.stride * 8 > kRowsLdsCap) r.stride = r.rc;
   r.swz = (!HB_ODD_STRIDE && (r.rc & (r.rc - 1)) == 0) ? r.rc - 1 : 0;
   r.rcp = 1.0f / (float)r.rc;
   return r;
@@ -690,11 +695,13 @@ __device__ __forceinline__ void model_pass_chain(const double* __restrict__ tT, 
     for (int k = 0; k < KC; ++k) {
       const int c = k * lc + j;
       if (c < rw.rc) {  // wave-uniform: the last chain may run past the row end
-        // cadences past n (the last row's padding) store harmless values: their keys are masked
+        // cadences past n (the last row's padding) store harmless values: their keys are masked;
+        // the rows kernel (NR > 128) sizes its slab to the live rows and stores no others
         const int sp = rs + (c ^ lsw);
-        vals[sp] = v[k];
+        const bool live = NR <= 128 || row < rw.live;
+        if (live) vals[sp] = v[k];
         const bool need = (!bad) & eclipse_lane(w, dd[k], zz[k]);
-        dq_push(dq, bad | need, copysign(dd[k], zz[k]), sp | (bad ? kSlowFlag : 0));
+        dq_push(dq, live & (bad | need), copysign(dd[k], zz[k]), sp | (bad ? kSlowFlag : 0));
       }
       tk[k] = tn[k];
     }
@@ -1343,10 +1350,11 @@ __device__ __forceinline__ double wave_select3(const uint64_t (&key)[VPT], uint3
 // run the same bin picks on the same histogram, so every decision is uniform
 // over the pair.
 // ---------------------------------------------------------------------------
+constexpr int kMaxWPW = 16;
 struct PairShared {
-  uint32_t hmn[2], hmx[2];  // per wave: min / max key high words
-  double chi[2];            // per wave: chi^2 partial
-  uint32_t ncand;           // survivor counter
+  uint32_t hmn[kMaxWPW], hmx[kMaxWPW];  // per wave: min / max key high words
+  double chi[kMaxWPW];                  // per wave: chi^2 partial
+  uint32_t ncand;                       // survivor counter
   uint32_t pad[3];
 };
 static_assert(sizeof(PairShared) % 16 == 0, "LDS carve must stay 16-B aligned");
@@ -1530,7 +1538,7 @@ __global__ __launch_bounds__(64 * WPB * WPW) HB_WPE_ATTR void hb_eval_wave_kerne
     double* __restrict__ tmpl_out, int mode, int slab_bytes, double gap, const TargetDesc* __restrict__ tab,
     const int* __restrict__ wt, const int* __restrict__ list, hbds::AccArgs hst, int count, int lds_per,
     double* __restrict__ dqbuf) {
-  static_assert(WPW == 1 || (WPW == 2 && WPB == 1 && !ACC && HB_SEL_V == 3 && HB_GQ), "pair: plain batched path");
+  static_assert(WPW == 1 || (WPW <= kMaxWPW && WPB == 1 && !ACC && HB_SEL_V == 3 && HB_GQ), "pair/rows: plain batched path");
   constexpr int NR = 64 * WPW;  // lane rows per walker
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_all[];
   const int lane = threadIdx.x & 63;
@@ -1659,15 +1667,20 @@ __global__ __launch_bounds__(64 * WPB * WPW) HB_WPE_ATTR void hb_eval_wave_kerne
     else load_keys3<VPT, false>(vals, rw, row, lim, key, hmn, hmx);
     hmn = wave_reduce_u32(hmn, OpMinU32());
     hmx = wave_reduce_u32(hmx, OpMaxU32());
-    if (WPW > 1) {  // the pair's bracket; both waves' keys are loaded before the slab turns histogram
+    if (WPW > 1) {  // the walker's bracket; every wave's keys are loaded before the slab turns histogram
       if (lane == 0) {
         ps->hmn[h] = hmn;
         ps->hmx[h] = hmx;
         if (h == 0) ps->ncand = 0u;
       }
       __syncthreads();
-      hmn = min(ps->hmn[0], ps->hmn[1]);
-      hmx = max(ps->hmx[0], ps->hmx[1]);
+      hmn = ps->hmn[0];
+      hmx = ps->hmx[0];
+#pragma unroll
+      for (int q = 1; q < WPW; ++q) {
+        hmn = min(hmn, ps->hmn[q]);
+        hmx = max(hmx, ps->hmx[q]);
+      }
     }
     HB_CLK_MARK(1);
     HB_WSYNC();  // the slab becomes the histogram
@@ -1690,10 +1703,12 @@ __global__ __launch_bounds__(64 * WPB * WPW) HB_WPE_ATTR void hb_eval_wave_kerne
     const double acc = full ? chi2_keys3<VPT, true, NR>(key, med, w, fT, iT, rw, lane, lim)
                             : chi2_keys3<VPT, false, NR>(key, med, w, fT, iT, rw, lane, lim);
     double chi2 = wave_sum_dpp(acc);
-    if (WPW > 1) {  // the halves in a fixed order
+    if (WPW > 1) {  // the waves' partials in a fixed order
       if (lane == 0) ps->chi[h] = chi2;
       __syncthreads();
-      chi2 = ps->chi[0] + ps->chi[1];
+      chi2 = ps->chi[0];
+#pragma unroll
+      for (int q = 1; q < WPW; ++q) chi2 += ps->chi[q];
     }
     double c = chi2 + w.chi2_extra;
     if (w.roche != 0.0) c = kBig;
@@ -2269,10 +2284,23 @@ static hipError_t launch_wave_t(const EvalPlan& pl, const double* t, const doubl
                                 const double* sg, const double* rows,
                                 const WalkerConst* wc, int nwalk, double* logl, double* tmpl, int mode,
                                 hipStream_t s, double* dq) {
-  if constexpr (VPT == 16 || VPT == 8)
-    if (pl.wpw == 2)
-      return launch_wave_w<VPT, false, false, 2>(pl.slab_bytes, nwalk, s, t, ph, f, sg, rows, pl.n, pl.kth, wc, logl,
-                                                 tmpl, mode, pl.gap, nullptr, nullptr, nullptr, hbds::AccArgs{}, dq);
+#define HB_WPW_CASE(WV)                                                                                      \
+  if (pl.wpw == WV)                                                                                          \
+    return launch_wave_w<VPT, false, false, WV>(pl.slab_bytes, nwalk, s, t, ph, f, sg, rows, pl.n, pl.kth, wc, logl, \
+                                                tmpl, mode, pl.gap, nullptr, nullptr, nullptr, hbds::AccArgs{}, dq);
+  if constexpr (VPT == 16 || VPT == 8) {
+    HB_WPW_CASE(2)
+  }
+  if constexpr (VPT == 16) {
+    HB_WPW_CASE(4)
+    HB_WPW_CASE(8)
+    HB_WPW_CASE(16)
+  }
+  if constexpr (VPT == 32) {
+    HB_WPW_CASE(16)
+  }
+#undef HB_WPW_CASE
+  if (pl.wpw != 1) return hipErrorInvalidValue;
   return launch_wave_w<VPT, false, false>(pl.slab_bytes, nwalk, s, t, ph, f, sg, rows, pl.n, pl.kth, wc, logl, tmpl,
                                           mode, pl.gap, nullptr, nullptr, nullptr, hbds::AccArgs{}, dq);
 }
@@ -2427,15 +2455,29 @@ hipError_t preload_code_object() {
 #define HB_PAIR_NMIN (64 * 20 + 1)  // experiment knob: smallest N of the pair plan
 #endif
 constexpr long kPairNmin = HB_PAIR_NMIN;
+//
+// Above 2048 cadences the same code runs with WPW = 4 waves of lane rows per
+// walker (the rows kernel: 256 rows of <= 16 cadences, warm Kepler chains)
+// up to N = 4096, where it beats the block kernel (4096 walkers, HIP events:
+// N = 3000 127 vs 130 us, N = 4001 145 vs 159); above, the block kernel is
+// faster (8192: 329 vs 305; 20 000 with 16 waves of rows: 1179 vs 890 --
+// the rows' deferred eclipse queue goes through HBM, the block kernel's
+// eclipse terms stay in LDS), so 0 = no rows plan there.  (8 / 16 waves of
+// rows remain instantiable for experiments.)  HB_NO_ROWS=1 (A/B knob): the
+// block kernel above 2048.
+constexpr long kRowsNmax = 64 * 4 * 16;
 int wave_nr_for(long n) {
   static const bool no_pair = getenv("HB_NO_PAIR") != nullptr && atoi(getenv("HB_NO_PAIR")) != 0;
-  return (n >= kPairNmin && n <= 64 * 32 && !no_pair) ? 128 : 64;
+  static const bool no_rows = getenv("HB_NO_ROWS") != nullptr && atoi(getenv("HB_NO_ROWS")) != 0;
+  if (n <= 64 * 32) return (n >= kPairNmin && !no_pair) ? 128 : 64;
+  if (no_rows || n > kRowsNmax) return 0;
+  return 256;
 }
 
 // cadences per lane (a power of two) of the one-wave path, 0 if n > 2048
 int wave_vpt_for(long n) {
-  if (n > 64 * 32) return 0;
   const long nr = wave_nr_for(n);
+  if (nr == 0) return 0;
   int vpt = 1;
   while ((long)vpt * nr < n) vpt <<= 1;
   return vpt;
@@ -2445,7 +2487,11 @@ int wave_vpt_for(long n) {
 // 2^kSelBits-bin histogram of the select
 size_t wave_slab_bytes(long n) {
   const long nr = wave_nr_for(n);
-  const size_t vals = (size_t)nr * rows_stride((int)((n + nr - 1) / nr)) * 8;
+  const int rc = (int)((n + nr - 1) / nr);
+  const long live = (n + rc - 1) / rc;
+  int stride = rows_stride(rc);
+  if (nr > 128 && live * stride * 8 > kRowsLdsCap) stride = rc;  // as make_rows
+  const size_t vals = (size_t)(nr > 128 ? live : nr) * stride * 8;
   const size_t slab = vals > (size_t)(4u << kSelBits) ? vals : (size_t)(4u << kSelBits);
   return (slab + 15) & ~(size_t)15;
 }
@@ -2499,10 +2545,10 @@ EvalPlan make_plan(long n) {
   pl.n = n;
   pl.kth = (n % 2 == 0) ? n / 2 : n / 2 + 1;  // likelihood3.c:97-99
   static const long wave_max = getenv("HB_WAVE_NMAX") ? atol(getenv("HB_WAVE_NMAX")) : 64 * 32;  // A/B knob
-  if (n <= wave_max && n <= 64 * 32) {  // one wave (or a pair) per walker, keys in registers
+  if ((n <= wave_max || n > 64 * 32) && wave_nr_for(n) > 0) {  // one wave (or 2..16) per walker, keys in registers
     pl.vpt = wave_vpt_for(n);
     pl.wpw = wave_nr_for(n) / 64;
-    pl.nw = 1;
+    pl.nw = pl.wpw;  // waves per walker (hb_ctx_waves_per_walker)
     pl.lds = true;
     pl.slab_bytes = wave_slab_bytes(n);
     pl.lds_bytes = wave_lds_bytes(pl.slab_bytes, pl.vpt, pl.wpw);

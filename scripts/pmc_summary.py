@@ -4,8 +4,8 @@
 
 Reads gpurun_out/pmc_TAG/*/run_counter_collection.csv (separate --pmc passes
 over `bench.py`, scripts/pmc.sh), keeps the dispatches of the timed workload
-(C2/C4: hb_eval_wave_kernel over 64 x WALKERS threads; C3: the largest
-hb_eval_block_kernel; C5: the catalog's hb_eval_wave_kernel<.., true, ..>
+(C2/C4: hb_eval_wave_kernel over 64 x WALKERS threads; C3: the eval kernel
+dispatch with the largest grid (the 16-wave rows kernel); C5: the catalog's hb_eval_wave_kernel<.., true, ..>
 classes, summed per call = per hb_prep_kernel over all walkers) and writes
 
   profiles/TAG_pmc_CONFIG.json        per-call counters + derived figures
@@ -40,8 +40,8 @@ def is_eval(r):
     k = r["Kernel_Name"]
     if config in ("C2", "C4"):
         return "hb_eval_wave_kernel<" in k and int(r["Grid_Size"]) == 64 * walkers
-    if config == "C3":
-        return "hb_eval_block_kernel<" in k
+    if config == "C3":  # the rows kernel (hb_eval_wave_kernel<.., WPW = 16>) or, HB_NO_ROWS=1, the block kernel
+        return "hb_eval_block_kernel<" in k or "hb_eval_wave_kernel<" in k
     return "hb_eval_wave_kernel<" in k and ", true," in k
 
 
@@ -52,7 +52,7 @@ ev = collections.defaultdict(float)
 calls = collections.Counter()
 disp = collections.defaultdict(set)
 if config == "C3":  # only the workload's (largest) block-kernel dispatches
-    gmax = max(int(r["Grid_Size"]) for r in rows if "hb_eval_block_kernel<" in r["Kernel_Name"])
+    gmax = max(int(r["Grid_Size"]) for r in rows if is_eval(r))
 for r in rows:
     c = r["Counter_Name"]
     if "hb_prep_kernel" in r["Kernel_Name"] and int(r["Grid_Size"]) == prep_grid:

@@ -176,19 +176,23 @@ def test_n20000_lds_tiled_path(hbmi):
     assert (np.abs(tm.sum(1) - g["tsum"]) <= 20000 * tol[:, 0]).all()
 
 
-@pytest.mark.parametrize("n", [2049, 4001, 6001, 8192, 12000])
+@pytest.mark.parametrize("n", [2049, 3000, 4001, 4096, 4097, 6001, 8192, 12000])
 def test_block_kernel_sizes(hbmi, oracle, n):
-    """Register-key block kernel across its (waves, keys-per-thread) classes,
-    odd and even N (median rank likelihood3.c:97-101), templates and logL."""
+    """N = 2049..4096: the rows kernel (4 waves of lane rows per walker);
+    above, the register-key block kernel across its (waves, keys-per-thread)
+    classes.  Odd and even N (median rank likelihood3.c:97-101), templates
+    and logL; each walker bit-identical when the batch is reversed."""
     from hb_mcmc_amd import synth
     from hb_mcmc_amd.likelihood import HBLikelihood
 
     t, f, s = synth.dataset(n, oracle.light_curve)
     P = synth.walkers(8, seed=n)
     with HBLikelihood(t, f, s) as L:
-        assert L.eval_kernel == "hb_eval_block_kernel"
+        assert L.eval_kernel == ("hb_eval_wave_kernel" if n <= 4096 else "hb_eval_block_kernel")
         ll = L.loglike(P)
+        rev = L.loglike(P[::-1].copy())[::-1]
         tm = L.light_curve(P)
+    assert np.array_equal(ll, rev, equal_nan=True)
     close_logl(ll, oracle.loglike_batch(t, f, s, P, synth.MAG_DEFAULT, synth.MAGERR_DEFAULT, 8))
     ref = oracle.light_curve_batch(t, P, 8)
     tol = lc_tol(P[:, 3])[:, None]
