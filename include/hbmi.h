@@ -160,9 +160,11 @@ int hb_light_curve_batch(hb_ctx *ctx, const double *params, int W, double *out, 
  * whether the template lives in LDS (1) or in an HBM scratch slab (0). */
 int hb_ctx_waves_per_walker(const hb_ctx *ctx);
 int hb_ctx_template_in_lds(const hb_ctx *ctx);
-/* Eval kernel the context launches: 0 hb_eval_wave_kernel (N <= 2048, one wave
- * per walker), 1 hb_eval_block_kernel (register keys, N <= 32 x 64 x waves),
- * 2 hb_eval_kernel (LDS-walking select; template in LDS or an HBM slab). */
+/* Eval kernel the context launches: 0 hb_eval_wave_kernel (lane rows: one wave
+ * per walker up to N = 1280, a pair up to 2048, four waves up to 4096; see
+ * hb_ctx_waves_per_walker), 1 hb_eval_block_kernel (register keys, N <= 32 x
+ * 64 x waves), 2 hb_eval_kernel (LDS-walking select; template in LDS or an
+ * HBM slab). */
 int hb_ctx_eval_kind(const hb_ctx *ctx);
 /* on != 0: batches of fewer than 512 walkers (N <= 2048) run the multi-wave
  * kernel (several waves per walker: lower latency when most SIMDs would sit
