@@ -928,6 +928,11 @@ struct hb_dsampler {
   std::condition_variable scv;
   std::vector<std::thread> workers;
   bool stop = false;
+  // sticky failure: a producer could not reuse its ring slot, or an iteration
+  // failed after its schedule was consumed (the device state is then partly
+  // advanced): every later step / download returns this error (under smu)
+  bool failed = false;
+  std::string fail_msg;
   long long q_prod = 0, q_cons = 0, q_synced = 0;  // produced / consumed / skipped on the host stream
   uint32_t base_w[31] = {};                         // the swap stream at creation (hb_lagfib.hpp window)
   size_t sched_cap = 0;                             // bytes per ring slot
@@ -981,6 +986,38 @@ struct hb_dsampler {
 };
 
 static int ds_upload(hb_dsampler* d, const int* chain_of_slot);
+
+// Puts the sampler into its sticky failed state (first message wins) and
+// wakes every waiter (producers and a ds_begin waiting for a schedule).
+static void ds_mark_failed(hb_dsampler* d, const std::string& msg) {
+  {
+    std::lock_guard<std::mutex> lk(d->smu);
+    if (!d->failed) {
+      d->failed = true;
+      d->fail_msg = msg;
+    }
+  }
+  d->scv.notify_all();
+}
+// the failed state as an error return (0 if the sampler is healthy)
+static int ds_check_failed(hb_dsampler* d, const char* where) {
+  std::string m;
+  {
+    std::lock_guard<std::mutex> lk(d->smu);
+    if (!d->failed) return 0;
+    m = std::string(where) + ": the sampler failed earlier (" + d->fail_msg + "); destroy it";
+  }
+  return hbx_set_error(m.c_str());
+}
+// Marks the sampler failed unless disarmed: every return path of an iteration
+// after its schedule was consumed (DS_TRY returns included).
+struct DsFailGuard {
+  hb_dsampler* d;
+  bool armed = true;
+  ~DsFailGuard() {
+    if (armed) ds_mark_failed(d, std::string("an iteration failed after its schedule was consumed: ") + hb_last_error());
+  }
+};
 
 // Builds iteration q's swap schedule into ring slot `slot`: the 2W draws of
 // ptmcmc (:791, :810) from the stream jumped to 2 W q draws past creation,
@@ -1103,13 +1140,13 @@ static void sched_worker(hb_dsampler* d) {
     {
       std::unique_lock<std::mutex> lk(d->smu);
       d->scv.wait(lk, [&] {
-        if (d->stop) return true;
+        if (d->stop || d->failed) return true;
         const hb_dsampler::Slot& sl = d->slots[d->q_prod % K];
         if (sl.q < 0) return true;
         const long long q_rec = (sl.q / d->ev_every) * d->ev_every + d->ev_every - 1;  // next recorded event
         return sl.q == d->q_prod - K && sl.released && d->q_issued > q_rec;
       });
-      if (d->stop) return;
+      if (d->stop || d->failed) return;
       q = d->q_prod++;
       slot = (int)(q % K);
       reused = d->slots[slot].q >= 0;
@@ -1117,7 +1154,13 @@ static void sched_worker(hb_dsampler* d) {
       d->slots[slot] = hb_dsampler::Slot{};
       d->slots[slot].q = q;
     }
-    if (reused && hipEventSynchronize(d->ev_used[ev_slot]) != hipSuccess) return;  // the GPU is done with it
+    if (reused) {  // the GPU is done with the slot's previous schedule
+      const hipError_t e = hipEventSynchronize(d->ev_used[ev_slot]);
+      if (e != hipSuccess) {  // e.g. after a GPU fault: fail the sampler, do not leave ds_begin waiting
+        ds_mark_failed(d, std::string("schedule producer: hipEventSynchronize: ") + hipGetErrorString(e));
+        return;
+      }
+    }
     const double t0 = now_s();
     sched_build(d, q, slot, sc);
     const double dt = now_s() - t0;
@@ -1217,7 +1260,19 @@ static hb_dsampler* ds_create(hb_sampler* s, hb_ctx* ctx, const int* chain_of_sl
     const char* fp = getenv("HB_DS_FUSED_PREP");
     d->fused_prep = fp ? atoi(fp) != 0 : d->nl <= 16 * cus;
   }
-  if (const char* ee = getenv("HB_DS_EV_EVERY")) d->ev_every = std::max(1, atoi(ee));  // experiment knob
+  if (const char* ee = getenv("HB_DS_EV_EVERY")) {  // experiment knob
+    // a producer reuses ring slot q % R_RING once the event after iteration
+    // ceil((q+1)/ev_every) ev_every - 1 completed: that iteration must not need
+    // the slot being reused (ev_every <= R_RING), and the events must land on
+    // fixed slots (R_RING % ev_every == 0)
+    const int ev = atoi(ee);
+    if (ev < 1 || ev > hb_dsampler::R_RING || hb_dsampler::R_RING % ev != 0) {
+      hbx_set_error("hb_dsampler_create: HB_DS_EV_EVERY must divide the schedule ring size (8)");
+      delete d;
+      return nullptr;
+    }
+    d->ev_every = ev;
+  }
   // swap segments of <= kSegSlots owned slots; an attempt is listed for at
   // most min(G, 3 + 2 kMaxLevels / (smallest segment)) segments
   d->nseg = std::max(1, (d->nl + kSegSlots - 1) / kSegSlots);
@@ -1375,6 +1430,7 @@ static int ds_drain_events(hb_dsampler* d);
 
 extern "C" int hb_dsampler_download(hb_dsampler* d) {
   if (!d) return hbx_set_error("hb_dsampler_download: null");
+  if (const int rc = ds_check_failed(d, "hb_dsampler_download")) return rc;
   const HbSamplerView& v = d->v;
   const int nl = d->nl;
   const size_t Nz = (size_t)nl;
@@ -1520,6 +1576,7 @@ static long ds_begin(hb_dsampler* d, long iter, double* send, long cap) {
   const Dev& D = d->D;
   hipStream_t s = d->st;
   if (d->cur_iter >= 0) return hbx_set_error("hb_dsampler: step_begin twice without step_end");
+  if (const int rc = ds_check_failed(d, "hb_dsampler_step")) return rc;
   DS_TRY(hipSetDevice(d->device), "hipSetDevice");
   const double tw0 = now_s();
   const long long q = d->q_cons;
@@ -1527,10 +1584,14 @@ static long ds_begin(hb_dsampler* d, long iter, double* send, long cap) {
   hb_dsampler::Slot sl;
   {
     std::unique_lock<std::mutex> lk(d->smu);
-    d->scv.wait(lk, [&] { return d->slots[slot].q == q && d->slots[slot].ready; });
+    d->scv.wait(lk, [&] { return d->failed || (d->slots[slot].q == q && d->slots[slot].ready); });
     sl = d->slots[slot];
   }
-  d->q_cons = q + 1;
+  if (const int rc = ds_check_failed(d, "hb_dsampler_step")) return rc;  // a producer failed
+  // from here on the iteration's schedule is consumed: any failure leaves the
+  // device state partly advanced, so it is sticky (DsFailGuard); q_cons
+  // advances only when the iteration's swaps are enqueued (ds_end)
+  DsFailGuard guard{d};
   const double tw1 = now_s();
   if (sl.overflow)
     return hbx_set_error("hb_dsampler: an iteration's swap schedule exceeds its buffer (more than 64 levels)");
@@ -1610,6 +1671,7 @@ static long ds_begin(hb_dsampler* d, long iter, double* send, long cap) {
   d->cur_n = n;
   d->t_wait += tw1 - tw0;
   d->t_issue += now_s() - tw1;
+  guard.armed = false;
   return n;
 }
 
@@ -1619,7 +1681,11 @@ static int ds_end(hb_dsampler* d, long iter, const double* recv, long n) {
   const int W = d->W;
   const Dev& D = d->D;
   hipStream_t s = d->st;
+  if (const int rc = ds_check_failed(d, "hb_dsampler_step_end")) return rc;
   if (d->cur_iter != iter) return hbx_set_error("hb_dsampler_step_end: no step_begin for this iteration");
+  // the iteration's proposals and likelihood are enqueued: failing from here
+  // on is sticky, like the second half of ds_begin
+  DsFailGuard guard{d};
   if (d->xchg && (!recv || n != d->cur_n))
     return hbx_set_error("hb_dsampler_step_end: gathered buffer missing or of the wrong size");
   const double t0 = now_s();
@@ -1656,6 +1722,8 @@ static int ds_end(hb_dsampler* d, long iter, const double* recv, long n) {
     d->slots[slot].released = true;
     d->q_issued = sl.q + 1;
   }
+  d->q_cons = sl.q + 1;  // the iteration's swap draws are now on the stream
+  guard.armed = false;
   d->scv.notify_all();
   d->t_issue += now_s() - t0;
   if (d->P.log_on && iter > 10000 && iter % 100 == 0) return ds_drain_events(d);

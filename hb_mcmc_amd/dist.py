@@ -136,6 +136,9 @@ def run_sharded(t, flux, sigma, niter, run_id, log10_period, run=0, nchains=50, 
             if out_root:
                 writer = Writer(out_root, run_id, run, W)
                 writer.attach(S)  # big-jump log lines of rank 0's slots (the reference logs slots 0-5)
+        # whether any rank prints or writes: the periodic gathers run only then
+        # (one collective here, so the flag is the same on every rank)
+        report = comm.allreduce_sum([1.0 if (verbose or out_root) else 0.0])[0] > 0
         t_start = time.perf_counter()
         dst = np.arange(W)
         for it in range(int(niter)):
@@ -166,9 +169,9 @@ def run_sharded(t, flux, sigma, niter, run_id, log10_period, run=0, nchains=50, 
             if r == 0 and Lp[0] > logLmap:  # :565-572
                 xmap = S.get()[0][0].copy()
                 logLmap = float(Lp[0])
-            # collectives at fixed iterations on every rank (not keyed to a
-            # rank's own verbose / out_root, which only select what rank 0 does)
-            if it % 1000 == 0:  # :575-589 (counters summed over ranks)
+            # collectives at fixed iterations on every rank, and only when some
+            # rank reports (`report`, agreed once over the ranks)
+            if report and it % 1000 == 0:  # :575-589 (counters summed over ranks)
                 st = S.stats()
                 acc, de_acc, de_trial = comm.allreduce_sum([st["acc"], st["DEacc"], st["DEtrial"]])
                 x_all = comm.gather_rows(S.get()[0], counts)
@@ -179,7 +182,7 @@ def run_sharded(t, flux, sigma, niter, run_id, log10_period, run=0, nchains=50, 
                             np.float64(de_acc) / np.float64(de_trial)))
                     print("Parameter values: ")
                     print("".join("%f\t" % v for v in x_all[min(10, W - 1), :5]))
-            if it % 100 == 0:  # :593-649
+            if report and it % 100 == 0:  # :593-649
                 x_all = comm.gather_rows(S.get()[0], counts)
                 if out_root and r == 0:
                     writer.step(it, Lp, x_all)
@@ -239,6 +242,8 @@ def run_sharded_device(t, flux, sigma, niter, run_id, log10_period, run=0, nchai
             writer.attach(S)  # big-jump log lines of rank 0's slots (the reference logs slots 0-5)
         D = ShardedDeviceSampler(S, gpu, group)
         D.init_logl()
+        # whether any rank prints or writes: the periodic gathers run only then
+        report = comm.allreduce_sum([1.0 if (verbose or out_root) else 0.0])[0] > 0
         if r == 0 and verbose:
             _, _, _, lmap, _ = D.gather()
             print("initial chi2 and likelihood %f \t %f" % (-2 * lmap, lmap))
@@ -246,10 +251,10 @@ def run_sharded_device(t, flux, sigma, niter, run_id, log10_period, run=0, nchai
         model = (lambda p: gpu.light_curve(p[None, :])[0])
         for it in range(int(niter)):
             D.step(it)
-            # collective cadence fixed by the iteration number alone (every
-            # rank calls the same collectives whatever its own verbose /
-            # out_root); the flags only decide what rank 0 prints or writes
-            if it % 100 != 0:
+            # collective cadence fixed by the iteration number and `report`
+            # (agreed once over the ranks), so every rank calls the same
+            # collectives; a run that prints and writes nothing gathers nothing
+            if not report or it % 100 != 0:
                 continue
             show = verbose and it % 1000 == 0
             write = bool(out_root)
