@@ -2,8 +2,10 @@
 
 Workload (BASELINE.json configs[1]): a synthetic
 1024-cadence heartbeat-binary light curve, 4096 walkers per GPU.  One "step"
-= one batched log-likelihood over the rank's walkers (two launches: per-walker
-constants + the one-wave-per-walker model/median/chi^2 kernel), followed,
+= one batched log-likelihood over the rank's walkers (hb_loglik_batch_dev:
+ONE launch at C2, the per-walker constants computed in the prologue of the
+one-wave-per-walker model/median/chi^2 kernel; two launches, constants then
+that kernel, beyond 16 walkers per CU as at C4), followed,
 when N > 1, by the RCCL all-gather of every walker's logL (what the tempering
 swap of mcmc_wrapper2.c:554-563 needs).  Inputs are resident in HBM before the
 timed region; the walker batches rotate over 4 pre-generated sets.
@@ -531,6 +533,11 @@ def main():
     pending = [None, None]
     stream = torch.cuda.current_stream()
 
+    # one step = hb_loglik_batch_dev: a single fused launch (records in the
+    # eval kernel's prologue) up to 16 walkers per CU, else prep + eval; the
+    # kernel-timing pass times the fused kernel, or the two launches apart
+    fused = L.fused_wpb(w) > 0
+
     def step(k, ev=None):
         b = k & 1
         if pending[b] is not None:
@@ -538,11 +545,15 @@ def main():
             pending[b] = None
         if ev is not None:
             ev[0].record(stream)
-        L.prepare_dev(P[k % nb], stream)
-        if ev is not None:
+        if ev is None or fused:
+            L.loglike_dev(P[k % nb], outs[b], stream)
+            if ev is not None:
+                ev[1].record(stream)
+                ev[2].record(stream)
+        else:
+            L.prepare_dev(P[k % nb], stream)
             ev[1].record(stream)
-        L.evaluate_dev(w, outs[b], 0, stream)
-        if ev is not None:
+            L.evaluate_dev(w, outs[b], 0, stream)
             ev[2].record(stream)
         if world > 1:
             pending[b] = dist.all_gather_into_tensor(gathered[b], outs[b], async_op=True)
@@ -580,8 +591,12 @@ def main():
     drain()
     torch.cuda.synchronize()
     timed = evs
-    prep_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in timed]))
-    eval_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in timed]))
+    if fused:  # one kernel: ev[0] -> ev[1]
+        eval_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in timed]))
+        prep_ms = 0.0
+    else:
+        prep_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in timed]))
+        eval_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in timed]))
     if world > 1:
         tt = torch.tensor([wall, eval_ms, prep_ms], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -624,7 +639,9 @@ def main():
                        "note": "reference sampler spends 2 evals per walker-step (mcmc_wrapper2.c:488-489)"},
             "roofline": roofline(a.config if a.config != "C2" or n <= 2048 else "C3", eval_ms, float(w),
                                  float(bytes_per_eval * w),
-                                 {"kernel": kernel_name, "kernel_ms": eval_ms, "prep_kernel_ms": prep_ms,
+                                 {"kernel": kernel_name + (f" (fused: records in its prologue, {L.fused_wpb(w)} "
+                                                           "walkers per workgroup)" if fused else ""),
+                                  "kernel_ms": eval_ms, "prep_kernel_ms": None if fused else prep_ms,
                                   "kernel_event_samples": len(timed), "kernel_timer": a.timer,
                                   "bytes_per_eval": bytes_per_eval}),
             "kernel_only_evals_per_s": w / ((eval_ms + prep_ms) * 1e-3),

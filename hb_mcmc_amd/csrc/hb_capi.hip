@@ -162,6 +162,7 @@ constexpr int kLatencyW = 512;
 
 struct hb_ctx {
   int device = 0;
+  int cus = 256;                  // compute units of the device (the fused launch's workgroup size)
   EvalPlan plan;
   EvalPlan lat;                   // multi-wave plan for batches below kLatencyW (N <= 2048 only)
   bool has_lat = false;
@@ -266,6 +267,8 @@ extern "C" hb_ctx* hb_create(const double* t, const double* f, const double* sig
   for (int k = 0; k < 4; ++k) c->mags.magerr[k] = magerr4 ? magerr4[k] : deferr[k];
 
   if (hipSetDevice(device) != hipSuccess) { set_err_msg("hb_create: hipSetDevice failed"); return nullptr; }
+  if (hipDeviceGetAttribute(&c->cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || c->cus <= 0)
+    c->cus = 256;
   std::vector<double> s(sigma, sigma + n);
   for (long i = 0; i < n; ++i) {
     if (s[i] < 1.e-5) s[i] = 1.e-5;  // likelihood3.c:824-827, applied once
@@ -323,6 +326,10 @@ extern "C" int hb_ctx_set_latency_plan(hb_ctx* c, int on) {
   c->has_lat = on != 0 && c->plan.vpt > 0 && c->lat.lds && c->lat.bvpt > 0;
   return 0;
 }
+extern "C" int hb_ctx_fused_wpb(const hb_ctx* c, int w) {
+  if (!c) return set_err_msg("null context");
+  return hbk::fused_wpb(c->plan, w, c->cus);
+}
 extern "C" int hb_ctx_eval_kind(const hb_ctx* c) {
   if (!c) return -1;
   return c->plan.vpt > 0 ? 0 : c->plan.bvpt > 0 ? 1 : 2;
@@ -339,11 +346,20 @@ static int run_batch(hb_ctx* c, const double* d_params, int w, double* d_logl, d
     int rc = hb_reserve(c, w);
     if (rc) return rc;
   }
+  const EvalPlan& pl = (acc == nullptr && c->has_lat && w < kLatencyW) ? c->lat : c->plan;
+  // logL batches of the one-wave plan: ONE launch, the records computed in
+  // the eval kernel's prologue (hbk::launch_eval_fused)
+  const int fw = (prep && acc == nullptr && d_tmpl == nullptr && &pl == &c->plan) ? hbk::fused_wpb(pl, w, c->cus) : 0;
+  if (fw > 0) {
+    const hbk::PreArgs pa{d_params, c->mags, c->d_wc, c->d_ph, c->d_tab_pc};
+    HB_TRY(hbk::launch_eval_fused(pl, fw, pa, c->d_t, c->d_f, c->d_s, c->d_rows, w, d_logl, s, c->d_dq),
+           "hb_eval_wave_kernel (fused)");
+    return 0;
+  }
   if (prep)
     HB_TRY(hbk::launch_prep(d_params, w, c->mags, c->d_wc, s, nullptr, nullptr, c->d_t, c->plan.n, c->d_ph, nullptr,
                             0, c->d_tab_pc),
            "hb_prep_kernel");
-  const EvalPlan& pl = (acc == nullptr && c->has_lat && w < kLatencyW) ? c->lat : c->plan;
   HB_TRY(hbk::launch_eval(pl, c->d_t, c->d_ph, c->d_f, c->d_s, c->d_rows, c->d_wc, w, d_logl, d_tmpl, c->d_scratch,
                           d_tmpl ? 1 : 0, s, acc, c->d_dq),
          "hb_eval_kernel");

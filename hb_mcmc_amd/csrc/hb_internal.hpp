@@ -105,6 +105,22 @@ hipError_t launch_eval_multi(int vpt, size_t slab_bytes, const double* t, const 
                              const double* sg, const double* rows,
                              const TargetDesc* tab, const int* wt, const int* list, int count,
                              const hbdev::WalkerConst* wc, double* logl, hipStream_t s, double* dq, int wpw = 1);
+// The fused launch: per-walker records (hb_prep.hpp) in the prologue of the
+// one-wave eval kernel, WPB walkers per workgroup (hb_kernels.hip
+// launch_eval_fused); the records and the shared-period phase table are also
+// written to the context's buffers (as hb_prep_kernel writes them).
+struct PreArgs {
+  const double* params;     // W x 21
+  MagArgs ma;
+  hbdev::WalkerConst* wc;   // records out (then read back by the eval waves)
+  double2* ph;              // the global phase table (each workgroup writes a slice)
+  double* tab_pc;           // its period [s]
+};
+// walkers per workgroup of the fused launch for w walkers on `cus` CUs (0: the
+// two-launch path: prep + eval)
+int fused_wpb(const EvalPlan& pl, int w, int cus);
+hipError_t launch_eval_fused(const EvalPlan& pl, int wpb, const PreArgs& pa, const double* t, const double* f,
+                             const double* sg, const double* rows, int nwalk, double* logl, hipStream_t s, double* dq);
 int wave_vpt_for(long n);  // cadences per lane of the one-wave path, 0 if n > 2048
 int wave_nr_for(long n);   // lane rows per walker: 64, or 128 (a pair of waves) for 1024 < n <= 2048
 // device bytes of the one-wave kernel's deferred cadence queue for `count`

@@ -924,6 +924,9 @@ constexpr int kSelBits2 = HB_SEL_BITS2;  // later digits (the survivors of one b
 #define HB_CAND 64
 #endif
 constexpr int kCandMax = HB_CAND;  // survivors ranked directly (<= 64: one per lane)
+// slab bytes from which the fused launch keeps the survivors inside the slab
+// (above the 2^kSelBits-bin histogram)
+constexpr int kCandInSlab = (4 << kSelBits) + 8 * kCandMax;
 
 template <int VPT>
 __device__ double wave_select(const uint64_t (&key)[VPT], uint32_t kth, uint64_t kmin, uint64_t kmax,
@@ -1519,6 +1522,90 @@ __device__ __forceinline__ bool key_live(const Rows& r, int v, int lane, long n)
   return (v < r.rc) & (lane * r.rc + v < n);
 }
 
+// ---------------------------------------------------------------------------
+// Fused launch (PRE): the per-walker records of the workgroup's WPB walkers in
+// the eval kernel's prologue, instead of a separate hb_prep_kernel launch.
+// Waves 0-3 run the four prep roles with lane = walker (hb_prep.hpp, the
+// same operations as hb_prep_kernel: bit-identical records); the other waves
+// meanwhile fill the shared-period phase table into LDS (every workgroup the
+// whole table, the values hb_prep_kernel writes: (sin, cos)(t_i DAY 2pi/P0)
+// for walker 0's period P0) and store their workgroup's slice of it to the
+// context's global table, so later launches (hb_evaluate_dev, the device
+// sampler) see what a prep launch would have left.  The records go to the
+// context's workspace too, where each eval wave reads its own with scalar
+// loads after the prologue's last barrier (stores complete first).  The prep
+// scratch aliases the waves' slabs, which the model pass only writes after
+// that barrier.
+// ---------------------------------------------------------------------------
+template <int WPB>
+__device__ __forceinline__ void fused_prologue(const PreArgs& pa, int count, int n, const double* __restrict__ t,
+                                               unsigned char* smem_all, double2* tabl) {
+  static_assert(WPB >= kPrepRoles && WPB <= 16, "four prep roles, <= 1024 threads");
+  constexpr int NT = 64 * WPB;
+  PrepShared<WPB>& L = *reinterpret_cast<PrepShared<WPB>*>(smem_all);
+  const int tid = threadIdx.x;
+  const int base = blockIdx.x * WPB;
+  const int nb = min(WPB, count - base);
+  {  // parameters, all loads in flight before the first LDS write
+    constexpr int U = (WPB * kNpars + NT - 1) / NT;
+    double v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = tid + u * NT;
+      v[u] = i < nb * kNpars ? pa.params[(size_t)base * kNpars + i] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = tid + u * NT;
+      if (i < nb * kNpars) L.sp[i] = v[u];
+    }
+  }
+  // the table period: walker 0's (hb_prep_kernel's tab_pc of a single context)
+  const double Pc0 = exp10(pa.params[2]) * kDay;
+  auto tab_pc = [&](int) -> double { return Pc0; };
+  // (sin, cos)(t_i DAY 2pi/Pc0) for i = first, first + stride, ... < n, into
+  // LDS; this workgroup's slice [lo, hi) of the cadences also to the global table
+  auto table = [&](int first, int stride) {
+    const double mA0 = kTwoPi / Pc0;
+    const int G = (int)gridDim.x;
+    const int lo = (int)((long)n * blockIdx.x / G), hi = (int)((long)n * (blockIdx.x + 1) / G);
+    for (int i = first; i < n; i += stride) {
+      double sv, cv;
+      sincos_table((t[i] * kDay) * mA0, sv, cv);
+      const double2 e = make_double2(sv, cv);
+      tabl[i] = e;
+      if (i >= lo && i < hi) pa.ph[i] = e;
+    }
+    if (blockIdx.x == 0 && first == 0 && pa.tab_pc != nullptr) *pa.tab_pc = Pc0;
+  };
+  __syncthreads();
+  auto none = []() {};
+  if constexpr (WPB > kPrepRoles) {
+    auto idle = [&]() { table(tid - 64 * kPrepRoles, NT - 64 * kPrepRoles); };
+    prep_records<WPB>(L, nb, pa.ma, nullptr, nullptr, base, tab_pc, none, idle);
+  } else {
+    prep_records<WPB>(L, nb, pa.ma, nullptr, nullptr, base, tab_pc, none);
+    table(tid, NT);  // four waves: the table after the roles
+  }
+  {  // the records to the workspace (coalesced), complete before the barrier
+    double* dst = reinterpret_cast<double*>(pa.wc) + (size_t)base * kWcDoubles;
+    constexpr int U = (WPB * kWcDoubles + NT - 1) / NT;
+    double v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = tid + u * NT;
+      v[u] = i < nb * kWcDoubles ? L.so[i] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = tid + u * NT;
+      if (i < nb * kWcDoubles) dst[i] = v[u];
+    }
+  }
+  __builtin_amdgcn_s_waitcnt(0);  // the stores acknowledged (L2) before any wave's scalar loads
+  __syncthreads();
+}
+
 // MULTI (catalog mode): the walker is list[blockIdx.x] and its light curve is
 // its target's slice (tab[wt[walker]]); n and kth come from the descriptor.
 // ACC (device sampler): the wave then runs the Hastings test and history write
@@ -1530,15 +1617,19 @@ __device__ __forceinline__ bool key_live(const Rows& r, int v, int lane, long n)
 // WPW = 2: a pair of waves per walker (N = 1025..2048, see PairShared): wave h
 // owns lane rows 64 h .. 64 h + 63 of 128; VPT is then the cadences per lane
 // of the pair's rows (<= 16).
-template <int VPT, bool MULTI, bool ACC = false, int WPB = 1, int WPW = 1>
+// PRE: the fused launch (fused_prologue above): WPB walkers per workgroup, the
+// records computed in the prologue, the phase table read from LDS.
+template <int VPT, bool MULTI, bool ACC = false, int WPB = 1, int WPW = 1, bool PRE = false>
 __global__ __launch_bounds__(64 * WPB * WPW) HB_WPE_ATTR void hb_eval_wave_kernel(
     const double* __restrict__ t, const double2* __restrict__ ph, const double* __restrict__ f,
     const double* __restrict__ isg, const double* __restrict__ rows,
     long n, long kth, const WalkerConst* __restrict__ wcs, double* __restrict__ logl,
     double* __restrict__ tmpl_out, int mode, int slab_bytes, double gap, const TargetDesc* __restrict__ tab,
     const int* __restrict__ wt, const int* __restrict__ list, hbds::AccArgs hst, int count, int lds_per,
-    double* __restrict__ dqbuf) {
+    double* __restrict__ dqbuf, PreArgs pre) {
   static_assert(WPW == 1 || (WPW <= kMaxWPW && WPB == 1 && !ACC && HB_SEL_V == 3 && HB_GQ), "pair/rows: plain batched path");
+  static_assert(!PRE || (WPW == 1 && !MULTI && !ACC && WPB >= kPrepRoles && HB_SEL_V == 3 && HB_GQ && HB_PRIO != 2),
+                "fused launch: plain one-wave batched path");
   constexpr int NR = 64 * WPW;  // lane rows per walker
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_all[];
   const int lane = threadIdx.x & 63;
@@ -1548,6 +1639,17 @@ __global__ __launch_bounds__(64 * WPB * WPW) HB_WPE_ATTR void hb_eval_wave_kerne
   const int slot = (int)blockIdx.x * WPB + wib;
   const bool valid = WPB == 1 || slot < count;
   unsigned char* smem = smem_all + (size_t)wib * (size_t)lds_per;
+  if constexpr (PRE) {
+    double2* tabl = reinterpret_cast<double2*>(smem_all + (size_t)WPB * (size_t)lds_per);
+    fused_prologue<WPB>(pre, count, (int)n, t, smem_all, tabl);
+    // the records just written: scalar loads (constant address space), issued
+    // only after the prologue's last barrier (the pointer passes through asm)
+    typedef const __attribute__((address_space(4))) WalkerConst cwc_t;
+    uint64_t a = (uint64_t)pre.wc;
+    __asm__ volatile("" : "+s"(a));
+    wcs = (const WalkerConst*)(cwc_t*)a;
+    ph = tabl;
+  }
   int wv = slot;
   if (ACC && hst.ecnt != nullptr && valid) wv = hbds::eval_slot_by_e(hst, slot, lane);  // device sampler
   if (MULTI && valid) {
@@ -1567,7 +1669,9 @@ __global__ __launch_bounds__(64 * WPB * WPW) HB_WPE_ATTR void hb_eval_wave_kerne
 #endif
   double* vals = reinterpret_cast<double*>(smem);
   uint32_t* hist = reinterpret_cast<uint32_t*>(smem);
-  uint64_t* cand = reinterpret_cast<uint64_t*>(smem + slab_bytes);
+  // the select's survivors: past the slab, or (fused launch) inside it, past
+  // the histogram (the slab is dead once the keys are in registers)
+  uint64_t* cand = reinterpret_cast<uint64_t*>(smem + (PRE && slab_bytes >= kCandInSlab ? (4 << kSelBits) : slab_bytes));
   const WalkerConst& w = wcs[valid ? wv : 0];
 #ifdef HB_ABLATE_EXIT  // experiment builds only: every wave takes the early exit (launch floor)
   const bool roche_exit = mode == 0;
@@ -2233,14 +2337,16 @@ int wave_wpb(int count, size_t lds_per) {
   return wpb < 1 ? 1 : wpb;
 }
 
-template <int VPT, bool MULTI, bool ACC, int WPB, int WPW = 1>
+template <int VPT, bool MULTI, bool ACC, int WPB, int WPW = 1, bool PRE = false>
 static hipError_t launch_wave_g(size_t lds_per, int count, hipStream_t s, const double* t, const double2* ph,
                                 const double* f, const double* sg, const double* rows, long n, long kth, const WalkerConst* wc,
                                 double* logl, double* tmpl, int mode, size_t slab, double gap,
                                 const TargetDesc* tab, const int* wt, const int* list,
-                                const hbds::AccArgs& acc, double* dq) {
-  auto kern = hb_eval_wave_kernel<VPT, MULTI, ACC, WPB, WPW>;
-  const size_t lds = (size_t)WPB * lds_per + (WPB > 1 ? 64 : 0);
+                                const hbds::AccArgs& acc, double* dq, const PreArgs* pre = nullptr) {
+  auto kern = hb_eval_wave_kernel<VPT, MULTI, ACC, WPB, WPW, PRE>;
+  // PRE: the slices, then the LDS phase table (16 B per cadence)
+  const size_t lds = (size_t)WPB * lds_per + (PRE ? (((size_t)n * 16 + 15) & ~(size_t)15) : (WPB > 1 ? 64 : 0));
+  if (lds > kLdsCap) return hipErrorInvalidValue;
   static bool attr_set = false;  // per instantiation; benign race (idempotent)
   if (!attr_set && lds > 65536) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
@@ -2249,8 +2355,72 @@ static hipError_t launch_wave_g(size_t lds_per, int count, hipStream_t s, const 
     attr_set = true;
   }
   hipLaunchKernelGGL(kern, dim3((count + WPB - 1) / WPB), dim3(64 * WPB * WPW), lds, s, t, ph, f, sg, rows, n, kth, wc, logl,
-                     tmpl, mode, (int)slab, gap, tab, wt, list, acc, count, (int)lds_per, dq);
+                     tmpl, mode, (int)slab, gap, tab, wt, list, acc, count, (int)lds_per, dq, pre ? *pre : PreArgs{});
   return hipGetLastError();
+}
+
+// LDS bytes per walker of the fused launch: the slab, with the survivors
+// inside it when it is big enough (kCandInSlab)
+static size_t fused_lds_per(const EvalPlan& pl) {
+  const size_t slab = pl.slab_bytes;
+  return slab >= (size_t)kCandInSlab ? slab : wave_lds_bytes(slab, pl.vpt, 1);
+}
+
+// Walkers per workgroup of the fused launch (0: prep + eval launches).  The
+// workgroup keeps WPB one-wave walkers plus the LDS phase table; the largest
+// WPB in {16, 8, 4} that still gives every CU a workgroup, as long as the
+// resident walkers per CU (LDS) match the one-wave kernel's 16 (or the batch's
+// share).  Batches beyond one resident round (w > 16 CUs) keep two launches:
+// a 1024-thread workgroup frees its CU only when its slowest walker is done,
+// where single-wave workgroups backfill.  HB_FUSED=0 (A/B knob): never;
+// HB_FUSED=2: whenever it fits.
+int fused_wpb(const EvalPlan& pl, int w, int cus) {
+  static const int mode = getenv("HB_FUSED") ? atoi(getenv("HB_FUSED")) : 1;
+  if (mode == 0 || pl.vpt <= 0 || pl.vpt > 16 || pl.wpw != 1 || !HB_GQ || HB_SEL_V != 3 || HB_PRIO == 2) return 0;
+  if (w <= 0 || cus <= 0 || (mode == 1 && (long)w > 16L * cus)) return 0;
+  const size_t per = fused_lds_per(pl), tabb = ((size_t)pl.n * 16 + 15) & ~(size_t)15;
+  const long share = std::min<long>(16, ((long)w + cus - 1) / cus);  // walkers a CU must hold at once
+  for (int wpb = 16; wpb >= 4; wpb >>= 1) {
+    const size_t lds = (size_t)wpb * per + tabb;
+    if (lds > kLdsCap) continue;
+    const long resident = (long)(kLdsCap / lds) * wpb;
+    if (resident < share) continue;
+    if (wpb > 4 && ((long)w + wpb - 1) / wpb < cus) continue;  // a workgroup for every CU
+    return wpb;
+  }
+  return 0;
+}
+
+template <int VPT>
+static hipError_t launch_fused_t(const EvalPlan& pl, int wpb, const PreArgs& pa, const double* t, const double* f,
+                                 const double* sg, const double* rows, int nwalk, double* logl, hipStream_t s,
+                                 double* dq) {
+  const size_t per = fused_lds_per(pl);
+  const hbds::AccArgs none{};
+#define HB_FCASE(WV)                                                                                               \
+  if (wpb == WV)                                                                                                   \
+    return launch_wave_g<VPT, false, false, WV, 1, true>(per, nwalk, s, t, pa.ph, f, sg, rows, pl.n, pl.kth, pa.wc, \
+                                                         logl, nullptr, 0, pl.slab_bytes, pl.gap, nullptr, nullptr,  \
+                                                         nullptr, none, dq, &pa);
+  HB_FCASE(16)
+  HB_FCASE(8)
+  HB_FCASE(4)
+#undef HB_FCASE
+  return hipErrorInvalidValue;
+}
+
+hipError_t launch_eval_fused(const EvalPlan& pl, int wpb, const PreArgs& pa, const double* t, const double* f,
+                             const double* sg, const double* rows, int nwalk, double* logl, hipStream_t s, double* dq) {
+  if (nwalk <= 0) return hipSuccess;
+  if (dq == nullptr || pa.params == nullptr || pa.wc == nullptr || pa.ph == nullptr) return hipErrorInvalidValue;
+  switch (pl.vpt) {
+    case 1: return launch_fused_t<1>(pl, wpb, pa, t, f, sg, rows, nwalk, logl, s, dq);
+    case 2: return launch_fused_t<2>(pl, wpb, pa, t, f, sg, rows, nwalk, logl, s, dq);
+    case 4: return launch_fused_t<4>(pl, wpb, pa, t, f, sg, rows, nwalk, logl, s, dq);
+    case 8: return launch_fused_t<8>(pl, wpb, pa, t, f, sg, rows, nwalk, logl, s, dq);
+    case 16: return launch_fused_t<16>(pl, wpb, pa, t, f, sg, rows, nwalk, logl, s, dq);
+    default: return hipErrorInvalidValue;
+  }
 }
 
 template <int VPT, bool MULTI, bool ACC, int WPW = 1>
@@ -2374,9 +2544,9 @@ hipError_t launch_eval(const EvalPlan& pl, const double* t, const double2* ph, c
   if (pl.bvpt > 0) {
 #define HB_BCASE(NWV, V)                                                                    \
   if (pl.nw == NWV && pl.bvpt == V) return launch_block_t<NWV, V>(pl, t, ph, f, sg, wc, nwalk, logl, tmpl, mode, s);
-    HB_BCASE(4, 8) HB_BCASE(4, 16) HB_BCASE(4, 24) HB_BCASE(4, 32)
-    HB_BCASE(8, 8) HB_BCASE(8, 16) HB_BCASE(8, 24) HB_BCASE(8, 32)
-    HB_BCASE(16, 8) HB_BCASE(16, 16) HB_BCASE(16, 24) HB_BCASE(16, 32)
+    HB_BCASE(4, 8) HB_BCASE(4, 16) HB_BCASE(4, 20) HB_BCASE(4, 24) HB_BCASE(4, 32)
+    HB_BCASE(8, 8) HB_BCASE(8, 16) HB_BCASE(8, 20) HB_BCASE(8, 24) HB_BCASE(8, 32)
+    HB_BCASE(16, 8) HB_BCASE(16, 16) HB_BCASE(16, 20) HB_BCASE(16, 24) HB_BCASE(16, 32)
 #undef HB_BCASE
     return hipErrorInvalidValue;
   }
@@ -2576,7 +2746,9 @@ EvalPlan make_block_plan(long n) {
 #if HB_BLOCK_KEYS
     const long per = (n + 64L * nw - 1) / (64L * nw);  // cadences per thread
     if (per <= 32 && need >= sizeof(SelShared) + (4u << kSelBits) + 8 * kCandMax)
-      pl.bvpt = per <= 8 ? 8 : per <= 16 ? 16 : per <= 24 ? 24 : 32;
+      // exact fit at 17..20 (C3: N = 20 000 over 16 waves is 19.5 per thread): 24
+      // key slots there cost <16, 24> 14 VGPR spills (64 B of scratch per lane)
+      pl.bvpt = per <= 8 ? 8 : per <= 16 ? 16 : per <= 20 ? 20 : per <= 24 ? 24 : 32;
 #endif
   } else {
     pl.lds = false;

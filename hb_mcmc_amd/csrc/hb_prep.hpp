@@ -51,19 +51,31 @@ struct PrepShared {
   double gs[3][NW];            // wave 2's Gaia term and sin/cos omega
 };
 
+struct PrepNoIdle {
+  __device__ void operator()() const {}
+};
 // Records of the nb <= NW walkers whose parameters are in L.sp, into L.so.
-// Every thread of the four waves calls it (it holds two workgroup barriers and
+// Every thread of the workgroup calls it (it holds two workgroup barriers and
 // ends with a third).  tab/wt/base: catalog mode (the walker's target
 // descriptor), else null.  tab_pc(j): the period [s] of the phase table walker
 // j may use (NaN: no table).  slack(): wave 2's spare work after its own terms.
-template <int NW, class TabPc, class Slack>
+// Waves past the four roles (a workgroup of more than 256 threads: the fused
+// eval kernel) run idle() between the first and the second barrier.
+template <int NW, class TabPc, class Slack, class Idle = PrepNoIdle>
 __device__ __forceinline__ void prep_records(PrepShared<NW>& L, int nb, const MagArgs& ma,
                                              const TargetDesc* __restrict__ tab, const int* __restrict__ wt,
-                                             int base, TabPc tab_pc, Slack slack) {
+                                             int base, TabPc tab_pc, Slack slack, Idle idle = Idle()) {
   static_assert(NW >= 1 && NW <= 64, "one walker per lane");
   const int tid = threadIdx.x;
   const int j = tid & 63;
-  const int wv = tid >> 6;  // wave-uniform role
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform role
+  if (wv >= kPrepRoles) {  // no role: the barriers, and the caller's work in between
+    __syncthreads();
+    idle();
+    __syncthreads();
+    __syncthreads();
+    return;
+  }
   const int star = wv & 1;
   const bool chainR = wv < 2;  // radius law + coefficients; else Teff law + tail
   const bool live = j < nb;

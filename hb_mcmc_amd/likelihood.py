@@ -84,6 +84,12 @@ class HBLikelihood:
         kind = self.lib.hb_ctx_eval_kind(self._h)
         return ("hb_eval_wave_kernel", "hb_eval_block_kernel", "hb_eval_kernel")[kind]
 
+    def fused_wpb(self, w: int) -> int:
+        """Walkers per workgroup of the single fused launch loglike_dev makes
+        for w walkers (records in the eval kernel's prologue), 0 when it makes
+        two launches (prepare_dev + evaluate_dev)."""
+        return int(self.lib.hb_ctx_fused_wpb(self._h, int(w)))
+
     def reserve(self, max_walkers: int):
         _lib.check(self.lib.hb_reserve(self._h, int(max_walkers)), "hb_reserve")
 

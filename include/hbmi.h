@@ -144,13 +144,20 @@ int hb_reserve(hb_ctx *ctx, int max_walkers);
 int hb_loglik_batch_dev(hb_ctx *ctx, const double *d_params, int W, double *d_logl, void *stream);
 int hb_loglik_batch(hb_ctx *ctx, const double *params, int W, double *logl, void *stream);
 
-/* The two launches behind hb_loglik_batch_dev, exposed for timing:
- * hb_prepare_dev computes the per-walker constant records (one lane per
- * walker) into the context workspace; hb_evaluate_dev runs the one-workgroup-
- * per-walker model + median + chi^2 kernel on them (mode 0: logL into d_out[W],
- * mode 1: templates into d_out[W x N]).  Same stream, same W. */
+/* The two launches behind hb_loglik_batch_dev when it is not fused (below),
+ * exposed for timing: hb_prepare_dev computes the per-walker constant records
+ * (one lane per walker) into the context workspace; hb_evaluate_dev runs the
+ * one-workgroup-per-walker model + median + chi^2 kernel on them (mode 0: logL
+ * into d_out[W], mode 1: templates into d_out[W x N]).  Same stream, same W. */
 int hb_prepare_dev(hb_ctx *ctx, const double *d_params, int W, void *stream);
 int hb_evaluate_dev(hb_ctx *ctx, int W, double *d_out, int mode, void *stream);
+/* Walkers per workgroup of the fused launch hb_loglik_batch_dev makes for W
+ * walkers (the records computed in the eval kernel's prologue: ONE launch), or
+ * 0 when it makes the two launches above.  Fused: one-wave plans of up to 1024
+ * cadences, W up to 16 walkers per compute unit (4096 on MI355X).  Either way
+ * the records and the phase table the context keeps are the same, and so are
+ * the logL values (bit for bit). */
+int hb_ctx_fused_wpb(const hb_ctx *ctx, int W);
 
 /* Model light curves (median removed, blended), row-major W x N. */
 int hb_light_curve_batch_dev(hb_ctx *ctx, const double *d_params, int W, double *d_out, void *stream);

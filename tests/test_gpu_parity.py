@@ -340,6 +340,45 @@ def test_dropin_concurrent_calls_are_combined_exactly(hbmi):
     close_logl(solo, g["logl"][:24])
 
 
+# ------------------------------------------------- fused launch
+@pytest.mark.parametrize("n,w", [(1024, 4096), (1024, 2048), (1024, 1000), (1024, 5), (1024, 4097),
+                                 (512, 4096), (100, 777), (7, 64)])
+def test_fused_launch_equals_two_launches(hbmi, oracle, n, w):
+    """hb_loglik_batch_dev makes ONE launch up to 16 walkers per CU (the
+    records computed in the eval kernel's prologue, the phase table in LDS):
+    bit-identical to the two-launch path (hb_prepare_dev + hb_evaluate_dev) on
+    the same walkers, and it leaves the same records and global phase table
+    behind (an hb_evaluate_dev right after it gives the same values again).
+    Walkers off the table period, Roche walkers and cold (e = 0.85) walkers
+    included; a sample against the oracle."""
+    import torch
+
+    from hb_mcmc_amd import synth
+    from hb_mcmc_amd.likelihood import HBLikelihood
+
+    t, f, s = synth.dataset(n, oracle.light_curve)
+    P = synth.walkers(w, seed=n + w)
+    P[1::7, 2] += 1e-4  # off walker 0's period: direct sincos
+    P[2::9, 3] = 0.85   # cold Kepler path
+    dev = torch.device("cuda", 0)
+    Pd = torch.from_numpy(P).to(dev)
+    a, b, c = (torch.empty(w, dtype=torch.float64, device=dev) for _ in range(3))
+    with HBLikelihood(t, f, s) as L:
+        L.reserve(w)
+        fw = L.fused_wpb(w)
+        assert (fw > 0) == (n <= 1024 and w <= 4096), fw
+        L.prepare_dev(Pd)
+        L.evaluate_dev(w, a)
+        L.loglike_dev(Pd, b)
+        L.evaluate_dev(w, c)  # the records / table the fused launch left behind
+        torch.cuda.synchronize()
+    a, b, c = a.cpu().numpy(), b.cpu().numpy(), c.cpu().numpy()
+    assert np.array_equal(a, b, equal_nan=True)
+    assert np.array_equal(b, c, equal_nan=True)
+    idx = np.arange(0, w, max(1, w // 128))
+    close_logl(b[idx], oracle.loglike_batch(t, f, s, P[idx], synth.MAG_DEFAULT, synth.MAGERR_DEFAULT, 8))
+
+
 # ------------------------------------------------- full-size (config C2)
 def test_full_size_c2_against_oracle_and_properties(hbmi, oracle):
     """W=4096, N=1024: oracle on a 256-walker sample; size-independent
