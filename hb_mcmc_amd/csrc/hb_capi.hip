@@ -374,7 +374,9 @@ static int run_batch(hb_ctx* c, const double* d_params, int w, double* d_logl, d
 extern "C" int hbx_loglik_accept_dev(hb_ctx* c, const double* d_params, int w, double* d_logl, const void* acc,
                                      void* stream) {
   if (!c) return set_err_msg("null context");
-  if (c->plan.vpt == 0 || c->plan.wpw != 1) return 1;  // no fused epilogue: multi-wave or pair plans
+  // no fused epilogue: multi-wave or pair plans, and 32 cadences per lane
+  // (the epilogue's registers would spill there, hbk::launch_eval)
+  if (c->plan.vpt == 0 || c->plan.wpw != 1 || c->plan.vpt > 16) return 1;
   if (w > c->cap) return set_err_msg("hbx_loglik_accept_dev: W exceeds the prepared workspace");
   static const bool split = getenv("HB_DS_SPLIT_ACCEPT") != nullptr;  // experiment knob: separate ds_accept
   if (split) return 1;
@@ -471,7 +473,8 @@ static int host_batch(hb_ctx* c, const double* params, int w, double* out, void*
 // and slab sizes are those of 32 cadences per lane of one wave
 static constexpr int kCatClasses = 7;
 static constexpr int kCatRcHi[kCatClasses] = {1, 2, 4, 8, 16, 32, 32};
-static constexpr int kCatStreams = 4;  // the caller's + 3 forked
+static constexpr int kCatStreams = 4;  // at most: the caller's + 3 forked
+static constexpr int kCatDefaultStreams = 2;
 // experiment knob (A/B only): HB_CAT_STREAMS = streams used (1..4)
 static int cat_env(const char* k, int def) {
   const char* v = getenv(k);
@@ -748,7 +751,10 @@ static int catalog_run(hb_catalog* c, const double* d_params, double* d_logl, hi
   for (int cl = 0; cl < kCatClasses; ++cl)
     if (c->class_off[cl + 1] > c->class_off[cl]) order[nc++] = cl;
   std::sort(order, order + nc, [&](int a, int b) { return c->class_work[a] > c->class_work[b]; });
-  static const int kns = std::max(1, std::min(kCatStreams, cat_env("HB_CAT_STREAMS", kCatStreams)));
+  // two streams: C5 0.164 ms per call against 0.183 on four and 0.196 on one
+  // (profiles/r04/r04c_bench_c5_s*.json: the forked streams' event waits cost
+  // more than the extra overlap buys)
+  static const int kns = std::max(1, std::min(kCatStreams, cat_env("HB_CAT_STREAMS", kCatDefaultStreams)));
   const int ns = nc < kns ? nc : kns;
   if (ns > 1) {
     HB_TRY(hipEventRecord(c->ev_fork, s), "fork event");

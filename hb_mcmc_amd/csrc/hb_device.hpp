@@ -1088,4 +1088,137 @@ __device__ __forceinline__ void hb_cadence_flux_chain(const double (&t)[K], cons
   bad = !ok;
 }
 
+// ------------------------------------------------------------------------
+// The same chain step in two halves, so the model pass can software-pipeline
+// the chains (model_pass_chain_pipe, hb_kernels.hip): step j's Kepler solve
+// and step j-1's photometric polynomial read the same chain state and are
+// independent, so both sit in one basic block and interleave (twice the
+// independent fp64 chains per lane: the drain, where one or two waves are
+// left on a SIMD, is latency-bound).  Same operations in the same order as
+// hb_cadence_flux_chain (HB_WARM_V == 2, HB_RCP_REUSE): bit-identical values.
+// ------------------------------------------------------------------------
+#if HB_WARM_V == 2 && HB_RCP_REUSE && HB_WARM
+#define HB_CHAIN_SPLIT 1
+// warm half: the mean anomaly up to a multiple of 2pi (no exactness flags),
+// the third-order start from the chain state, the degree-9 rotation and one
+// Newton step; fine: the lane's step converged (see hb_cadence_flux_chain)
+template <int K>
+__device__ __forceinline__ void chain_kepler_warm(const double (&t)[K], const WalkerConst& w, const ChainState<K>& st,
+                                                  double (&m)[K], double (&E)[K], double (&s)[K], double (&c)[K],
+                                                  double (&ys)[K], bool& fine, bool& ok) {
+  const double e = w.e;
+  fine = true;
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const double x = fma(t[k], kDay, w.mB) * w.mA;
+    ok &= sincos_fast_ok(x);
+    m[k] = fma(-trunc(x * 0.15915494309189533577), kTwoPi, x);
+  }
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const double D = m[k] - fma(-e, st.s[k], st.E[k]);
+    const double q = rint(D * 0.15915494309189533577);
+    const double Dc = fma(-q, kTwoPi, D);
+    const double r = st.inv[k];
+    const double x = Dc * r;
+    const double A = (e * st.s[k]) * (0.5 * r);
+    const double B = (e * st.c[k]) * (r * (1.0 / 6.0));
+    const double C = fma(2.0 * A, A, -B);
+    const double dl = fma(x * x, fma(C, x, -A), x);
+    double E0 = fma(q, kTwoPi, st.E[k]) + dl;
+    double s0 = st.s[k], c0 = st.c[k];
+    const double z0 = dl * dl;
+    fine &= fabs(dl) <= 0.0625;
+    {
+      const double sd = fma(dl * z0, fma(z0, fma(z0, fma(z0, 1.0 / 362880.0, -1.0 / 5040.0), 1.0 / 120.0),
+                                         -1.0 / 6.0), dl);
+      const double cd = fma(z0, fma(z0, fma(z0, fma(z0, 1.0 / 40320.0, -1.0 / 720.0), 1.0 / 24.0), -0.5), 1.0);
+      const double s1 = fma(s0, cd, c0 * sd);
+      const double c1 = fma(c0, cd, -(s0 * sd));
+      s0 = s1;
+      c0 = c1;
+    }
+    const double den = fma(-e, c0, 1.0);
+    double y = __builtin_amdgcn_rcp(den);
+    y = fma(fma(-den, y, 1.0), y, y);
+    const double d = ((E0 - e * s0) - m[k]) * y;
+    E0 = E0 - d;
+    const double z = d * d;
+    fine &= (fabs(d) <= 0x1p-22) & (e * z <= 0x1p-51 * den);
+    rotate_back_tiny(d, z, s0, c0);
+    E[k] = E0;
+    s[k] = s0;
+    c[k] = c0;
+    ys[k] = y;
+  }
+}
+// the rest of a warm step once the wave knows whether every lane is fine:
+// the reciprocal from the Newton step's seed, or the general Newton loop from
+// the lane's iterate (a lane that was not fine first re-evaluates (sin, cos))
+// and, failing that, the reference's start; then the chain state
+template <int K>
+__device__ __forceinline__ void chain_finish_warm(const double (&t)[K], const WalkerConst& w, bool all_fine,
+                                                  bool fine, double (&m)[K], double (&E)[K], double (&s)[K],
+                                                  double (&c)[K], const double (&ys)[K], bool& ok,
+                                                  ChainState<K>& st) {
+  const double e = w.e;
+  if (all_fine) {
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const double den = fma(-e, c[k], 1.0);
+      double y = ys[k];
+      y = fma(fma(-den, y, 1.0), y, y);
+      st.inv[k] = fma(fma(-den, y, 1.0), y, y);
+      st.E[k] = E[k];
+      st.s[k] = s[k];
+      st.c[k] = c[k];
+    }
+    return;
+  }
+  if (!fine) {
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      ok &= sincos_fast_ok(E[k]);
+      sincos_fast(E[k], &s[k], &c[k]);
+    }
+  }
+  double yk[K];
+  if (!newton_k<K>(e, m, E, s, c, yk, ok)) {  // redo from the reference's start
+    bool plus[K], exact = false;
+    ok = true;
+    mean_anomaly_k<K>(t, w, m, plus, ok, exact);
+    const double2 p0[K] = {};
+    cold_start_k<K>(t, p0, false, exact, w, m, plus, E, s, c, ok);
+    (void)newton_k<K>(e, m, E, s, c, yk, ok);
+  }
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    st.E[k] = E[k];
+    st.s[k] = s[k];
+    st.c[k] = c[k];
+    st.inv[k] = fast_rcp(fma(-e, c[k], 1.0));
+  }
+}
+// a chain's first cadence: the reference's start (table entries) and Newton
+template <int K>
+__device__ __forceinline__ void chain_first(const double (&t)[K], const double2 (&ph)[K], bool tab, const WalkerConst& w,
+                                            ChainState<K>& st, bool& ok) {
+  const double e = w.e;
+  double m[K], E[K], s[K], c[K], yk[K];
+  bool exact = false, plus[K];
+  mean_anomaly_k<K>(t, w, m, plus, ok, exact);
+  cold_start_k<K>(t, ph, tab, exact, w, m, plus, E, s, c, ok);
+  (void)newton_k<K>(e, m, E, s, c, yk, ok);
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    st.E[k] = E[k];
+    st.s[k] = s[k];
+    st.c[k] = c[k];
+    st.inv[k] = fast_rcp(fma(-e, c[k], 1.0));
+  }
+}
+#else
+#define HB_CHAIN_SPLIT 0
+#endif
+
 }  // namespace hbdev

@@ -26,6 +26,18 @@
 #include "hb_accept.hpp"
 #include "hb_device.hpp"
 #include "hb_internal.hpp"
+#ifdef HB_WAVE_CLOCKS
+// the fused launch's prologue, 16 marks per workgroup (see HB_PCLK below);
+// prep-role marks 5..8 (phase 1 done, role 0..3), 9..12 (phase 2), 13 (wave
+// 0: records combined)
+__device__ unsigned long long hb_pro_clk[16 * 4096];
+#define HB_PREP_MARK(i)                                                                      \
+  do {                                                                                       \
+    if ((i) != 13 || (threadIdx.x >> 6) == 0)                                                \
+      if ((threadIdx.x & 63) == 0 && blockIdx.x < 4096)                                      \
+        hb_pro_clk[16 * blockIdx.x + (i)] = __builtin_amdgcn_s_memtime();                    \
+  } while (0)
+#endif
 #include "hb_prep.hpp"
 
 using namespace hbdev;
@@ -92,7 +104,16 @@ __device__ unsigned long long hb_wave_clk[8 * 65536];
       hb_wave_clk[8 * (wv) + 7] = clkm_[3];                                             \
     }                                                                                   \
   } while (0)
+// the fused launch's prologue (wave 0 of each workgroup): 0 entry, 1 parameters
+// in LDS, 2 records in LDS (prep_records done), 3 after the last barrier,
+// 4 the table waves' work done (thread 256); 5.. the prep roles (HB_PREP_MARK)
+#define HB_PCLK(i, thr)                                                                \
+  do {                                                                                 \
+    if (threadIdx.x == (thr) && blockIdx.x < 4096)                                     \
+      hb_pro_clk[16 * blockIdx.x + (i)] = __builtin_amdgcn_s_memtime();                \
+  } while (0)
 #else
+#define HB_PCLK(i, thr) do { } while (0)
 #define HB_CLK_BEGIN() do { } while (0)
 #define HB_CLK_MARK(i) do { } while (0)
 #define HB_CLK_END(wv) do { } while (0)
@@ -740,6 +761,78 @@ __device__ __forceinline__ void model_pass_chain(const double* __restrict__ tT, 
     }
 #endif
   }
+}
+
+// Software-pipelined model_pass_chain (HB_GQ; HB_CHAIN_SPLIT): the loop body
+// of step j holds step j's warm Kepler solve and step j-1's polynomial, which
+// both read only the chain state left by step j-1 -- one basic block with
+// two independent dependency chains per Kepler chain (ILP 2 KC instead of KC
+// for the latency-bound tail of the launch).  Step j-1's values are stored and
+// queued after it, then step j is finished (converged lanes: the reciprocal;
+// else the general Newton loop / the reference's start).  Values, queue
+// entries and slab positions are those of model_pass_chain.
+#ifndef HB_PIPE
+#define HB_PIPE 1
+#endif
+template <int VPT, int NR = 64>
+__device__ __forceinline__ void model_pass_chain_pipe(const double* __restrict__ tT, const double2* __restrict__ ph,
+                                                      int n, const Rows& rw, const WalkerConst& w, double* vals,
+                                                      int lane, int row, Pacer pc, DeferQ& dq) {
+#if HB_CHAIN_SPLIT && HB_GQ
+  constexpr int KCM = NR > 64 ? HB_PAIR_KC : HB_KC;
+  constexpr int KC = VPT < KCM ? VPT : KCM;
+  const int lc = (rw.rc + KC - 1) / KC;  // chain length (wave-uniform)
+  const bool tab = (ph != nullptr) && (w.tab != 0.0);  // walker-uniform
+  const int last = n - 1;
+  const int base = row * rw.rc;
+  const int rs = row * rw.stride, lsw = HB_ODD_STRIDE ? 0 : (row & rw.swz);  // slab_pos = rs + (c ^ lsw)
+  const bool live = NR <= 128 || row < rw.live;
+  ChainState<KC> st;
+  double tk[KC];
+#pragma unroll
+  for (int k = 0; k < KC; ++k) tk[k] = tT[min(k * lc, rw.rc - 1) * NR + lane];
+  // the step whose polynomial is pending: its (s, c, 1/den) are the chain state
+  bool pend_ok = true;
+  {  // step 0: the chains' first cadences (the reference's start, table entries)
+    double2 p0[KC];
+#pragma unroll
+    for (int k = 0; k < KC; ++k) p0[k] = tab ? ph[min(base + k * lc, last)] : make_double2(0.0, 1.0);
+    chain_first<KC>(tk, p0, tab, w, st, pend_ok);
+  }
+  // store the pending step jp's values and queue its eclipse / slow-path cadences
+  auto emit = [&](int jp, const double (&v)[KC], const double (&dd)[KC], const double (&zz)[KC], bool bad) {
+#pragma unroll
+    for (int k = 0; k < KC; ++k) {
+      const int c = k * lc + jp;
+      if (c < rw.rc) {  // wave-uniform
+        const int sp = rs + (c ^ lsw);
+        if (live) vals[sp] = v[k];
+        const bool need = (!bad) & eclipse_lane(w, dd[k], zz[k]);
+        dq_push(dq, live & (bad | need), copysign(dd[k], zz[k]), sp | (bad ? kSlowFlag : 0));
+      }
+    }
+  };
+  pc.begin(lc);
+  for (int j = 1; j < lc; ++j) {
+    pc.step(j, lc);
+#pragma unroll
+    for (int k = 0; k < KC; ++k) tk[k] = tT[min(k * lc + j, rw.rc - 1) * NR + lane];
+    double m[KC], E[KC], s[KC], c[KC], ys[KC], v[KC], dd[KC], zz[KC];
+    bool ok = true, fine;
+    chain_kepler_warm<KC>(tk, w, st, m, E, s, c, ys, fine, ok);  // step j
+    flux_poly_inv_k<KC>(st.s, st.c, st.inv, w, v, dd, zz);      // step j - 1, same block
+    emit(j - 1, v, dd, zz, !pend_ok);
+    chain_finish_warm<KC>(tk, w, wave_all(fine), fine, m, E, s, c, ys, ok, st);
+    pend_ok = ok;
+  }
+  {  // the last step's polynomial
+    double v[KC], dd[KC], zz[KC];
+    flux_poly_inv_k<KC>(st.s, st.c, st.inv, w, v, dd, zz);
+    emit(lc - 1, v, dd, zz, !pend_ok);
+  }
+#else
+  (void)tT; (void)ph; (void)n; (void)rw; (void)w; (void)vals; (void)lane; (void)row; (void)pc; (void)dq;
+#endif
 }
 
 // k-th smallest (0-based) of vals[0..n) by radix select; every thread of the
@@ -1544,6 +1637,7 @@ __device__ __forceinline__ void fused_prologue(const PreArgs& pa, int count, int
   constexpr int NT = 64 * WPB;
   PrepShared<WPB>& L = *reinterpret_cast<PrepShared<WPB>*>(smem_all);
   const int tid = threadIdx.x;
+  HB_PCLK(0, 0);
   const int base = blockIdx.x * WPB;
   const int nb = min(WPB, count - base);
   {  // parameters, all loads in flight before the first LDS write
@@ -1579,14 +1673,19 @@ __device__ __forceinline__ void fused_prologue(const PreArgs& pa, int count, int
     if (blockIdx.x == 0 && first == 0 && pa.tab_pc != nullptr) *pa.tab_pc = Pc0;
   };
   __syncthreads();
+  HB_PCLK(1, 0);
   auto none = []() {};
   if constexpr (WPB > kPrepRoles) {
-    auto idle = [&]() { table(tid - 64 * kPrepRoles, NT - 64 * kPrepRoles); };
+    auto idle = [&]() {
+      table(tid - 64 * kPrepRoles, NT - 64 * kPrepRoles);
+      HB_PCLK(4, 64 * kPrepRoles);
+    };
     prep_records<WPB>(L, nb, pa.ma, nullptr, nullptr, base, tab_pc, none, idle);
   } else {
     prep_records<WPB>(L, nb, pa.ma, nullptr, nullptr, base, tab_pc, none);
     table(tid, NT);  // four waves: the table after the roles
   }
+  HB_PCLK(2, 0);
   {  // the records to the workspace (coalesced), complete before the barrier
     double* dst = reinterpret_cast<double*>(pa.wc) + (size_t)base * kWcDoubles;
     constexpr int U = (WPB * kWcDoubles + NT - 1) / NT;
@@ -1604,6 +1703,7 @@ __device__ __forceinline__ void fused_prologue(const PreArgs& pa, int count, int
   }
   __builtin_amdgcn_s_waitcnt(0);  // the stores acknowledged (L2) before any wave's scalar loads
   __syncthreads();
+  HB_PCLK(3, 0);
 }
 
 // MULTI (catalog mode): the walker is list[blockIdx.x] and its light curve is
@@ -1733,11 +1833,17 @@ __global__ __launch_bounds__(64 * WPB * WPW) HB_WPE_ATTR void hb_eval_wave_kerne
       // the eclipse queue shares the select's candidate area (dead until the select)
       double* eq_dr = reinterpret_cast<double*>(smem + slab_bytes);
       int* eq_code = reinterpret_cast<int*>(eq_dr + kEclQ + 1);
+#if HB_PIPE && HB_CHAIN_SPLIT && HB_GQ && !defined(HB_CLK_STEP0) && !HB_ABLATE_MODEL
+      (void)eq_dr;
+      (void)eq_code;
+      model_pass_chain_pipe<VPT, NR>(tT, ph, (int)n, rw, w, vals, lane, row, pc, dq);
+#else
       model_pass_chain<VPT, NR>(tT, ph, (int)n, rw, w, vals, eq_dr, eq_code, lane, row, pc, dq
 #ifdef HB_CLK_STEP0
                             , clkm_[3]
 #endif
                             );
+#endif
     } else {
       model_pass_cold<NR>(t, ph, (int)n, rw, w, vals, row, pc, dq);
     }
@@ -2527,7 +2633,8 @@ hipError_t launch_eval(const EvalPlan& pl, const double* t, const double2* ph, c
       case 4: return launch_wave_acc_t<4>(pl, t, ph, f, sg, rows, wc, nwalk, logl, s, *acc, dq);
       case 8: return launch_wave_acc_t<8>(pl, t, ph, f, sg, rows, wc, nwalk, logl, s, *acc, dq);
       case 16: return launch_wave_acc_t<16>(pl, t, ph, f, sg, rows, wc, nwalk, logl, s, *acc, dq);
-      case 32: return launch_wave_acc_t<32>(pl, t, ph, f, sg, rows, wc, nwalk, logl, s, *acc, dq);
+      // 32 cadences per lane: the epilogue's registers would spill (22 VGPRs):
+      // the device sampler launches ds_accept (hbx_loglik_accept_dev returns 1)
       default: return hipErrorNotSupported;
     }
   }
@@ -2544,16 +2651,25 @@ hipError_t launch_eval(const EvalPlan& pl, const double* t, const double2* ph, c
   if (pl.bvpt > 0) {
 #define HB_BCASE(NWV, V)                                                                    \
   if (pl.nw == NWV && pl.bvpt == V) return launch_block_t<NWV, V>(pl, t, ph, f, sg, wc, nwalk, logl, tmpl, mode, s);
-    HB_BCASE(4, 8) HB_BCASE(4, 16) HB_BCASE(4, 20) HB_BCASE(4, 24) HB_BCASE(4, 32)
-    HB_BCASE(8, 8) HB_BCASE(8, 16) HB_BCASE(8, 20) HB_BCASE(8, 24) HB_BCASE(8, 32)
-    HB_BCASE(16, 8) HB_BCASE(16, 16) HB_BCASE(16, 20) HB_BCASE(16, 24) HB_BCASE(16, 32)
+    HB_BCASE(4, 8) HB_BCASE(4, 16) HB_BCASE(4, 20)
+    HB_BCASE(8, 8) HB_BCASE(8, 16) HB_BCASE(8, 20)
+    HB_BCASE(16, 8) HB_BCASE(16, 16) HB_BCASE(16, 20)
 #undef HB_BCASE
     return hipErrorInvalidValue;
   }
+  // the template in LDS always takes the register-key block kernel above
+  // (HB_BLOCK_KEYS); the LDS-walking select is built only without it
+#if HB_BLOCK_KEYS
+#define HB_CASE(NWV)                                                                              \
+  case NWV:                                                                                       \
+    return pl.lds ? hipErrorInvalidValue                                                          \
+                  : launch_eval_t<NWV, false>(pl, t, ph, f, sg, wc, nwalk, logl, tmpl, scratch, mode, s);
+#else
 #define HB_CASE(NWV)                                                                              \
   case NWV:                                                                                       \
     return pl.lds ? launch_eval_t<NWV, true>(pl, t, ph, f, sg, wc, nwalk, logl, tmpl, scratch, mode, s) \
                   : launch_eval_t<NWV, false>(pl, t, ph, f, sg, wc, nwalk, logl, tmpl, scratch, mode, s);
+#endif
   switch (pl.nw) {
     HB_CASE(1)
     HB_CASE(2)
@@ -2747,8 +2863,11 @@ EvalPlan make_block_plan(long n) {
     const long per = (n + 64L * nw - 1) / (64L * nw);  // cadences per thread
     if (per <= 32 && need >= sizeof(SelShared) + (4u << kSelBits) + 8 * kCandMax)
       // exact fit at 17..20 (C3: N = 20 000 over 16 waves is 19.5 per thread): 24
-      // key slots there cost <16, 24> 14 VGPR spills (64 B of scratch per lane)
-      pl.bvpt = per <= 8 ? 8 : per <= 16 ? 16 : per <= 20 ? 20 : per <= 24 ? 24 : 32;
+      // key slots there cost <16, 24> 14 VGPR spills (64 B of scratch per lane).
+      // Whenever the slab fits LDS, per <= 20 (N <= 20 300 over 16 waves; fewer
+      // waves only for shorter light curves), so 24 / 32 keys are never needed
+      // (and not instantiated: they spill)
+      pl.bvpt = per <= 8 ? 8 : per <= 16 ? 16 : per <= 20 ? 20 : 0;
 #endif
   } else {
     pl.lds = false;
@@ -2772,6 +2891,11 @@ extern "C" int hb_dbg_chain_stats(unsigned long long* out, int reset) {
 #endif
 
 #ifdef HB_WAVE_CLOCKS
+extern "C" int hb_debug_prologue_clocks(unsigned long long* out, int nwg) {
+  if (nwg > 4096) nwg = 4096;
+  hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(hb_pro_clk), 16 * sizeof(unsigned long long) * nwg);
+  return e == hipSuccess ? 0 : -1;
+}
 extern "C" int hb_debug_wave_clocks(unsigned long long* out, int nwaves) {
   if (nwaves > 65536) nwaves = 65536;
   hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(hb_wave_clk), 8 * sizeof(unsigned long long) * nwaves);

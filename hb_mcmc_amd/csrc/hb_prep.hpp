@@ -24,6 +24,12 @@
 #include "hb_device.hpp"
 #include "hb_internal.hpp"
 
+// experiment builds only (HB_WAVE_CLOCKS, hb_kernels.hip): shader-clock marks
+// of the prep roles, mark i of the calling wave's lane 0
+#ifndef HB_PREP_MARK
+#define HB_PREP_MARK(i) do { } while (0)
+#endif
+
 namespace hbk {
 
 using namespace hbdev;
@@ -101,6 +107,7 @@ __device__ __forceinline__ void prep_records(PrepShared<NW>& L, int nb, const Ma
   }
   const double pd = exp10(p[2]);
   const double e = p[3];
+  HB_PREP_MARK(5 + wv);  // phase 1 computed (values in registers / LDS stores issued)
   __syncthreads();
   const int o = star ^ 1;
   const double r = L.xs[star][1][jc], tk = L.xs[star][2][jc], ab = L.xs[star][3][jc];
@@ -200,6 +207,7 @@ __device__ __forceinline__ void prep_records(PrepShared<NW>& L, int nb, const Ma
     }
     slack();
   }
+  HB_PREP_MARK(9 + wv);  // phase 2 computed
   __syncthreads();  // star-2 terms and the Gaia term are in LDS
   if (wv == 0 && live) {
     double tt[12];
@@ -242,6 +250,7 @@ __device__ __forceinline__ void prep_records(PrepShared<NW>& L, int nb, const Ma
     wc->tune = p[20];
     wc->chi2_extra = gr * gr;
   }
+  HB_PREP_MARK(13);  // wave 0: records combined (other waves: no-op)
   __syncthreads();
 }
 

@@ -16,6 +16,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--ncad", type=int, default=1024)
 ap.add_argument("--walkers", type=int, default=4096)
 ap.add_argument("--reps", type=int, default=20)
+ap.add_argument("--fused", action="store_true", help="time hb_loglik_batch_dev (the fused launch when it applies)")
 a = ap.parse_args()
 n, w = a.ncad, a.walkers
 t = synth.cadences(n)
@@ -29,10 +30,27 @@ P = torch.from_numpy(synth.walkers(w, seed=1000)).cuda()
 out = torch.empty(w, dtype=torch.float64, device="cuda")
 st = torch.cuda.current_stream()
 for _ in range(a.reps):
-    L.prepare_dev(P, st)
-    L.evaluate_dev(w, out, 0, st)
+    if a.fused:
+        L.loglike_dev(P, out, st)
+    else:
+        L.prepare_dev(P, st)
+        L.evaluate_dev(w, out, 0, st)
 torch.cuda.synchronize()
 lib = _lib.lib()
+prologue = None
+if a.fused and L.fused_wpb(w) > 0:  # the fused prologue's marks, wave 0 of every workgroup
+    nwg = (w + L.fused_wpb(w) - 1) // L.fused_wpb(w)
+    pb = (C.c_ulonglong * (16 * nwg))()
+    assert lib.hb_debug_prologue_clocks(pb, nwg) == 0
+    pc = np.frombuffer(pb, dtype=np.uint64).reshape(nwg, 16).astype(np.int64)
+    d = pc[:, 1:14] - pc[:, 0:1]
+    prologue = {"workgroups": int(nwg), "marks": ["params in LDS", "records in LDS", "after last barrier",
+                                                  "table waves done"] +
+                                                 [f"role {r} phase 1 done" for r in range(4)] +
+                                                 [f"role {r} phase 2 done" for r in range(4)] + ["records combined"],
+                "mean_cycles_from_entry": [float(x) for x in d.mean(axis=0)],
+                "max_cycles_from_entry": [float(x) for x in d.max(axis=0)],
+                "entry_spread_cycles": float(pc[:, 0].max() - pc[:, 0].min())}
 buf = (C.c_ulonglong * (8 * w))()
 assert lib.hb_debug_wave_clocks(buf, w) == 0
 c = np.frombuffer(buf, dtype=np.uint64).reshape(w, 8).astype(np.int64)
@@ -76,5 +94,16 @@ for k in np.unique(key):
     m = key == k
     starts.append(np.sort(t0[m] - t0[m].min()))
 res["start_stagger_mean"] = [float(np.mean([s[i] for s in starts if len(s) > i])) for i in range(4)]
+if prologue is not None:  # per workgroup: entry (prologue mark 0) to its last wave's end
+    wpb = L.fused_wpb(w)
+    ent = pc[:, 0]
+    wg = np.arange(w) // wpb
+    ends_wg = np.array([t1[wg == g].max() for g in range(len(ent))])
+    starts_wg = np.array([t0[wg == g].min() for g in range(len(ent))])
+    prologue["wg_entry_to_first_eval_start_mean"] = float((starts_wg - ent).mean())
+    prologue["wg_entry_to_last_end_mean"] = float((ends_wg - ent).mean())
+    prologue["wg_entry_to_last_end_max"] = float((ends_wg - ent).max())
+    prologue["kernel_span_cycles"] = float(ends_wg.max() - ent.min())
+res["prologue"] = prologue
 print(json.dumps(res, indent=1))
 L.close()
