@@ -291,9 +291,13 @@ extern "C" hb_ctx* hb_create(const double* t, const double* f, const double* sig
     hb_destroy(c.release());
     return nullptr;
   }
-  if (c->plan.vpt > 0) {
-    std::vector<double> rows((size_t)hbk::wave_rows_doubles(n));
-    hbk::build_rows(t, f, s.data(), n, rows.data());
+  // lane-row arrays: the one-wave path's rows, or the NW-wave path's 64 nw
+  // rows (its warm-chain model pass)
+  static const bool block_chain = getenv("HB_BLOCK_CHAIN") == nullptr || atoi(getenv("HB_BLOCK_CHAIN")) != 0;
+  if (c->plan.vpt == 0 && c->plan.bvpt > 0 && block_chain) c->plan.brows = 64 * c->plan.nw;
+  if (c->plan.vpt > 0 || c->plan.brows > 0) {
+    std::vector<double> rows((size_t)hbk::wave_rows_doubles(n, c->plan.brows));
+    hbk::build_rows(t, f, s.data(), n, rows.data(), c->plan.brows);
     if (hipMalloc(&c->d_rows, sizeof(double) * rows.size()) != hipSuccess ||
         hipMemcpy(c->d_rows, rows.data(), sizeof(double) * rows.size(), hipMemcpyHostToDevice) != hipSuccess) {
       set_err_msg("hb_create: lane-row arrays: hipMalloc/upload failed");
@@ -333,6 +337,11 @@ extern "C" int hb_ctx_fused_wpb(const hb_ctx* c, int w) {
 extern "C" int hb_ctx_eval_kind(const hb_ctx* c) {
   if (!c) return -1;
   return c->plan.vpt > 0 ? 0 : c->plan.bvpt > 0 ? 1 : 2;
+}
+
+extern "C" int hb_ctx_block_rows(const hb_ctx* c) {
+  if (!c) return -1;
+  return c->plan.vpt > 0 ? 0 : c->plan.brows;
 }
 
 static int run_batch(hb_ctx* c, const double* d_params, int w, double* d_logl, double* d_tmpl,
@@ -739,12 +748,22 @@ static int catalog_layout(hb_catalog* c, const int* walkers, hipStream_t s) {
   return 0;
 }
 
+// One catalog call.  Every class launches on its stream at once (forked at
+// the call's start): a one-wave class of up to 16 cadences per lane is ONE
+// fused launch (its walkers' records in the eval kernel's prologue), the pair
+// class and the one-wave class of 32 cadences per lane a records launch for
+// their walkers (launch_prep_list) then the eval.  The evals evaluate the
+// per-target phase-table entries in place (no table launch).  HB_CAT_FUSED=0
+// (A/B knob): one records launch for every walker first, then the classes.
 static int catalog_run(hb_catalog* c, const double* d_params, double* d_logl, hipStream_t s) {
   if (c->total == 0) return 0;
-  MagArgs unused{};
-  HB_TRY(hbk::launch_prep(d_params, c->total, unused, c->d_wc, s, c->d_tab, c->d_wt, c->d_t, 0, c->d_ph, c->d_w0,
-                          c->ntargets),
-         "prep launch");
+  static const bool fused = cat_env("HB_CAT_FUSED", 1) != 0;
+  if (!fused) {
+    MagArgs unused{};
+    HB_TRY(hbk::launch_prep(d_params, c->total, unused, c->d_wc, s, c->d_tab, c->d_wt, c->d_t, 0, c->d_ph, c->d_w0,
+                            c->ntargets),
+           "prep launch");
+  }
   // classes by descending work, dealt round-robin over the caller's stream
   // and the forked ones
   int order[kCatClasses], nc = 0;
@@ -752,8 +771,8 @@ static int catalog_run(hb_catalog* c, const double* d_params, double* d_logl, hi
     if (c->class_off[cl + 1] > c->class_off[cl]) order[nc++] = cl;
   std::sort(order, order + nc, [&](int a, int b) { return c->class_work[a] > c->class_work[b]; });
   // two streams: C5 0.164 ms per call against 0.183 on four and 0.196 on one
-  // (profiles/r04/r04c_bench_c5_s*.json: the forked streams' event waits cost
-  // more than the extra overlap buys)
+  // (profiles/r04/r04c_bench_c5_s*.json, two-launch path: the forked streams'
+  // event waits cost more than the extra overlap buys)
   static const int kns = std::max(1, std::min(kCatStreams, cat_env("HB_CAT_STREAMS", kCatDefaultStreams)));
   const int ns = nc < kns ? nc : kns;
   if (ns > 1) {
@@ -771,9 +790,25 @@ static int catalog_run(hb_catalog* c, const double* d_params, double* d_logl, hi
       wpw = 2;
     }
     hipStream_t sj = (j % ns == 0) ? s : c->aux[j % ns - 1];
+    const int* lst = c->d_list + c->class_off[cl];
+    double* dq = reinterpret_cast<double*>(reinterpret_cast<unsigned char*>(c->d_dq) + c->class_dq[cl]);
+    if (fused && wpw == 1 && vpt <= 16) {
+      hbk::PreArgs pa{};
+      pa.params = d_params;
+      pa.wc = c->d_wc;
+      pa.list = lst;
+      pa.wt = c->d_wt;
+      pa.tab = c->d_tab;
+      pa.w0 = c->d_w0;
+      HB_TRY(hbk::launch_eval_multi_fused(vpt, c->class_slab[cl], pa, c->d_t, c->d_f, c->d_s, c->d_rows, cnt, d_logl,
+                                          sj, dq),
+             "fused eval launch");
+      continue;
+    }
+    if (fused)
+      HB_TRY(hbk::launch_prep_list(d_params, lst, cnt, c->d_wc, sj, c->d_tab, c->d_wt, c->d_w0), "records launch");
     HB_TRY(hbk::launch_eval_multi(vpt, c->class_slab[cl], c->d_t, c->d_ph, c->d_f, c->d_s, c->d_rows, c->d_tab, c->d_wt,
-                                  c->d_list + c->class_off[cl], cnt, c->d_wc, d_logl, sj,
-                                  reinterpret_cast<double*>(reinterpret_cast<unsigned char*>(c->d_dq) + c->class_dq[cl]), wpw),
+                                  lst, cnt, c->d_wc, d_logl, sj, dq, wpw),
            "eval launch");
   }
   for (int i = 0; i < ns - 1; ++i) {

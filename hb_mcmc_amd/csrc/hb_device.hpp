@@ -222,15 +222,24 @@ __device__ __forceinline__ Stellar stellar_of(const double* p) {
 
 // Gaia-band (673 nm) magnitude of both stars (calc_mags, :725-795) and the
 // full 4-band version for the C-ABI.  R in Rsun, T in K, dist in pc.
-__device__ __forceinline__ double band_flux(double lam_nm, double r1cm, double r2cm, double t1,
-                                            double t2, double dist, double blend) {
-  const double hp = 6.626e-27, kb = 1.38e-16, pc = 3.086e18;
+// one star's Planck factor of band_flux: pre / (exp(h nu / (k T)) - 1)
+__device__ __forceinline__ double band_term(double lam_nm, double t) {
+  const double hp = 6.626e-27, kb = 1.38e-16;
   double fr = kC / (lam_nm * 1e-7);
   double pre = 2.0 * hp * (fr * fr * fr) / (kC * kC);
-  double f = kPi * (r1cm * r1cm * (pre / (exp(hp * fr / (kb * t1)) - 1.0)) +
-                    r2cm * r2cm * (pre / (exp(hp * fr / (kb * t2)) - 1.0))) /
-             ((dist * dist) * (pc * pc));
+  return pre / (exp(hp * fr / (kb * t)) - 1.0);
+}
+// band_flux from both stars' Planck factors (the prep computes each in the
+// wave that has its star's temperature)
+__device__ __forceinline__ double band_flux_terms(double r1cm, double r2cm, double bt1, double bt2, double dist,
+                                                  double blend) {
+  const double pc = 3.086e18;
+  double f = kPi * (r1cm * r1cm * bt1 + r2cm * r2cm * bt2) / ((dist * dist) * (pc * pc));
   return f / (1.0 - blend);
+}
+__device__ __forceinline__ double band_flux(double lam_nm, double r1cm, double r2cm, double t1,
+                                            double t2, double dist, double blend) {
+  return band_flux_terms(r1cm, r2cm, band_term(lam_nm, t1), band_term(lam_nm, t2), dist, blend);
 }
 __device__ __forceinline__ double ab_mag(double f) { return -2.5 * log10(f) - 48.6; }
 
@@ -254,9 +263,17 @@ struct StarCoef {
   double kb, am1, am2, c21, am3, c22, c4, s1, s3, kref;
 };
 
-__device__ __forceinline__ StarCoef star_coef(double pd, double ma, double mb, double e, double si,
-                                              double rk, double rc, double mu, double tau,
-                                              double aref, double ab) {
+// star_coef in three steps, for the prep's lane layout: star_coef_x holds
+// everything that needs neither radius (the factors in front of each
+// coefficient's R^k), star_coef_r multiplies the star's own radius in, and
+// star_coef_finish the companion's radius (reflection) and alpha_beam
+// (beaming).  Each coefficient's operations and their order are those of the
+// one-expression form (left to right: the R^k factor and ppm come last).
+struct StarCoefX {
+  double kb, am1, am2, c21, a3, a22, a4, x5, b1, b3, x4, kref;
+};
+__device__ __forceinline__ StarCoefX star_coef_x(double pd, double ma, double mb, double e, double si, double mu,
+                                                 double tau, double aref) {
   const double ppm = 1.e-6;
   const double s2 = si * si, s3 = s2 * si, s4 = s3 * si;
   const double cP = cbrt(pd);
@@ -268,30 +285,62 @@ __device__ __forceinline__ StarCoef star_coef(double pd, double ma, double mb, d
   const double cM = cbrt(ma);
   const double cq = cbrt(opq);
   const double inv_ma = 1.0 / ma;
-  StarCoef c;
+  StarCoefX x;
   // beaming: pow(1+q, 2/3) is integer 2/3 == 0 in the reference -> factor 1
-  c.kb = -2830. * ab * q * cM / cP * si / sqrt(1.0 - e * e) * ppm;
+  x.kb = -2830. * q * cM / cP * si / sqrt(1.0 - e * e) * ppm;
   const double a11 = 15 * mu * (2 + tau) / (32 * (3 - mu));
   const double a21 = 3 * (15 + mu) * (1 + tau) / (20 * (3 - mu));
   const double a2b = 15 * (1 - mu) * (3 + tau) / (64 * (3 - mu));
   const double a01 = a21 / 9, a0b = 3 * a2b / 20, a31 = 5 * a11 / 3, a41 = 7 * a2b / 4;
   const double qq = q / opq;
+  x.am1 = 26870 * a01 * (2 - 3 * s2) * inv_ma / (prot * prot);
+  x.am2 = 40305 * a01 * (2 - 3 * s2) * inv_ma * qq * (inv_pd * inv_pd);
+  x.c21 = 13435 * a21 * s2 * inv_ma * qq * (inv_pd * inv_pd);
+  // M^-5/3 q/(1+q)^5/3 P^-10/3 (x R^5 ppm)
+  x.x5 = qq / (cq * cq) * inv_ma / (cM * cM) * (inv_pd * inv_pd * inv_pd) / cP;
+  x.a3 = 759 * a0b * (8 - 40 * s2 + 35 * s4);
+  x.a22 = 759 * a2b * (6 * s2 - 7 * s4);
+  x.a4 = 759 * a41 * s4;
+  // M^-4/3 q/(1+q)^4/3 P^-8/3 (x R^4 ppm)
+  x.x4 = qq / cq * inv_ma / cM * (inv_pd * inv_pd) / (cP * cP);
+  x.b1 = 3194 * a11 * (4 * si - 5 * s3);
+  x.b3 = 3194 * a31 * s3;
+  // reflection: (1+q)^-2/3 M^-2/3 P^-4/3 (Rc^2 ppm: star_coef_finish)
+  x.kref = 56514 * aref / (cq * cq) / (cM * cM) * inv_pd / cP;
+  return x;
+}
+__device__ __forceinline__ StarCoef star_coef_r(const StarCoefX& x, double rk) {
+  const double ppm = 1.e-6;
   const double rk3 = rk * rk * rk;
-  c.am1 = 26870 * a01 * (2 - 3 * s2) * inv_ma / (prot * prot) * rk3 * ppm;
-  c.am2 = 40305 * a01 * (2 - 3 * s2) * inv_ma * qq * (inv_pd * inv_pd) * rk3 * ppm;
-  c.c21 = 13435 * a21 * s2 * inv_ma * qq * (inv_pd * inv_pd) * rk3 * ppm;
-  // M^-5/3 q/(1+q)^5/3 P^-10/3 R^5
-  const double c5 = qq / (cq * cq) * inv_ma / (cM * cM) * (inv_pd * inv_pd * inv_pd) / cP *
-                    (rk3 * rk * rk) * ppm;
-  c.am3 = 759 * a0b * (8 - 40 * s2 + 35 * s4) * c5;
-  c.c22 = 759 * a2b * (6 * s2 - 7 * s4) * c5;
-  c.c4 = 759 * a41 * s4 * c5;
-  // M^-4/3 q/(1+q)^4/3 P^-8/3 R^4
-  const double c4c = qq / cq * inv_ma / cM * (inv_pd * inv_pd) / (cP * cP) * (rk3 * rk) * ppm;
-  c.s1 = 3194 * a11 * (4 * si - 5 * s3) * c4c;
-  c.s3 = 3194 * a31 * s3 * c4c;
-  // reflection: (1+q)^-2/3 M^-2/3 P^-4/3 Rc^2
-  c.kref = 56514 * aref / (cq * cq) / (cM * cM) * inv_pd / cP * (rc * rc) * ppm;
+  StarCoef c;
+  c.kb = x.kb;
+  c.am1 = x.am1 * rk3 * ppm;
+  c.am2 = x.am2 * rk3 * ppm;
+  c.c21 = x.c21 * rk3 * ppm;
+  const double c5 = x.x5 * (rk3 * rk * rk) * ppm;
+  c.am3 = x.a3 * c5;
+  c.c22 = x.a22 * c5;
+  c.c4 = x.a4 * c5;
+  const double c4c = x.x4 * (rk3 * rk) * ppm;
+  c.s1 = x.b1 * c4c;
+  c.s3 = x.b3 * c4c;
+  c.kref = x.kref;
+  return c;
+}
+__device__ __forceinline__ StarCoef star_coef_pre(double pd, double ma, double mb, double e, double si,
+                                                  double rk, double mu, double tau, double aref) {
+  return star_coef_r(star_coef_x(pd, ma, mb, e, si, mu, tau, aref), rk);
+}
+__device__ __forceinline__ void star_coef_finish(StarCoef& c, double rc, double ab) {
+  const double ppm = 1.e-6;
+  c.kb = ab * c.kb;
+  c.kref = c.kref * (rc * rc) * ppm;
+}
+__device__ __forceinline__ StarCoef star_coef(double pd, double ma, double mb, double e, double si,
+                                              double rk, double rc, double mu, double tau,
+                                              double aref, double ab) {
+  StarCoef c = star_coef_pre(pd, ma, mb, e, si, rk, mu, tau, aref);
+  star_coef_finish(c, rc, ab);
   return c;
 }
 

@@ -576,7 +576,7 @@ __global__ __launch_bounds__(64 * kPW) HB_DS_PROPOSE_ATTR void ds_propose(Dev D,
   hbk::prep_records<kPW>(PL, nb, D.ma, nullptr, nullptr, 0, [&](int) { return pc_tab; }, [] {});
   for (int q = threadIdx.x; q < nb * hbk::kWcDoubles; q += 64 * kPW) {
     const int w = q / hbk::kWcDoubles, f = q - w * hbk::kWcDoubles;
-    D.wc[(size_t)jl_s[w] * hbk::kWcDoubles + f] = PL.so[q];
+    D.wc[(size_t)jl_s[w] * hbk::kWcDoubles + f] = PL.so[w * hbk::kSoStride + f];
   }
 }
 

@@ -43,6 +43,8 @@ struct EvalPlan {
   bool lds = true;     // template in LDS (else HBM scratch slab)
   size_t lds_bytes = 0;
   double gap = 0.0;    // typical cadence spacing [d] (hb_cadence_gap), warm-chain gate
+  int brows = 0;       // >0: the NW-wave path's lane rows (64 nw) of the context's lane-row
+                       // arrays -- its warm-chain model pass; 0: strided cold pass only
 };
 
 // One light curve of a catalog (hb_catalog_*): its slice of the concatenated
@@ -98,6 +100,10 @@ hipError_t launch_prep(const double* d_params, int nwalk, const MagArgs& ma, hbd
                        hipStream_t s, const TargetDesc* tab = nullptr, const int* wt = nullptr,
                        const double* t = nullptr, long n = 0, double2* ph = nullptr, const int* w0 = nullptr,
                        int ntargets = 0, double* tab_pc = nullptr);
+// catalog mode: records of the walkers list[0..count) (one size class; the
+// per-target tables are not written: the catalog's evals evaluate them in place)
+hipError_t launch_prep_list(const double* d_params, const int* list, int count, hbdev::WalkerConst* d_wc,
+                            hipStream_t s, const TargetDesc* tab, const int* wt, const int* w0);
 // catalog mode: walkers list[0..count) of one size class (cadences per lane
 // vpt), each reading its target's slice through tab[wt[walker]]
 // (wpw = 2: a pair of waves per walker, vpt the cadences per lane of 128 rows)
@@ -115,12 +121,25 @@ struct PreArgs {
   hbdev::WalkerConst* wc;   // records out (then read back by the eval waves)
   double2* ph;              // the global phase table (each workgroup writes a slice)
   double* tab_pc;           // its period [s]
+  // catalog mode (launch_eval_multi_fused): the walkers of the launch are
+  // list[0..count), each of target wt[walker] (magnitudes in tab[]); a walker
+  // uses the phase table of its target's first walker w0[target] (evaluated
+  // in place, hbk vt_entry; ph / tab_pc unused)
+  const int* list;
+  const int* wt;
+  const TargetDesc* tab;
+  const int* w0;
 };
 // walkers per workgroup of the fused launch for w walkers on `cus` CUs (0: the
 // two-launch path: prep + eval)
 int fused_wpb(const EvalPlan& pl, int w, int cus);
 hipError_t launch_eval_fused(const EvalPlan& pl, int wpb, const PreArgs& pa, const double* t, const double* f,
                              const double* sg, const double* rows, int nwalk, double* logl, hipStream_t s, double* dq);
+// catalog mode, one size class of one-wave walkers (cadences per lane vpt <=
+// 16), records in the prologue: pa.list / wt / tab / w0 set, count walkers
+hipError_t launch_eval_multi_fused(int vpt, size_t slab, const PreArgs& pa, const double* t, const double* f,
+                                   const double* sg, const double* rows, int count, double* logl, hipStream_t s,
+                                   double* dq);
 int wave_vpt_for(long n);  // cadences per lane of the one-wave path, 0 if n > 2048
 int wave_nr_for(long n);   // lane rows per walker: 64, or 128 (a pair of waves) for 1024 < n <= 2048
 // device bytes of the one-wave kernel's deferred cadence queue for `count`
@@ -129,8 +148,9 @@ size_t wave_queue_bytes(int vpt, long count, int wpw = 1);
 size_t wave_slab_bytes(long n);
 size_t wave_lds_bytes(size_t slab, int vpt, int wpw = 1);
 // t, f, 1/sigma in the one-wave kernel's lane-row order (3 x nr x ceil(n/nr) doubles)
-long wave_rows_doubles(long n);
-void build_rows(const double* t, const double* f, const double* isg, long n, double* out);
+// (nr > 0: that many rows instead, the NW-wave path's 64 nw)
+long wave_rows_doubles(long n, long nr = 0);
+void build_rows(const double* t, const double* f, const double* isg, long n, double* out, long nr = 0);
 // acc (device sampler, one-wave path only): each wave also runs its slot's
 // Hastings test and history write (hb_accept.hpp); hipErrorNotSupported on the
 // multi-wave path

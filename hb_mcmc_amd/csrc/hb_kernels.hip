@@ -139,7 +139,11 @@ constexpr int kPrepThreads = 64 * kPrepRoles;
 
 // NW walkers per workgroup: kPrepWalkers, or 32 / 64 for batches that still
 // fill 256 workgroups with them (C4, C5: one round instead of two or four)
-template <int NW>
+// LIST (catalog, one size class): the launch's walkers are list[0..nwalk),
+// their magnitude data gathered into LDS; a walker's table period is its
+// target's first walker's (the catalog's evals evaluate the table entries in
+// place, so no table is written)
+template <int NW, bool LIST = false>
 __global__ __launch_bounds__(kPrepThreads) void hb_prep_kernel(const double* __restrict__ params,
                                                               int nwalk, MagArgs ma,
                                                               WalkerConst* __restrict__ out,
@@ -148,14 +152,29 @@ __global__ __launch_bounds__(kPrepThreads) void hb_prep_kernel(const double* __r
                                                               const double* __restrict__ tcad, int ncad,
                                                               double2* __restrict__ ph,
                                                               const int* __restrict__ w0, int ntargets,
-                                                              double* __restrict__ tab_pc_out) {
+                                                              double* __restrict__ tab_pc_out,
+                                                              const int* __restrict__ list) {
   constexpr int kPrepWalkers = NW;
   __shared__ PrepShared<kPrepWalkers> L;
+  __shared__ double mg_s[LIST ? 3 * NW : 1];
+  __shared__ int wl_s[LIST ? NW : 1], wtl_s[LIST ? NW : 1];
   const int G = (int)gridDim.x;
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int base = blockIdx.x * kPrepWalkers;
   const int nb = min(kPrepWalkers, nwalk - base);
+  if constexpr (LIST) {
+    if (tid < NW) {
+      const int wk = tid < nb ? list[base + tid] : 0;
+      const int tg = wt[wk];
+      wl_s[tid] = wk;
+      wtl_s[tid] = tg;
+      mg_s[tid] = tab[tg].dist;
+      mg_s[NW + tid] = tab[tg].gmag;
+      mg_s[2 * NW + tid] = tab[tg].gerr;
+    }
+    __syncthreads();
+  }
   // wave 2 writes a single context's shared-period phase table in its slack;
   // its first operands are in flight with the parameters
   const bool tabwave = ph != nullptr && tab == nullptr && (tid >> 6) == 2;
@@ -171,7 +190,12 @@ __global__ __launch_bounds__(kPrepThreads) void hb_prep_kernel(const double* __r
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int i = tid + u * kPrepThreads;
-      v[u] = i < nb * kNpars ? params[(size_t)base * kNpars + i] : 0.0;
+      if constexpr (LIST) {
+        const int j = i / kNpars;
+        v[u] = i < nb * kNpars ? params[(size_t)wl_s[j] * kNpars + (i - j * kNpars)] : 0.0;
+      } else {
+        v[u] = i < nb * kNpars ? params[(size_t)base * kNpars + i] : 0.0;
+      }
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -183,6 +207,7 @@ __global__ __launch_bounds__(kPrepThreads) void hb_prep_kernel(const double* __r
   // the table period: walker 0's (single context) or the first walker's of
   // the walker's target in this batch (catalog)
   auto tab_pc = [&](int j) -> double {
+    if constexpr (LIST) return exp10(params[(size_t)w0[wtl_s[j]] * kNpars + 2]) * kDay;
     if (ph == nullptr) return __builtin_nan("");
     return exp10(params[(tab ? (size_t)w0[wt[base + j]] * kNpars : 0) + 2]) * kDay;
   };
@@ -201,7 +226,10 @@ __global__ __launch_bounds__(kPrepThreads) void hb_prep_kernel(const double* __r
       if (i + G * 64 < ncad) ti = tcad[i + G * 64];
     }
   };
-  prep_records<kPrepWalkers>(L, nb, ma, tab, wt, base, tab_pc, slack);
+  if constexpr (LIST)
+    prep_records<kPrepWalkers>(L, nb, ma, nullptr, nullptr, 0, tab_pc, slack, PrepNoIdle(), mg_s);
+  else
+    prep_records<kPrepWalkers>(L, nb, ma, tab, wt, base, tab_pc, slack);
   {
     double* dst = reinterpret_cast<double*>(out) + (size_t)base * kWcDoubles;
     constexpr int U = (kPrepWalkers * kWcDoubles + kPrepThreads - 1) / kPrepThreads;
@@ -209,14 +237,23 @@ __global__ __launch_bounds__(kPrepThreads) void hb_prep_kernel(const double* __r
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int i = tid + u * kPrepThreads;
-      v[u] = i < nb * kWcDoubles ? L.so[i] : 0.0;
+      const int jw = i / kWcDoubles;  // record rows of kSoStride doubles in LDS
+      v[u] = i < nb * kWcDoubles ? L.so[jw * kSoStride + (i - jw * kWcDoubles)] : 0.0;
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int i = tid + u * kPrepThreads;
-      if (i < nb * kWcDoubles) dst[i] = v[u];
+      if (i < nb * kWcDoubles) {
+        if constexpr (LIST) {
+          const int j = i / kWcDoubles;
+          reinterpret_cast<double*>(out)[(size_t)wl_s[j] * kWcDoubles + (i - j * kWcDoubles)] = v[u];
+        } else {
+          dst[i] = v[u];
+        }
+      }
     }
   }
+  if constexpr (LIST) return;
   // Catalog phase table (WalkerConst::tab), written after the walker records
   // so its latency overlaps their stores: per target k, for the period of its
   // first walker w0[k] in this batch (-1: no walkers), ph[i] = (sin, cos)(t_i
@@ -580,18 +617,29 @@ struct Pacer {
   }
 };
 
+// Virtual phase table (VT): the entry (sin, cos)(t DAY 2pi/P0) a walker on
+// the table period (w.tab = 1: its Pc equals P0 bit for bit, so w.mA is
+// 2pi/P0 computed the same way) would read, evaluated in place with the
+// expression the prep writes the table with -- bit-identical, no table in
+// memory (the catalog's fused launches, whose workgroups mix targets)
+__device__ __forceinline__ double2 vt_entry(double t, const WalkerConst& w) {
+  double sv, cv;
+  sincos_table((t * kDay) * w.mA, sv, cv);
+  return make_double2(sv, cv);
+}
+
 // Cold path in the one-wave kernel: the wave sweeps the light curve 64*K
 // consecutive cadences at a time (cadence base + k*64 + lane), so the eclipse
 // lanes of an iteration are neighbours in phase and the inline eclipse term
 // runs only on the few iterations that cross an eclipse.  Values are stored
 // at the lane-row slab positions (slab_pos_of) that the key load reads.
 // NT threads per walker (64, or 128 for a pair of waves), thread tid
-template <int NT = 64>
+template <int NT = 64, bool VT = false>
 __device__ __forceinline__ void model_pass_cold(const double* __restrict__ t, const double2* __restrict__ ph,
                                                 int n, const Rows& rw, const WalkerConst& w, double* vals,
                                                 int lane, Pacer pc, DeferQ& dq) {
   constexpr int K = HB_K;
-  const bool tab = (ph != nullptr) && (w.tab != 0.0);  // walker-uniform
+  const bool tab = (VT || ph != nullptr) && (w.tab != 0.0);  // walker-uniform
   const int last = n - 1;
   const int nit = (n + K * NT - 1) / (K * NT);
   pc.begin(nit);
@@ -603,7 +651,7 @@ __device__ __forceinline__ void model_pass_cold(const double* __restrict__ t, co
     for (int k = 0; k < K; ++k) {
       const int i = min(base + k * NT + lane, last);
       tk[k] = t[i];
-      pk[k] = tab ? ph[i] : make_double2(0.0, 1.0);
+      pk[k] = tab ? (VT ? vt_entry(tk[k], w) : ph[i]) : make_double2(0.0, 1.0);
     }
     bool bad;
 #if HB_SPLIT_LIVE
@@ -774,7 +822,7 @@ __device__ __forceinline__ void model_pass_chain(const double* __restrict__ tT, 
 #ifndef HB_PIPE
 #define HB_PIPE 1
 #endif
-template <int VPT, int NR = 64>
+template <int VPT, int NR = 64, bool VT = false>
 __device__ __forceinline__ void model_pass_chain_pipe(const double* __restrict__ tT, const double2* __restrict__ ph,
                                                       int n, const Rows& rw, const WalkerConst& w, double* vals,
                                                       int lane, int row, Pacer pc, DeferQ& dq) {
@@ -782,7 +830,7 @@ __device__ __forceinline__ void model_pass_chain_pipe(const double* __restrict__
   constexpr int KCM = NR > 64 ? HB_PAIR_KC : HB_KC;
   constexpr int KC = VPT < KCM ? VPT : KCM;
   const int lc = (rw.rc + KC - 1) / KC;  // chain length (wave-uniform)
-  const bool tab = (ph != nullptr) && (w.tab != 0.0);  // walker-uniform
+  const bool tab = (VT || ph != nullptr) && (w.tab != 0.0);  // walker-uniform
   const int last = n - 1;
   const int base = row * rw.rc;
   const int rs = row * rw.stride, lsw = HB_ODD_STRIDE ? 0 : (row & rw.swz);  // slab_pos = rs + (c ^ lsw)
@@ -796,7 +844,8 @@ __device__ __forceinline__ void model_pass_chain_pipe(const double* __restrict__
   {  // step 0: the chains' first cadences (the reference's start, table entries)
     double2 p0[KC];
 #pragma unroll
-    for (int k = 0; k < KC; ++k) p0[k] = tab ? ph[min(base + k * lc, last)] : make_double2(0.0, 1.0);
+    for (int k = 0; k < KC; ++k)
+      p0[k] = tab ? (VT ? vt_entry(tk[k], w) : ph[min(base + k * lc, last)]) : make_double2(0.0, 1.0);
     chain_first<KC>(tk, p0, tab, w, st, pend_ok);
   }
   // store the pending step jp's values and queue its eclipse / slow-path cadences
@@ -1630,23 +1679,45 @@ __device__ __forceinline__ bool key_live(const Rows& r, int v, int lane, long n)
 // scratch aliases the waves' slabs, which the model pass only writes after
 // that barrier.
 // ---------------------------------------------------------------------------
-template <int WPB>
+template <int WPB, bool MULTI>
 __device__ __forceinline__ void fused_prologue(const PreArgs& pa, int count, int n, const double* __restrict__ t,
                                                unsigned char* smem_all, double2* tabl) {
   static_assert(WPB >= kPrepRoles && WPB <= 16, "four prep roles, <= 1024 threads");
   constexpr int NT = 64 * WPB;
   PrepShared<WPB>& L = *reinterpret_cast<PrepShared<WPB>*>(smem_all);
+  // catalog: the workgroup's walkers and their targets (past the prep scratch)
+  double* mg = reinterpret_cast<double*>(smem_all + sizeof(PrepShared<WPB>));  // [3][WPB] magnitude data
+  int* wl = reinterpret_cast<int*>(mg + 3 * WPB);
+  int* wtl = wl + WPB;
   const int tid = threadIdx.x;
   HB_PCLK(0, 0);
   const int base = blockIdx.x * WPB;
   const int nb = min(WPB, count - base);
+  if constexpr (MULTI) {
+    if (tid < WPB) {
+      const int wk = tid < nb ? pa.list[base + tid] : 0;
+      const int tg = pa.wt[wk];
+      wl[tid] = wk;
+      wtl[tid] = tg;
+      const TargetDesc& td = pa.tab[tg];
+      mg[tid] = td.dist;
+      mg[WPB + tid] = td.gmag;
+      mg[2 * WPB + tid] = td.gerr;
+    }
+    __syncthreads();
+  }
   {  // parameters, all loads in flight before the first LDS write
     constexpr int U = (WPB * kNpars + NT - 1) / NT;
     double v[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int i = tid + u * NT;
-      v[u] = i < nb * kNpars ? pa.params[(size_t)base * kNpars + i] : 0.0;
+      if constexpr (MULTI) {
+        const int j = i / kNpars;
+        v[u] = i < nb * kNpars ? pa.params[(size_t)wl[j] * kNpars + (i - j * kNpars)] : 0.0;
+      } else {
+        v[u] = i < nb * kNpars ? pa.params[(size_t)base * kNpars + i] : 0.0;
+      }
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -1654,9 +1725,13 @@ __device__ __forceinline__ void fused_prologue(const PreArgs& pa, int count, int
       if (i < nb * kNpars) L.sp[i] = v[u];
     }
   }
-  // the table period: walker 0's (hb_prep_kernel's tab_pc of a single context)
-  const double Pc0 = exp10(pa.params[2]) * kDay;
-  auto tab_pc = [&](int) -> double { return Pc0; };
+  // the table period: walker 0's (hb_prep_kernel's tab_pc of a single
+  // context), or the first walker's of the walker's target (catalog)
+  const double Pc0 = MULTI ? 0.0 : exp10(pa.params[2]) * kDay;
+  auto tab_pc = [&](int j) -> double {
+    if constexpr (MULTI) return exp10(pa.params[(size_t)pa.w0[wtl[j]] * kNpars + 2]) * kDay;
+    return Pc0;
+  };
   // (sin, cos)(t_i DAY 2pi/Pc0) for i = first, first + stride, ... < n, into
   // LDS; this workgroup's slice [lo, hi) of the cadences also to the global table
   auto table = [&](int first, int stride) {
@@ -1675,7 +1750,9 @@ __device__ __forceinline__ void fused_prologue(const PreArgs& pa, int count, int
   __syncthreads();
   HB_PCLK(1, 0);
   auto none = []() {};
-  if constexpr (WPB > kPrepRoles) {
+  if constexpr (MULTI) {  // no table: the eval waves evaluate its entries in place
+    prep_records<WPB>(L, nb, pa.ma, nullptr, nullptr, 0, tab_pc, none, PrepNoIdle(), mg);
+  } else if constexpr (WPB > kPrepRoles) {
     auto idle = [&]() {
       table(tid - 64 * kPrepRoles, NT - 64 * kPrepRoles);
       HB_PCLK(4, 64 * kPrepRoles);
@@ -1686,19 +1763,26 @@ __device__ __forceinline__ void fused_prologue(const PreArgs& pa, int count, int
     table(tid, NT);  // four waves: the table after the roles
   }
   HB_PCLK(2, 0);
-  {  // the records to the workspace (coalesced), complete before the barrier
-    double* dst = reinterpret_cast<double*>(pa.wc) + (size_t)base * kWcDoubles;
+  {  // the records to the workspace (coalesced rows), complete before the barrier
     constexpr int U = (WPB * kWcDoubles + NT - 1) / NT;
     double v[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int i = tid + u * NT;
-      v[u] = i < nb * kWcDoubles ? L.so[i] : 0.0;
+      const int jw = i / kWcDoubles;  // record rows of kSoStride doubles in LDS
+      v[u] = i < nb * kWcDoubles ? L.so[jw * kSoStride + (i - jw * kWcDoubles)] : 0.0;
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int i = tid + u * NT;
-      if (i < nb * kWcDoubles) dst[i] = v[u];
+      if (i < nb * kWcDoubles) {
+        if constexpr (MULTI) {
+          const int j = i / kWcDoubles;
+          reinterpret_cast<double*>(pa.wc)[(size_t)wl[j] * kWcDoubles + (i - j * kWcDoubles)] = v[u];
+        } else {
+          reinterpret_cast<double*>(pa.wc)[(size_t)base * kWcDoubles + i] = v[u];
+        }
+      }
     }
   }
   __builtin_amdgcn_s_waitcnt(0);  // the stores acknowledged (L2) before any wave's scalar loads
@@ -1728,8 +1812,13 @@ __global__ __launch_bounds__(64 * WPB * WPW) HB_WPE_ATTR void hb_eval_wave_kerne
     const int* __restrict__ wt, const int* __restrict__ list, hbds::AccArgs hst, int count, int lds_per,
     double* __restrict__ dqbuf, PreArgs pre) {
   static_assert(WPW == 1 || (WPW <= kMaxWPW && WPB == 1 && !ACC && HB_SEL_V == 3 && HB_GQ), "pair/rows: plain batched path");
-  static_assert(!PRE || (WPW == 1 && !MULTI && !ACC && WPB >= kPrepRoles && HB_SEL_V == 3 && HB_GQ && HB_PRIO != 2),
+  static_assert(!PRE || (WPW == 1 && !ACC && WPB >= kPrepRoles && HB_SEL_V == 3 && HB_GQ && HB_PRIO != 2),
                 "fused launch: plain one-wave batched path");
+  // the catalog evaluates its phase-table entries in place (vt_entry): a
+  // workgroup's walkers belong to several targets, and no launch writes the
+  // per-target tables
+  constexpr bool kVT = MULTI;
+  static_assert(!kVT || (HB_PIPE && HB_CHAIN_SPLIT), "the virtual table needs the pipelined chain pass");
   constexpr int NR = 64 * WPW;  // lane rows per walker
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_all[];
   const int lane = threadIdx.x & 63;
@@ -1741,7 +1830,7 @@ __global__ __launch_bounds__(64 * WPB * WPW) HB_WPE_ATTR void hb_eval_wave_kerne
   unsigned char* smem = smem_all + (size_t)wib * (size_t)lds_per;
   if constexpr (PRE) {
     double2* tabl = reinterpret_cast<double2*>(smem_all + (size_t)WPB * (size_t)lds_per);
-    fused_prologue<WPB>(pre, count, (int)n, t, smem_all, tabl);
+    fused_prologue<WPB, MULTI>(pre, count, (int)n, t, smem_all, tabl);
     // the records just written: scalar loads (constant address space), issued
     // only after the prologue's last barrier (the pointer passes through asm)
     typedef const __attribute__((address_space(4))) WalkerConst cwc_t;
@@ -1836,7 +1925,7 @@ __global__ __launch_bounds__(64 * WPB * WPW) HB_WPE_ATTR void hb_eval_wave_kerne
 #if HB_PIPE && HB_CHAIN_SPLIT && HB_GQ && !defined(HB_CLK_STEP0) && !HB_ABLATE_MODEL
       (void)eq_dr;
       (void)eq_code;
-      model_pass_chain_pipe<VPT, NR>(tT, ph, (int)n, rw, w, vals, lane, row, pc, dq);
+      model_pass_chain_pipe<VPT, NR, kVT>(tT, ph, (int)n, rw, w, vals, lane, row, pc, dq);
 #else
       model_pass_chain<VPT, NR>(tT, ph, (int)n, rw, w, vals, eq_dr, eq_code, lane, row, pc, dq
 #ifdef HB_CLK_STEP0
@@ -1845,7 +1934,7 @@ __global__ __launch_bounds__(64 * WPB * WPW) HB_WPE_ATTR void hb_eval_wave_kerne
                             );
 #endif
     } else {
-      model_pass_cold<NR>(t, ph, (int)n, rw, w, vals, row, pc, dq);
+      model_pass_cold<NR, kVT>(t, ph, (int)n, rw, w, vals, row, pc, dq);
     }
   }
 #if HB_GQ
@@ -2119,12 +2208,116 @@ __device__ double block_select2(const uint64_t (&key)[VPT], uint32_t kth, uint64
   return dval(sh->ans);
 }
 
+// Warm-chain model pass of the NW-wave kernel (the plan's lane-row arrays,
+// EvalPlan::brows): thread tid of NT owns lane row tid -- cadences tid*rc ..
+// tid*rc + rc - 1 -- solved as KC warm Kepler chains with the one-wave
+// kernel's steps (chain_first / chain_kepler_warm / chain_finish_warm,
+// software-pipelined as in model_pass_chain_pipe: step j's Kepler solve and
+// step j-1's polynomial in one block).  Values are stored column-major,
+// vals[c*NT + tid]: a step's stores are one contiguous 512-B row per wave (no
+// LDS bank conflicts), and key slot v of thread tid is vals[v*NT + tid] as in
+// the strided pass (cadence tid*rc + v here).  A wave's 64 rows are a
+// contiguous 1/NW of the light curve, so its eclipsing lanes come in runs:
+// the eclipse term is applied inline behind a wave-level test (no queue: the
+// slab fills the LDS).  Per cadence the value is the one-wave kernel's --
+// the polynomial minus the same eclipse term, or the reference-order slow
+// path -- so the template is the same.
+template <int NT, int VPT>
+__device__ __forceinline__ void model_pass_block_chain(const double* __restrict__ tT, const double2* __restrict__ ph,
+                                                       int n, int rc, const WalkerConst& w, double* vals, int tid,
+                                                       uint64_t& kmn_out, uint64_t& kmx_out) {
+#if HB_CHAIN_SPLIT
+  static_assert(VPT <= 32, "slow-path slots in a 32-bit mask");
+  constexpr int KC = VPT < HB_KC ? VPT : HB_KC;
+  const int lc = (rc + KC - 1) / KC;  // chain length (block-uniform)
+  const bool tab = (ph != nullptr) && (w.tab != 0.0);
+  const int last = n - 1;
+  const int base = tid * rc;
+  double vmn = __builtin_inf(), vmx = -__builtin_inf();
+  bool nan = false;
+  ChainState<KC> st;
+  double tk[KC];
+#pragma unroll
+  for (int k = 0; k < KC; ++k) tk[k] = tT[min(k * lc, rc - 1) * NT + tid];
+  bool pend_ok = true;
+  {
+    double2 p0[KC];
+#pragma unroll
+    for (int k = 0; k < KC; ++k) p0[k] = tab ? ph[min(base + k * lc, last)] : make_double2(0.0, 1.0);
+    chain_first<KC>(tk, p0, tab, w, st, pend_ok);
+  }
+  // slots of out-of-domain cadences (bit c): redone after the pass in
+  // reference order (no call inside the loop)
+  uint32_t slow = 0u;
+  // step jp's values: eclipse term inline, store
+  auto emit = [&](int jp, double (&v)[KC], const double (&dd)[KC], const double (&zz)[KC], bool bad) {
+#pragma unroll
+    for (int k = 0; k < KC; ++k) {
+      const int c = k * lc + jp;
+      if (c < rc) {  // block-uniform
+        const bool need = (!bad) & eclipse_lane(w, dd[k], zz[k]);
+        if (wave_any(need)) {
+          if (need) v[k] -= eclipse_term_inl(&w, sqrt_fast(dd[k]) * w.aR, signbit(zz[k]) ? -1.0 : 1.0);
+        }
+        slow |= bad ? 1u << c : 0u;
+        // padding cadences (past n) repeat cadence n - 1: harmless for min / max
+        vals[c * NT + tid] = v[k];
+        vmn = fmin(vmn, v[k]);
+        vmx = fmax(vmx, v[k]);
+        nan |= v[k] != v[k];
+      }
+    }
+  };
+  for (int j = 1; j < lc; ++j) {
+#pragma unroll
+    for (int k = 0; k < KC; ++k) tk[k] = tT[min(k * lc + j, rc - 1) * NT + tid];
+    double m[KC], E[KC], s[KC], c[KC], ys[KC], v[KC], dd[KC], zz[KC];
+    bool ok = true, fine;
+    chain_kepler_warm<KC>(tk, w, st, m, E, s, c, ys, fine, ok);  // step j
+    flux_poly_inv_k<KC>(st.s, st.c, st.inv, w, v, dd, zz);      // step j - 1, same block
+    emit(j - 1, v, dd, zz, !pend_ok);
+    chain_finish_warm<KC>(tk, w, wave_all(fine), fine, m, E, s, c, ys, ok, st);
+    pend_ok = ok;
+  }
+  {  // the last step's polynomial
+    double v[KC], dd[KC], zz[KC];
+    flux_poly_inv_k<KC>(st.s, st.c, st.inv, w, v, dd, zz);
+    emit(lc - 1, v, dd, zz, !pend_ok);
+  }
+  if (wave_any(slow != 0u)) {  // out-of-domain angles: reference-order path (eclipse included)
+    while (slow != 0u) {
+      const int c = __builtin_ctz(slow);
+      slow &= slow - 1u;
+      const double v = hb_cadence_flux_slow(tT[c * NT + tid], &w);
+      vals[c * NT + tid] = v;
+      vmn = fmin(vmn, v);
+      vmx = fmax(vmx, v);
+      nan |= v != v;
+    }
+  }
+  uint64_t kmn = dkey(vmn == 0.0 ? -0.0 : vmn), kmx = dkey(vmx == 0.0 ? 0.0 : vmx);
+  if (wave_any(nan)) {  // never observed: keys of the stored values
+    kmn = ~0ull;
+    kmx = 0ull;
+    for (int c = 0; c < rc; ++c) {
+      const uint64_t key = dkey(vals[c * NT + tid]);
+      kmn = key < kmn ? key : kmn;
+      kmx = key > kmx ? key : kmx;
+    }
+  }
+  kmn_out = kmn;
+  kmx_out = kmx;
+#else
+  (void)tT; (void)ph; (void)n; (void)rc; (void)w; (void)vals; (void)tid; kmn_out = 0; kmx_out = 0;
+#endif
+}
+
 template <int NW, int VPT>
 __global__ __launch_bounds__(64 * NW) HB_WPE_ATTR void hb_eval_block_kernel(
     const double* __restrict__ t, const double2* __restrict__ ph, const double* __restrict__ f,
     const double* __restrict__ isg, long n,
     long kth, const WalkerConst* __restrict__ wcs, double* __restrict__ logl, double* __restrict__ tmpl_out,
-    int mode) {
+    int mode, const double* __restrict__ rows, double gap) {
   constexpr int NT = 64 * NW;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   SelShared* sh = reinterpret_cast<SelShared*>(smem);
@@ -2139,8 +2332,15 @@ __global__ __launch_bounds__(64 * NW) HB_WPE_ATTR void hb_eval_block_kernel(
     return;
   }
   const int nn = (int)n;
+  const int rc = (nn + NT - 1) / NT;  // cadences per lane row (<= VPT)
+  // block-uniform: the lane-row warm chains (model_pass_block_chain), else the
+  // strided cold pass; key slot v of thread tid is cadence tid*rc + v or v*NT + tid
+  const bool chain = rows != nullptr && rc >= HB_CHAIN_VPT_MIN && chain_eligible(w, gap);
   uint64_t kmn, kmx;
-  model_pass<NT>(t, ph, nn, w, vals, tid, kmn, kmx);
+  if (chain)
+    model_pass_block_chain<NT, VPT>(rows, ph, nn, rc, w, vals, tid, kmn, kmx);
+  else
+    model_pass<NT>(t, ph, nn, w, vals, tid, kmn, kmx);
   kmn = wave_reduce_u64(kmn, OpMinU64());
   kmx = wave_reduce_u64(kmx, OpMaxU64());
   if (lane == 0) {
@@ -2155,12 +2355,12 @@ __global__ __launch_bounds__(64 * NW) HB_WPE_ATTR void hb_eval_block_kernel(
     kmn = sh->red_min[k] < kmn ? sh->red_min[k] : kmn;
     kmx = sh->red_max[k] > kmx ? sh->red_max[k] : kmx;
   }
+  // key slots v < nlive hold cadences (a compare with a constant per slot: no
+  // per-slot predicate is held across the select)
+  const int nlive = chain ? min(rc, max(0, nn - tid * rc)) : (nn - tid + NT - 1) / NT;
   uint64_t key[VPT];
 #pragma unroll
-  for (int v = 0; v < VPT; ++v) {
-    const int i = v * NT + tid;
-    key[v] = i < nn ? dkey(vals[i]) : ~0ull;  // padding sorts last, never selected
-  }
+  for (int v = 0; v < VPT; ++v) key[v] = v < nlive ? dkey(vals[v * NT + tid]) : ~0ull;  // padding sorts last
   __syncthreads();  // the slab becomes the histogram
 #if HB_ABLATE_SELECT
   const double med = dval(kmn);
@@ -2172,22 +2372,24 @@ __global__ __launch_bounds__(64 * NW) HB_WPE_ATTR void hb_eval_block_kernel(
     double* o = tmpl_out + (size_t)wv * (size_t)n;
 #pragma unroll
     for (int v = 0; v < VPT; ++v) {
-      const int i = v * NT + tid;
-      if (i < nn) {
+      if (v < nlive) {
         const double m = (dval(key[v]) - med) + 1.0;
-        o[i] = (blend + m * one_m_blend) * tune;
+        o[chain ? tid * rc + v : v * NT + tid] = (blend + m * one_m_blend) * tune;
       }
     }
     return;
   }
+  // f and 1/sigma of key slot v: the lane-row arrays (same index) on the chain path
+  const double* __restrict__ fs = chain ? rows + (size_t)NT * rc : f;
+  const double* __restrict__ is = chain ? rows + 2 * (size_t)NT * rc : isg;
   double acc = 0.0;
 #pragma unroll
   for (int v = 0; v < VPT; ++v) {
     const int i = v * NT + tid;
-    if (i < nn) {
+    if (v < nlive) {
       double m = (dval(key[v]) - med) + 1.0;
       m = (blend + m * one_m_blend) * tune;
-      const double r = (m - f[i]) * isg[i];
+      const double r = (m - fs[i]) * is[i];
       acc += r * r;
     }
   }
@@ -2390,13 +2592,26 @@ hipError_t launch_prep(const double* d_params, int nwalk, const MagArgs& ma, Wal
   const int nb = (nwalk + nw - 1) / nw;
   auto kern = nw == 64 ? hb_prep_kernel<64> : nw == 32 ? hb_prep_kernel<32> : hb_prep_kernel<kPrepWalkers>;
   hipLaunchKernelGGL(kern, dim3(nb), dim3(kPrepThreads), 0, s, d_params, nwalk, ma, d_wc, tab, wt, t,
-                     (int)n, ph, w0, ntargets, tab_pc);
+                     (int)n, ph, w0, ntargets, tab_pc, (const int*)nullptr);
+  return hipGetLastError();
+}
+
+hipError_t launch_prep_list(const double* d_params, const int* list, int count, WalkerConst* d_wc, hipStream_t s,
+                            const TargetDesc* tab, const int* wt, const int* w0) {
+  if (count <= 0) return hipSuccess;
+  if (!list || !tab || !wt || !w0) return hipErrorInvalidValue;
+  const int nw = count >= 256 * 32 ? 32 : kPrepWalkers;
+  const int nb = (count + nw - 1) / nw;
+  const MagArgs unused{};
+  auto kern = nw == 32 ? hb_prep_kernel<32, true> : hb_prep_kernel<kPrepWalkers, true>;
+  hipLaunchKernelGGL(kern, dim3(nb), dim3(kPrepThreads), 0, s, d_params, count, unused, d_wc, tab, wt,
+                     (const double*)nullptr, 0, (double2*)nullptr, w0, 0, (double*)nullptr, list);
   return hipGetLastError();
 }
 
 template <int NW, int VPT>
 static hipError_t launch_block_t(const EvalPlan& pl, const double* t, const double2* ph, const double* f,
-                                 const double* sg,
+                                 const double* sg, const double* rows,
                                  const WalkerConst* wc, int nwalk, double* logl, double* tmpl, int mode,
                                  hipStream_t s) {
   auto kern = hb_eval_block_kernel<NW, VPT>;
@@ -2407,8 +2622,10 @@ static hipError_t launch_block_t(const EvalPlan& pl, const double* t, const doub
     if (e != hipSuccess) return e;
     attr_set = true;
   }
+  // the lane-row arrays only when they are this plan's (64 NW rows)
+  const double* br = (rows != nullptr && pl.brows == 64 * NW) ? rows : nullptr;
   hipLaunchKernelGGL(kern, dim3(nwalk), dim3(64 * NW), pl.lds_bytes, s, t, ph, f, sg, pl.n, pl.kth, wc, logl,
-                     tmpl, mode);
+                     tmpl, mode, br, pl.gap);
   return hipGetLastError();
 }
 
@@ -2451,7 +2668,7 @@ static hipError_t launch_wave_g(size_t lds_per, int count, hipStream_t s, const 
                                 const hbds::AccArgs& acc, double* dq, const PreArgs* pre = nullptr) {
   auto kern = hb_eval_wave_kernel<VPT, MULTI, ACC, WPB, WPW, PRE>;
   // PRE: the slices, then the LDS phase table (16 B per cadence)
-  const size_t lds = (size_t)WPB * lds_per + (PRE ? (((size_t)n * 16 + 15) & ~(size_t)15) : (WPB > 1 ? 64 : 0));
+  const size_t lds = (size_t)WPB * lds_per + (PRE ? (MULTI ? 0 : (((size_t)n * 16 + 15) & ~(size_t)15)) : (WPB > 1 ? 64 : 0));
   if (lds > kLdsCap) return hipErrorInvalidValue;
   static bool attr_set = false;  // per instantiation; benign race (idempotent)
   if (!attr_set && lds > 65536) {
@@ -2472,6 +2689,13 @@ static size_t fused_lds_per(const EvalPlan& pl) {
   return slab >= (size_t)kCandInSlab ? slab : wave_lds_bytes(slab, pl.vpt, 1);
 }
 
+// the prologue's scratch (prep records, catalog magnitudes and walker lists),
+// which aliases the workgroup's slabs
+static size_t fused_scratch_bytes(int wpb) {
+  const size_t ps = wpb == 16 ? sizeof(PrepShared<16>) : wpb == 8 ? sizeof(PrepShared<8>) : sizeof(PrepShared<4>);
+  return ps + (size_t)wpb * (3 * sizeof(double) + 2 * sizeof(int));
+}
+
 // Walkers per workgroup of the fused launch (0: prep + eval launches).  The
 // workgroup keeps WPB one-wave walkers plus the LDS phase table; the largest
 // WPB in {16, 8, 4} that still gives every CU a workgroup, as long as the
@@ -2488,7 +2712,7 @@ int fused_wpb(const EvalPlan& pl, int w, int cus) {
   const long share = std::min<long>(16, ((long)w + cus - 1) / cus);  // walkers a CU must hold at once
   for (int wpb = 16; wpb >= 4; wpb >>= 1) {
     const size_t lds = (size_t)wpb * per + tabb;
-    if (lds > kLdsCap) continue;
+    if (lds > kLdsCap || fused_scratch_bytes(wpb) > (size_t)wpb * per) continue;
     const long resident = (long)(kLdsCap / lds) * wpb;
     if (resident < share) continue;
     if (wpb > 4 && ((long)w + wpb - 1) / wpb < cus) continue;  // a workgroup for every CU
@@ -2513,6 +2737,51 @@ static hipError_t launch_fused_t(const EvalPlan& pl, int wpb, const PreArgs& pa,
   HB_FCASE(4)
 #undef HB_FCASE
   return hipErrorInvalidValue;
+}
+
+// catalog mode, records in the prologue: one size class of one-wave walkers.
+// 16 walkers per workgroup while their slabs fit LDS (the prep roles' issue
+// per walker falls with the walkers sharing a workgroup), else 8 / 4.
+template <int VPT>
+static hipError_t launch_multi_fused_t(size_t slab, const PreArgs& pa, const double* t, const double* f,
+                                       const double* sg, const double* rows, int count, double* logl, hipStream_t s,
+                                       double* dq) {
+  EvalPlan pl;
+  pl.vpt = VPT;
+  pl.slab_bytes = slab;
+  const size_t per = fused_lds_per(pl);
+  const hbds::AccArgs none{};
+#define HB_MFCASE(WV)                                                                                            \
+  if ((size_t)WV * per <= kLdsCap && fused_scratch_bytes(WV) <= (size_t)WV * per)                                \
+    return launch_wave_g<VPT, true, false, WV, 1, true>(per, count, s, t, nullptr, f, sg, rows, 0L, 0L, pa.wc,   \
+                                                        logl, nullptr, 0, slab, 0.0, pa.tab, pa.wt, pa.list, none, \
+                                                        dq, &pa);
+  if (count >= 64) {
+    HB_MFCASE(16)
+  }
+  if (count >= 16) {
+    HB_MFCASE(8)
+  }
+  HB_MFCASE(4)
+#undef HB_MFCASE
+  return hipErrorInvalidValue;
+}
+
+hipError_t launch_eval_multi_fused(int vpt, size_t slab, const PreArgs& pa, const double* t, const double* f,
+                                   const double* sg, const double* rows, int count, double* logl, hipStream_t s,
+                                   double* dq) {
+  if (count <= 0) return hipSuccess;
+  if (!HB_PIPE || !HB_CHAIN_SPLIT || dq == nullptr || pa.params == nullptr || pa.wc == nullptr || pa.list == nullptr ||
+      pa.wt == nullptr || pa.tab == nullptr || pa.w0 == nullptr)
+    return hipErrorInvalidValue;
+  switch (vpt) {
+    case 1: return launch_multi_fused_t<1>(slab, pa, t, f, sg, rows, count, logl, s, dq);
+    case 2: return launch_multi_fused_t<2>(slab, pa, t, f, sg, rows, count, logl, s, dq);
+    case 4: return launch_multi_fused_t<4>(slab, pa, t, f, sg, rows, count, logl, s, dq);
+    case 8: return launch_multi_fused_t<8>(slab, pa, t, f, sg, rows, count, logl, s, dq);
+    case 16: return launch_multi_fused_t<16>(slab, pa, t, f, sg, rows, count, logl, s, dq);
+    default: return hipErrorInvalidValue;
+  }
 }
 
 hipError_t launch_eval_fused(const EvalPlan& pl, int wpb, const PreArgs& pa, const double* t, const double* f,
@@ -2650,7 +2919,7 @@ hipError_t launch_eval(const EvalPlan& pl, const double* t, const double2* ph, c
   }
   if (pl.bvpt > 0) {
 #define HB_BCASE(NWV, V)                                                                    \
-  if (pl.nw == NWV && pl.bvpt == V) return launch_block_t<NWV, V>(pl, t, ph, f, sg, wc, nwalk, logl, tmpl, mode, s);
+  if (pl.nw == NWV && pl.bvpt == V) return launch_block_t<NWV, V>(pl, t, ph, f, sg, rows, wc, nwalk, logl, tmpl, mode, s);
     HB_BCASE(4, 8) HB_BCASE(4, 16) HB_BCASE(4, 20)
     HB_BCASE(8, 8) HB_BCASE(8, 16) HB_BCASE(8, 20)
     HB_BCASE(16, 8) HB_BCASE(16, 16) HB_BCASE(16, 20)
@@ -2800,12 +3069,12 @@ size_t wave_lds_bytes(size_t slab, int vpt, int wpw) {
 // t, f and 1/sigma in the one-wave kernel's lane-row order: row block c holds
 // cadence l * rc + c for lane rows l = 0..nr-1 (nr = wave_nr_for(n), rc =
 // ceil(n / nr); cadences past the end repeat the last one and are never used)
-long wave_rows_doubles(long n) {
-  const long nr = wave_nr_for(n);
+long wave_rows_doubles(long n, long nr) {
+  if (nr <= 0) nr = wave_nr_for(n);
   return 3L * nr * ((n + nr - 1) / nr);
 }
-void build_rows(const double* t, const double* f, const double* isg, long n, double* out) {
-  const long nr = wave_nr_for(n);
+void build_rows(const double* t, const double* f, const double* isg, long n, double* out, long nr) {
+  if (nr <= 0) nr = wave_nr_for(n);
   const long rc = (n + nr - 1) / nr;
   for (long c = 0; c < rc; ++c)
     for (long l = 0; l < nr; ++l) {

@@ -312,6 +312,44 @@ def test_rows_plan_cold_roche_shuffled(hbmi, oracle, n, order):
     assert worst <= 1.0, f"template error {worst:.2f} x the bound"
 
 
+@pytest.mark.parametrize("order", ["sorted", "shuffled"])
+@pytest.mark.parametrize("n", [4097, 6001, 12000, 20000])
+def test_block_chain_cold_roche_shuffled(hbmi, oracle, n, order):
+    """N > 4096 runs the block kernel; its walkers with e <= 0.8 on closely
+    spaced cadences take the lane-row warm-chain pass (model_pass_block_chain:
+    thread r solves cadences r*rc .. r*rc + rc - 1, values column-major in LDS,
+    eclipse terms inline), the others the strided cold pass.  64 walkers:
+    Roche walkers, e = 0.85 / 0.9 cold walkers beside warm ones in one batch,
+    and a shuffled cadence order (the warm-chain gate then sends every walker
+    to the cold pass); templates and logL against the oracle, and every
+    walker's logL bit-identical when the batch is evaluated in reverse."""
+    from hb_mcmc_amd import synth
+    from hb_mcmc_amd.likelihood import HBLikelihood
+
+    t, f, s = synth.dataset(n, oracle.light_curve)
+    if order == "shuffled":
+        p = np.random.default_rng(n).permutation(n)
+        t, f, s = t[p], f[p], s[p]
+    P = synth.walkers(64, seed=n + 1, roche_frac=0.1)
+    P[0::8, 3] = 0.85
+    P[4::8, 3] = 0.9
+    with HBLikelihood(t, f, s) as L:
+        assert L.eval_kernel == "hb_eval_block_kernel"
+        assert L.block_rows == 64 * L.waves_per_walker
+        ll = L.loglike(P)
+        rev = L.loglike(P[::-1].copy())[::-1]
+        tm = L.light_curve(P)
+    assert np.array_equal(ll, rev, equal_nan=True)
+    ref_ll = oracle.loglike_batch(t, f, s, P, synth.MAG_DEFAULT, synth.MAGERR_DEFAULT, 8)
+    close_logl(ll, ref_ll)
+    assert (ref_ll == -5e14).sum() >= 3  # Roche walkers present
+    ref = oracle.light_curve_batch(t, P, 8)
+    ok = ~np.isnan(ref).any(1)
+    tol = cold_tol(oracle, t, P, ref)
+    worst = np.nanmax(np.where(ok[:, None], np.abs(tm - ref) / tol, 0.0))
+    assert worst <= 1.0, f"template error {worst:.2f} x the bound"
+
+
 @pytest.mark.parametrize("latency", [True, False], ids=["small-batch-plan", "one-wave-plan"])
 @pytest.mark.parametrize("n", [1024, 6001])
 def test_phase_table_and_direct_paths(hbmi, oracle, n, latency):
