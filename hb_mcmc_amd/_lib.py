@@ -72,8 +72,6 @@ def _declare(lib):
     lib.hb_ctx_template_in_lds.argtypes = [_VP]
     lib.hb_ctx_eval_kind.restype = _I
     lib.hb_ctx_eval_kind.argtypes = [_VP]
-    lib.hb_ctx_block_rows.restype = _I
-    lib.hb_ctx_block_rows.argtypes = [_VP]
     lib.hb_ctx_fused_wpb.restype = _I
     lib.hb_ctx_fused_wpb.argtypes = [_VP, _I]
     lib.hb_ctx_set_latency_plan.restype = _I

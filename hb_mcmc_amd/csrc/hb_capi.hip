@@ -291,13 +291,9 @@ extern "C" hb_ctx* hb_create(const double* t, const double* f, const double* sig
     hb_destroy(c.release());
     return nullptr;
   }
-  // lane-row arrays: the one-wave path's rows, or the NW-wave path's 64 nw
-  // rows (its warm-chain model pass)
-  static const bool block_chain = getenv("HB_BLOCK_CHAIN") == nullptr || atoi(getenv("HB_BLOCK_CHAIN")) != 0;
-  if (c->plan.vpt == 0 && c->plan.bvpt > 0 && block_chain) c->plan.brows = 64 * c->plan.nw;
-  if (c->plan.vpt > 0 || c->plan.brows > 0) {
-    std::vector<double> rows((size_t)hbk::wave_rows_doubles(n, c->plan.brows));
-    hbk::build_rows(t, f, s.data(), n, rows.data(), c->plan.brows);
+  if (c->plan.vpt > 0) {
+    std::vector<double> rows((size_t)hbk::wave_rows_doubles(n));
+    hbk::build_rows(t, f, s.data(), n, rows.data());
     if (hipMalloc(&c->d_rows, sizeof(double) * rows.size()) != hipSuccess ||
         hipMemcpy(c->d_rows, rows.data(), sizeof(double) * rows.size(), hipMemcpyHostToDevice) != hipSuccess) {
       set_err_msg("hb_create: lane-row arrays: hipMalloc/upload failed");
@@ -337,11 +333,6 @@ extern "C" int hb_ctx_fused_wpb(const hb_ctx* c, int w) {
 extern "C" int hb_ctx_eval_kind(const hb_ctx* c) {
   if (!c) return -1;
   return c->plan.vpt > 0 ? 0 : c->plan.bvpt > 0 ? 1 : 2;
-}
-
-extern "C" int hb_ctx_block_rows(const hb_ctx* c) {
-  if (!c) return -1;
-  return c->plan.vpt > 0 ? 0 : c->plan.brows;
 }
 
 static int run_batch(hb_ctx* c, const double* d_params, int w, double* d_logl, double* d_tmpl,
@@ -748,16 +739,20 @@ static int catalog_layout(hb_catalog* c, const int* walkers, hipStream_t s) {
   return 0;
 }
 
-// One catalog call.  Every class launches on its stream at once (forked at
-// the call's start): a one-wave class of up to 16 cadences per lane is ONE
-// fused launch (its walkers' records in the eval kernel's prologue), the pair
-// class and the one-wave class of 32 cadences per lane a records launch for
-// their walkers (launch_prep_list) then the eval.  The evals evaluate the
-// per-target phase-table entries in place (no table launch).  HB_CAT_FUSED=0
-// (A/B knob): one records launch for every walker first, then the classes.
+// One catalog call: one records launch for every walker (hb_prep_kernel over
+// the catalog's walkers, per-target phase tables in its tail), then every
+// size class's eval launch on its stream (forked at the call's start).  The
+// evals evaluate the per-target phase-table entries in place.
+// HB_CAT_FUSED=1 (A/B knob): each one-wave class of up to 16 cadences per lane
+// is ONE fused launch (its walkers' records in the eval kernel's prologue),
+// the other classes a records launch for their walkers (launch_prep_list) and
+// the eval -- measured slower: 0.204 vs 0.168 ms per C5 call
+// (profiles/r04/r04f_bench_c5*.json): a class's 1024-thread workgroups hold
+// their CU until the slowest of their 16 walkers (targets of different
+// lengths and eccentricities) is done, where one-wave workgroups backfill.
 static int catalog_run(hb_catalog* c, const double* d_params, double* d_logl, hipStream_t s) {
   if (c->total == 0) return 0;
-  static const bool fused = cat_env("HB_CAT_FUSED", 1) != 0;
+  static const bool fused = cat_env("HB_CAT_FUSED", 0) != 0;
   if (!fused) {
     MagArgs unused{};
     HB_TRY(hbk::launch_prep(d_params, c->total, unused, c->d_wc, s, c->d_tab, c->d_wt, c->d_t, 0, c->d_ph, c->d_w0,
@@ -807,7 +802,8 @@ static int catalog_run(hb_catalog* c, const double* d_params, double* d_logl, hi
     }
     if (fused)
       HB_TRY(hbk::launch_prep_list(d_params, lst, cnt, c->d_wc, sj, c->d_tab, c->d_wt, c->d_w0), "records launch");
-    HB_TRY(hbk::launch_eval_multi(vpt, c->class_slab[cl], c->d_t, c->d_ph, c->d_f, c->d_s, c->d_rows, c->d_tab, c->d_wt,
+    HB_TRY(hbk::launch_eval_multi(vpt, c->class_slab[cl], c->d_t, fused ? nullptr : c->d_ph, c->d_f, c->d_s, c->d_rows,
+                                  c->d_tab, c->d_wt,
                                   lst, cnt, c->d_wc, d_logl, sj, dq, wpw),
            "eval launch");
   }

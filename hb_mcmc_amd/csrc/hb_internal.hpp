@@ -43,8 +43,6 @@ struct EvalPlan {
   bool lds = true;     // template in LDS (else HBM scratch slab)
   size_t lds_bytes = 0;
   double gap = 0.0;    // typical cadence spacing [d] (hb_cadence_gap), warm-chain gate
-  int brows = 0;       // >0: the NW-wave path's lane rows (64 nw) of the context's lane-row
-                       // arrays -- its warm-chain model pass; 0: strided cold pass only
 };
 
 // One light curve of a catalog (hb_catalog_*): its slice of the concatenated
@@ -148,9 +146,8 @@ size_t wave_queue_bytes(int vpt, long count, int wpw = 1);
 size_t wave_slab_bytes(long n);
 size_t wave_lds_bytes(size_t slab, int vpt, int wpw = 1);
 // t, f, 1/sigma in the one-wave kernel's lane-row order (3 x nr x ceil(n/nr) doubles)
-// (nr > 0: that many rows instead, the NW-wave path's 64 nw)
-long wave_rows_doubles(long n, long nr = 0);
-void build_rows(const double* t, const double* f, const double* isg, long n, double* out, long nr = 0);
+long wave_rows_doubles(long n);
+void build_rows(const double* t, const double* f, const double* isg, long n, double* out);
 // acc (device sampler, one-wave path only): each wave also runs its slot's
 // Hastings test and history write (hb_accept.hpp); hipErrorNotSupported on the
 // multi-wave path

@@ -639,7 +639,8 @@ __device__ __forceinline__ void model_pass_cold(const double* __restrict__ t, co
                                                 int n, const Rows& rw, const WalkerConst& w, double* vals,
                                                 int lane, Pacer pc, DeferQ& dq) {
   constexpr int K = HB_K;
-  const bool tab = (VT || ph != nullptr) && (w.tab != 0.0);  // walker-uniform
+  const bool vt = VT && ph == nullptr;                        // entries evaluated in place
+  const bool tab = (vt || ph != nullptr) && (w.tab != 0.0);  // walker-uniform
   const int last = n - 1;
   const int nit = (n + K * NT - 1) / (K * NT);
   pc.begin(nit);
@@ -651,7 +652,7 @@ __device__ __forceinline__ void model_pass_cold(const double* __restrict__ t, co
     for (int k = 0; k < K; ++k) {
       const int i = min(base + k * NT + lane, last);
       tk[k] = t[i];
-      pk[k] = tab ? (VT ? vt_entry(tk[k], w) : ph[i]) : make_double2(0.0, 1.0);
+      pk[k] = tab ? (vt ? vt_entry(tk[k], w) : ph[i]) : make_double2(0.0, 1.0);
     }
     bool bad;
 #if HB_SPLIT_LIVE
@@ -830,7 +831,8 @@ __device__ __forceinline__ void model_pass_chain_pipe(const double* __restrict__
   constexpr int KCM = NR > 64 ? HB_PAIR_KC : HB_KC;
   constexpr int KC = VPT < KCM ? VPT : KCM;
   const int lc = (rw.rc + KC - 1) / KC;  // chain length (wave-uniform)
-  const bool tab = (VT || ph != nullptr) && (w.tab != 0.0);  // walker-uniform
+  const bool vt = VT && ph == nullptr;                        // entries evaluated in place
+  const bool tab = (vt || ph != nullptr) && (w.tab != 0.0);  // walker-uniform
   const int last = n - 1;
   const int base = row * rw.rc;
   const int rs = row * rw.stride, lsw = HB_ODD_STRIDE ? 0 : (row & rw.swz);  // slab_pos = rs + (c ^ lsw)
@@ -845,7 +847,7 @@ __device__ __forceinline__ void model_pass_chain_pipe(const double* __restrict__
     double2 p0[KC];
 #pragma unroll
     for (int k = 0; k < KC; ++k)
-      p0[k] = tab ? (VT ? vt_entry(tk[k], w) : ph[min(base + k * lc, last)]) : make_double2(0.0, 1.0);
+      p0[k] = tab ? (vt ? vt_entry(tk[k], w) : ph[min(base + k * lc, last)]) : make_double2(0.0, 1.0);
     chain_first<KC>(tk, p0, tab, w, st, pend_ok);
   }
   // store the pending step jp's values and queue its eclipse / slow-path cadences
@@ -1814,9 +1816,10 @@ __global__ __launch_bounds__(64 * WPB * WPW) HB_WPE_ATTR void hb_eval_wave_kerne
   static_assert(WPW == 1 || (WPW <= kMaxWPW && WPB == 1 && !ACC && HB_SEL_V == 3 && HB_GQ), "pair/rows: plain batched path");
   static_assert(!PRE || (WPW == 1 && !ACC && WPB >= kPrepRoles && HB_SEL_V == 3 && HB_GQ && HB_PRIO != 2),
                 "fused launch: plain one-wave batched path");
-  // the catalog evaluates its phase-table entries in place (vt_entry): a
-  // workgroup's walkers belong to several targets, and no launch writes the
-  // per-target tables
+  // catalog launches without a table (ph == nullptr: the fused launches, whose
+  // workgroups mix targets, and the classes beside them, whose records launch
+  // writes no tables) evaluate the per-target entries in place (vt_entry);
+  // with the tables of the catalog's records launch they read them
   constexpr bool kVT = MULTI;
   static_assert(!kVT || (HB_PIPE && HB_CHAIN_SPLIT), "the virtual table needs the pipelined chain pass");
   constexpr int NR = 64 * WPW;  // lane rows per walker
@@ -2208,116 +2211,12 @@ __device__ double block_select2(const uint64_t (&key)[VPT], uint32_t kth, uint64
   return dval(sh->ans);
 }
 
-// Warm-chain model pass of the NW-wave kernel (the plan's lane-row arrays,
-// EvalPlan::brows): thread tid of NT owns lane row tid -- cadences tid*rc ..
-// tid*rc + rc - 1 -- solved as KC warm Kepler chains with the one-wave
-// kernel's steps (chain_first / chain_kepler_warm / chain_finish_warm,
-// software-pipelined as in model_pass_chain_pipe: step j's Kepler solve and
-// step j-1's polynomial in one block).  Values are stored column-major,
-// vals[c*NT + tid]: a step's stores are one contiguous 512-B row per wave (no
-// LDS bank conflicts), and key slot v of thread tid is vals[v*NT + tid] as in
-// the strided pass (cadence tid*rc + v here).  A wave's 64 rows are a
-// contiguous 1/NW of the light curve, so its eclipsing lanes come in runs:
-// the eclipse term is applied inline behind a wave-level test (no queue: the
-// slab fills the LDS).  Per cadence the value is the one-wave kernel's --
-// the polynomial minus the same eclipse term, or the reference-order slow
-// path -- so the template is the same.
-template <int NT, int VPT>
-__device__ __forceinline__ void model_pass_block_chain(const double* __restrict__ tT, const double2* __restrict__ ph,
-                                                       int n, int rc, const WalkerConst& w, double* vals, int tid,
-                                                       uint64_t& kmn_out, uint64_t& kmx_out) {
-#if HB_CHAIN_SPLIT
-  static_assert(VPT <= 32, "slow-path slots in a 32-bit mask");
-  constexpr int KC = VPT < HB_KC ? VPT : HB_KC;
-  const int lc = (rc + KC - 1) / KC;  // chain length (block-uniform)
-  const bool tab = (ph != nullptr) && (w.tab != 0.0);
-  const int last = n - 1;
-  const int base = tid * rc;
-  double vmn = __builtin_inf(), vmx = -__builtin_inf();
-  bool nan = false;
-  ChainState<KC> st;
-  double tk[KC];
-#pragma unroll
-  for (int k = 0; k < KC; ++k) tk[k] = tT[min(k * lc, rc - 1) * NT + tid];
-  bool pend_ok = true;
-  {
-    double2 p0[KC];
-#pragma unroll
-    for (int k = 0; k < KC; ++k) p0[k] = tab ? ph[min(base + k * lc, last)] : make_double2(0.0, 1.0);
-    chain_first<KC>(tk, p0, tab, w, st, pend_ok);
-  }
-  // slots of out-of-domain cadences (bit c): redone after the pass in
-  // reference order (no call inside the loop)
-  uint32_t slow = 0u;
-  // step jp's values: eclipse term inline, store
-  auto emit = [&](int jp, double (&v)[KC], const double (&dd)[KC], const double (&zz)[KC], bool bad) {
-#pragma unroll
-    for (int k = 0; k < KC; ++k) {
-      const int c = k * lc + jp;
-      if (c < rc) {  // block-uniform
-        const bool need = (!bad) & eclipse_lane(w, dd[k], zz[k]);
-        if (wave_any(need)) {
-          if (need) v[k] -= eclipse_term_inl(&w, sqrt_fast(dd[k]) * w.aR, signbit(zz[k]) ? -1.0 : 1.0);
-        }
-        slow |= bad ? 1u << c : 0u;
-        // padding cadences (past n) repeat cadence n - 1: harmless for min / max
-        vals[c * NT + tid] = v[k];
-        vmn = fmin(vmn, v[k]);
-        vmx = fmax(vmx, v[k]);
-        nan |= v[k] != v[k];
-      }
-    }
-  };
-  for (int j = 1; j < lc; ++j) {
-#pragma unroll
-    for (int k = 0; k < KC; ++k) tk[k] = tT[min(k * lc + j, rc - 1) * NT + tid];
-    double m[KC], E[KC], s[KC], c[KC], ys[KC], v[KC], dd[KC], zz[KC];
-    bool ok = true, fine;
-    chain_kepler_warm<KC>(tk, w, st, m, E, s, c, ys, fine, ok);  // step j
-    flux_poly_inv_k<KC>(st.s, st.c, st.inv, w, v, dd, zz);      // step j - 1, same block
-    emit(j - 1, v, dd, zz, !pend_ok);
-    chain_finish_warm<KC>(tk, w, wave_all(fine), fine, m, E, s, c, ys, ok, st);
-    pend_ok = ok;
-  }
-  {  // the last step's polynomial
-    double v[KC], dd[KC], zz[KC];
-    flux_poly_inv_k<KC>(st.s, st.c, st.inv, w, v, dd, zz);
-    emit(lc - 1, v, dd, zz, !pend_ok);
-  }
-  if (wave_any(slow != 0u)) {  // out-of-domain angles: reference-order path (eclipse included)
-    while (slow != 0u) {
-      const int c = __builtin_ctz(slow);
-      slow &= slow - 1u;
-      const double v = hb_cadence_flux_slow(tT[c * NT + tid], &w);
-      vals[c * NT + tid] = v;
-      vmn = fmin(vmn, v);
-      vmx = fmax(vmx, v);
-      nan |= v != v;
-    }
-  }
-  uint64_t kmn = dkey(vmn == 0.0 ? -0.0 : vmn), kmx = dkey(vmx == 0.0 ? 0.0 : vmx);
-  if (wave_any(nan)) {  // never observed: keys of the stored values
-    kmn = ~0ull;
-    kmx = 0ull;
-    for (int c = 0; c < rc; ++c) {
-      const uint64_t key = dkey(vals[c * NT + tid]);
-      kmn = key < kmn ? key : kmn;
-      kmx = key > kmx ? key : kmx;
-    }
-  }
-  kmn_out = kmn;
-  kmx_out = kmx;
-#else
-  (void)tT; (void)ph; (void)n; (void)rc; (void)w; (void)vals; (void)tid; kmn_out = 0; kmx_out = 0;
-#endif
-}
-
 template <int NW, int VPT>
 __global__ __launch_bounds__(64 * NW) HB_WPE_ATTR void hb_eval_block_kernel(
     const double* __restrict__ t, const double2* __restrict__ ph, const double* __restrict__ f,
     const double* __restrict__ isg, long n,
     long kth, const WalkerConst* __restrict__ wcs, double* __restrict__ logl, double* __restrict__ tmpl_out,
-    int mode, const double* __restrict__ rows, double gap) {
+    int mode) {
   constexpr int NT = 64 * NW;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   SelShared* sh = reinterpret_cast<SelShared*>(smem);
@@ -2332,15 +2231,8 @@ __global__ __launch_bounds__(64 * NW) HB_WPE_ATTR void hb_eval_block_kernel(
     return;
   }
   const int nn = (int)n;
-  const int rc = (nn + NT - 1) / NT;  // cadences per lane row (<= VPT)
-  // block-uniform: the lane-row warm chains (model_pass_block_chain), else the
-  // strided cold pass; key slot v of thread tid is cadence tid*rc + v or v*NT + tid
-  const bool chain = rows != nullptr && rc >= HB_CHAIN_VPT_MIN && chain_eligible(w, gap);
   uint64_t kmn, kmx;
-  if (chain)
-    model_pass_block_chain<NT, VPT>(rows, ph, nn, rc, w, vals, tid, kmn, kmx);
-  else
-    model_pass<NT>(t, ph, nn, w, vals, tid, kmn, kmx);
+  model_pass<NT>(t, ph, nn, w, vals, tid, kmn, kmx);
   kmn = wave_reduce_u64(kmn, OpMinU64());
   kmx = wave_reduce_u64(kmx, OpMaxU64());
   if (lane == 0) {
@@ -2355,9 +2247,9 @@ __global__ __launch_bounds__(64 * NW) HB_WPE_ATTR void hb_eval_block_kernel(
     kmn = sh->red_min[k] < kmn ? sh->red_min[k] : kmn;
     kmx = sh->red_max[k] > kmx ? sh->red_max[k] : kmx;
   }
-  // key slots v < nlive hold cadences (a compare with a constant per slot: no
-  // per-slot predicate is held across the select)
-  const int nlive = chain ? min(rc, max(0, nn - tid * rc)) : (nn - tid + NT - 1) / NT;
+  // key slots v < nlive hold cadences v*NT + tid (a compare with a constant per
+  // slot: no per-slot predicate is held across the select)
+  const int nlive = (nn - tid + NT - 1) / NT;
   uint64_t key[VPT];
 #pragma unroll
   for (int v = 0; v < VPT; ++v) key[v] = v < nlive ? dkey(vals[v * NT + tid]) : ~0ull;  // padding sorts last
@@ -2374,14 +2266,11 @@ __global__ __launch_bounds__(64 * NW) HB_WPE_ATTR void hb_eval_block_kernel(
     for (int v = 0; v < VPT; ++v) {
       if (v < nlive) {
         const double m = (dval(key[v]) - med) + 1.0;
-        o[chain ? tid * rc + v : v * NT + tid] = (blend + m * one_m_blend) * tune;
+        o[v * NT + tid] = (blend + m * one_m_blend) * tune;
       }
     }
     return;
   }
-  // f and 1/sigma of key slot v: the lane-row arrays (same index) on the chain path
-  const double* __restrict__ fs = chain ? rows + (size_t)NT * rc : f;
-  const double* __restrict__ is = chain ? rows + 2 * (size_t)NT * rc : isg;
   double acc = 0.0;
 #pragma unroll
   for (int v = 0; v < VPT; ++v) {
@@ -2389,7 +2278,7 @@ __global__ __launch_bounds__(64 * NW) HB_WPE_ATTR void hb_eval_block_kernel(
     if (v < nlive) {
       double m = (dval(key[v]) - med) + 1.0;
       m = (blend + m * one_m_blend) * tune;
-      const double r = (m - fs[i]) * is[i];
+      const double r = (m - f[i]) * isg[i];
       acc += r * r;
     }
   }
@@ -2611,7 +2500,7 @@ hipError_t launch_prep_list(const double* d_params, const int* list, int count, 
 
 template <int NW, int VPT>
 static hipError_t launch_block_t(const EvalPlan& pl, const double* t, const double2* ph, const double* f,
-                                 const double* sg, const double* rows,
+                                 const double* sg,
                                  const WalkerConst* wc, int nwalk, double* logl, double* tmpl, int mode,
                                  hipStream_t s) {
   auto kern = hb_eval_block_kernel<NW, VPT>;
@@ -2622,10 +2511,8 @@ static hipError_t launch_block_t(const EvalPlan& pl, const double* t, const doub
     if (e != hipSuccess) return e;
     attr_set = true;
   }
-  // the lane-row arrays only when they are this plan's (64 NW rows)
-  const double* br = (rows != nullptr && pl.brows == 64 * NW) ? rows : nullptr;
   hipLaunchKernelGGL(kern, dim3(nwalk), dim3(64 * NW), pl.lds_bytes, s, t, ph, f, sg, pl.n, pl.kth, wc, logl,
-                     tmpl, mode, br, pl.gap);
+                     tmpl, mode);
   return hipGetLastError();
 }
 
@@ -2919,7 +2806,7 @@ hipError_t launch_eval(const EvalPlan& pl, const double* t, const double2* ph, c
   }
   if (pl.bvpt > 0) {
 #define HB_BCASE(NWV, V)                                                                    \
-  if (pl.nw == NWV && pl.bvpt == V) return launch_block_t<NWV, V>(pl, t, ph, f, sg, rows, wc, nwalk, logl, tmpl, mode, s);
+  if (pl.nw == NWV && pl.bvpt == V) return launch_block_t<NWV, V>(pl, t, ph, f, sg, wc, nwalk, logl, tmpl, mode, s);
     HB_BCASE(4, 8) HB_BCASE(4, 16) HB_BCASE(4, 20)
     HB_BCASE(8, 8) HB_BCASE(8, 16) HB_BCASE(8, 20)
     HB_BCASE(16, 8) HB_BCASE(16, 16) HB_BCASE(16, 20)
@@ -3069,12 +2956,12 @@ size_t wave_lds_bytes(size_t slab, int vpt, int wpw) {
 // t, f and 1/sigma in the one-wave kernel's lane-row order: row block c holds
 // cadence l * rc + c for lane rows l = 0..nr-1 (nr = wave_nr_for(n), rc =
 // ceil(n / nr); cadences past the end repeat the last one and are never used)
-long wave_rows_doubles(long n, long nr) {
-  if (nr <= 0) nr = wave_nr_for(n);
+long wave_rows_doubles(long n) {
+  const long nr = wave_nr_for(n);
   return 3L * nr * ((n + nr - 1) / nr);
 }
-void build_rows(const double* t, const double* f, const double* isg, long n, double* out, long nr) {
-  if (nr <= 0) nr = wave_nr_for(n);
+void build_rows(const double* t, const double* f, const double* isg, long n, double* out) {
+  const long nr = wave_nr_for(n);
   const long rc = (n + nr - 1) / nr;
   for (long c = 0; c < rc; ++c)
     for (long l = 0; l < nr; ++l) {

@@ -86,9 +86,30 @@ struct PrepTask {
   }
 };
 
+// The light-curve polynomial's coefficients from both stars' summed terms
+// tt (star 1's term first) and sin i (already in the record)
+__device__ __forceinline__ void prep_coefficients(double* rec, WalkerConst* wc, const double (&tt)[12]) {
+#define HB_REC(field) rec[&wc->field - (double*)wc]
+  const double si = HB_REC(si);
+  const double s2 = si * si;
+  HB_REC(kconst) = tt[11] + tt[0];
+  HB_REC(kb) = tt[1];
+  HB_REC(kr0) = tt[2] * (0.64 + 0.18 * s2);
+  HB_REC(kr2) = -tt[2] * (0.18 * s2);
+  HB_REC(krs) = -tt[3] * si;
+  HB_REC(kam2) = tt[4];
+  HB_REC(kc21) = tt[5];
+  HB_REC(ks1) = tt[6];
+  HB_REC(ks3) = tt[7];
+  HB_REC(kam3) = tt[8];
+  HB_REC(kc22) = tt[9];
+  HB_REC(kc4) = tt[10];
+#undef HB_REC
+}
+
 // Records of the nb <= NW walkers whose parameters are in L.sp, into L.so
 // (row j at L.so[j * kSoStride]).  Every thread of the workgroup calls it (it
-// holds two workgroup barriers and ends with a third).  tab/wt/base: catalog
+// holds one workgroup barrier -- two when NW = 64 -- and ends with another).  tab/wt/base: catalog
 // mode (the walker's target descriptor), else null.  tab_pc(j): the period
 // [s] of the phase table walker j may use (NaN: no table).  slack(): wave 2's
 // spare work (phase 2).  Waves past the four roles (a workgroup of more than
@@ -98,16 +119,17 @@ struct PrepTask {
 //
 // Phase 1 (before the first barrier) holds every chain that needs no other
 // wave's result, split so that no wave carries much more issue than another:
-//   wave 0: the radius law (both stars);
+//   wave 0: the radius law and the Roche-lobe fraction (both stars);
 //   wave 1: each star's coefficient factors that need no radius (star_coef_x,
 //           with its own sin i);
 //   wave 2: the Teff law, alpha_beam and the Gaia-band Planck factor;
-//   wave 3: the orbit fields, sin/cos i | omega, Roche lobes, periastron and
+//   wave 3: the orbit fields, sin/cos i | omega, periastron and
 //           the phase-table rotations, straight into the record.
 // Phase 2 only combines values across waves: wave 1 multiplies the radii in
-// (star_coef_r, star_coef_finish) and weights each star's terms; wave 3 the
-// eclipse geometry and Roche test; wave 0 the Gaia term; wave 2 runs slack().
-// After the second barrier wave 0 sums the two stars' terms into the record.
+// (star_coef_r, star_coef_finish), weights each star's terms and sums the two
+// stars' into the polynomial coefficients (lane shuffles; with two passes,
+// NW = 64, through LDS after another barrier); wave 3 the eclipse geometry
+// and Roche test; wave 0 the Gaia term; wave 2 runs slack().
 template <int NW, class TabPc, class Slack, class Idle = PrepNoIdle>
 __device__ __forceinline__ void prep_records(PrepShared<NW>& L, int nb, const MagArgs& ma,
                                              const TargetDesc* __restrict__ tab, const int* __restrict__ wt,
@@ -115,6 +137,9 @@ __device__ __forceinline__ void prep_records(PrepShared<NW>& L, int nb, const Ma
                                              const double* mg = nullptr) {
   static_assert(NW >= 1 && NW <= 64, "one walker per lane");
   constexpr int kPass = (2 * NW + 63) / 64;
+  // one pass (NW <= 32): both stars' terms meet by lane shuffles in phase 2
+  // (two barriers in all); two passes: through LDS after a third barrier
+  constexpr bool kShfl = kPass == 1;
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform role
@@ -122,7 +147,7 @@ __device__ __forceinline__ void prep_records(PrepShared<NW>& L, int nb, const Ma
     idle();
     __syncthreads();
     __syncthreads();
-    __syncthreads();
+    if (!kShfl) __syncthreads();
     return;
   }
   // ---- phase 1 ----
@@ -133,7 +158,14 @@ __device__ __forceinline__ void prep_records(PrepShared<NW>& L, int nb, const Ma
       const double* p = &L.sp[k.jc * kNpars];
       const double m = exp10(p[k.star]);
       const double r = exp10(logradius_of_mass(m) + p[7 + k.star] * radius_spread_of_logmass(p[k.star]));
-      if (k.live) L.xs[k.star][1][k.j] = r;
+      // the star's Roche-lobe fraction (RocheOverflow :953-974: q12 = M1/M2, star 2 at 1/q12)
+      const double mo = exp10(p[k.star ^ 1]);
+      const double q12 = k.star ? mo / m : m / mo;
+      const double lf = lobe_fraction(k.star ? 1.0 / q12 : q12);
+      if (k.live) {
+        L.xs[k.star][1][k.j] = r;
+        L.gs[2 + k.star][k.j] = lf;
+      }
     }
   } else if (wv == 1) {  // radius-free coefficient factors
 #pragma unroll
@@ -194,8 +226,6 @@ __device__ __forceinline__ void prep_records(PrepShared<NW>& L, int nb, const Ma
       const double sq1me2 = sqrt(1.0 - e * e);
       double sa, ca;  // (sin, cos) of i (half 0) or omega (half 1)
       sincos(h1 ? p[5] : p[4], &sa, &ca);
-      const double q12 = m1 / m2;
-      const double lf = lobe_fraction(h1 ? 1.0 / q12 : q12);
       // phase-table rotations: psi = T0 2pi/P (half 0, walkers on the table
       // period), del = 0.85 e (half 1)
       const bool use_tab = h1 || Pc == tab_pc(k.jc);  // false for NaN (no table)
@@ -230,7 +260,6 @@ __device__ __forceinline__ void prep_records(PrepShared<NW>& L, int nb, const Ma
           HB_REC(cpsi) = cv;
           HB_REC(pad0) = 0.0;
           L.gs[1][k.j] = a_cgs * (1.0 - e);  // periastron
-          L.gs[2][k.j] = lf;
         } else {
           HB_REC(sw) = sa;
           HB_REC(cw) = ca;
@@ -238,7 +267,6 @@ __device__ __forceinline__ void prep_records(PrepShared<NW>& L, int nb, const Ma
           HB_REC(cwq) = ca * sq1me2;
           HB_REC(sdel) = sv;
           HB_REC(cdel) = cv;
-          L.gs[3][k.j] = lf;
         }
       }
     }
@@ -287,7 +315,21 @@ __device__ __forceinline__ void prep_records(PrepShared<NW>& L, int nb, const Ma
       terms[9] = nself * c.c22;
       terms[10] = nself * c.c4;
       terms[11] = nself;
-      if (k.live) {  // over the factors just read (same lane)
+      if constexpr (kShfl) {
+        // star 2's terms from lane j + NW; lane j (star 1) sums them into the
+        // walker's coefficients (star-1 term first, like the LDS path below)
+        double o[12];
+#pragma unroll
+        for (int q = 0; q < 12; ++q) o[q] = __shfl(terms[q], lane + NW, 64);
+        if (star == 0 && k.live) {
+          double tt[12];
+#pragma unroll
+          for (int q = 0; q < 12; ++q) tt[q] = terms[q] + o[q];
+          double* rec = &L.so[k.j * kSoStride];
+          WalkerConst* wc = reinterpret_cast<WalkerConst*>(rec);
+          prep_coefficients(rec, wc, tt);
+        }
+      } else if (k.live) {  // over the factors just read (same lane)
 #pragma unroll
         for (int q = 0; q < 12; ++q) d[q * NW] = terms[q];
       }
@@ -340,42 +382,31 @@ __device__ __forceinline__ void prep_records(PrepShared<NW>& L, int nb, const Ma
     const double r1 = L.xs[0][1][jc], r2 = L.xs[1][1][jc];
     const double g = ab_mag(band_flux_terms(r1 * kRsun, r2 * kRsun, L.xs[0][0][jc], L.xs[1][0][jc], dist,
                                             L.sp[jc * kNpars + 19]));
-    if (live) L.gs[0][j] = (g - gobs) / gerr;
+    if (live) {
+      const double gr = (g - gobs) / gerr;
+      double* rec = &L.so[j * kSoStride];
+      WalkerConst* wc = reinterpret_cast<WalkerConst*>(rec);
+      HB_REC(blend) = L.sp[j * kNpars + 19];
+      HB_REC(tune) = L.sp[j * kNpars + 20];
+      HB_REC(chi2_extra) = gr * gr;
+    }
   } else {
     slack();
   }
   HB_PREP_MARK(9 + wv);  // phase 2 computed
-  __syncthreads();  // both stars' terms and the Gaia term are in LDS
-  if (wv == 0 && lane < nb) {
-    const int j = lane;
-    const double* p = &L.sp[j * kNpars];
-    double* rec = &L.so[j * kSoStride];
-    WalkerConst* wc = reinterpret_cast<WalkerConst*>(rec);
-    double tt[12];
+  __syncthreads();  // two passes: both stars' terms are in LDS
+  if constexpr (!kShfl) {
+    if (wv == 0 && lane < nb) {
+      const int j = lane;
+      double tt[12];
 #pragma unroll
-    for (int q = 0; q < 12; ++q) tt[q] = L.xs[0][4 + q][j] + L.xs[1][4 + q][j];  // star-1 term first
-    const double gr = L.gs[0][j];
-    const double si = HB_REC(si);
-    // polynomial coefficients
-    const double s2 = si * si;
-    HB_REC(kconst) = tt[11] + tt[0];
-    HB_REC(kb) = tt[1];
-    HB_REC(kr0) = tt[2] * (0.64 + 0.18 * s2);
-    HB_REC(kr2) = -tt[2] * (0.18 * s2);
-    HB_REC(krs) = -tt[3] * si;
-    HB_REC(kam2) = tt[4];
-    HB_REC(kc21) = tt[5];
-    HB_REC(ks1) = tt[6];
-    HB_REC(ks3) = tt[7];
-    HB_REC(kam3) = tt[8];
-    HB_REC(kc22) = tt[9];
-    HB_REC(kc4) = tt[10];
-    HB_REC(blend) = p[19];
-    HB_REC(tune) = p[20];
-    HB_REC(chi2_extra) = gr * gr;
+      for (int q = 0; q < 12; ++q) tt[q] = L.xs[0][4 + q][j] + L.xs[1][4 + q][j];  // star-1 term first
+      double* rec = &L.so[j * kSoStride];
+      prep_coefficients(rec, reinterpret_cast<WalkerConst*>(rec), tt);
+    }
+    __syncthreads();
   }
 #undef HB_REC
-  __syncthreads();
 }
 
 }  // namespace hbk

@@ -84,12 +84,6 @@ class HBLikelihood:
         kind = self.lib.hb_ctx_eval_kind(self._h)
         return ("hb_eval_wave_kernel", "hb_eval_block_kernel", "hb_eval_kernel")[kind]
 
-    @property
-    def block_rows(self) -> int:
-        """Lane rows of the block kernel's warm-chain model pass (0: the strided
-        cold pass only, or not a block-kernel context)."""
-        return int(self.lib.hb_ctx_block_rows(self._h))
-
     def fused_wpb(self, w: int) -> int:
         """Walkers per workgroup of the single fused launch loglike_dev makes
         for w walkers (records in the eval kernel's prologue), 0 when it makes

@@ -173,11 +173,6 @@ int hb_ctx_template_in_lds(const hb_ctx *ctx);
  * 64 x waves), 2 hb_eval_kernel (LDS-walking select; template in LDS or an
  * HBM slab). */
 int hb_ctx_eval_kind(const hb_ctx *ctx);
-/* hb_eval_block_kernel contexts: the lane rows (64 x waves per walker) of its
- * warm-chain model pass -- thread r solves cadences r*rc .. r*rc + rc - 1 as
- * warm Kepler chains, for walkers with e <= 0.8 on closely spaced cadences --
- * or 0 when every walker takes the strided cold pass (other kinds: 0). */
-int hb_ctx_block_rows(const hb_ctx *ctx);
 /* on != 0: batches of fewer than 512 walkers (N <= 2048) run the multi-wave
  * kernel (several waves per walker: lower latency when most SIMDs would sit
  * idle).  Default off: one wave per walker at every batch size, which keeps a
