@@ -2475,8 +2475,11 @@ hipError_t launch_prep(const double* d_params, int nwalk, const MagArgs& ma, Wal
                        double2* ph, const int* w0, int ntargets, double* tab_pc) {
   if (nwalk <= 0) return hipSuccess;
   if (t == nullptr || (tab != nullptr && w0 == nullptr) || !HB_PHASE_TAB) ph = nullptr;
-  // the most walkers per workgroup that still leave >= 256 workgroups (one per CU)
-  static const int wmax = getenv("HB_PREP_WMAX") ? atoi(getenv("HB_PREP_WMAX")) : 64;  // A/B knob
+  // the most walkers per workgroup that still leave >= 256 workgroups (one per CU),
+  // at most 32: both stars' lane tasks then fit one pass (prep_records); 64
+  // walkers (two passes) measured 0.1648 vs 0.1640 ms per C5 call
+  // (profiles/r04/r04k_c5_w*.json, interleaved)
+  static const int wmax = getenv("HB_PREP_WMAX") ? atoi(getenv("HB_PREP_WMAX")) : 32;  // A/B knob
   const int nw = (wmax >= 64 && nwalk >= 256 * 64) ? 64 : (wmax >= 32 && nwalk >= 256 * 32) ? 32 : kPrepWalkers;
   const int nb = (nwalk + nw - 1) / nw;
   auto kern = nw == 64 ? hb_prep_kernel<64> : nw == 32 ? hb_prep_kernel<32> : hb_prep_kernel<kPrepWalkers>;

@@ -1,5 +1,6 @@
 #!/bin/bash
-# Full GPU session: parity tests, smoke, C2/C3/C5 bench lines, bench-only
+# Full GPU session: parity tests, smoke, C2/C3/C5/C4 bench lines, wave clocks
+# of the fused C2 launch (when the HB_WAVE_CLOCKS variant is built), bench-only
 # kernel trace.  $1 = profile tag.  Stops on any fault-like exit status (>1)
 # without starting further GPU work.
 TAG=${1:-r01}
@@ -17,4 +18,8 @@ step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 step bench_c2 600 python bench.py
 step bench_c3 600 python bench.py --config C3 --steps 20 --warmup 3 --no-cpu-baseline --sampler-iters 0 --dropin-iters 0
 step bench_c5 600 python bench.py --config C5 --steps 100 --warmup 10 --no-cpu-baseline --sampler-iters 0 --dropin-iters 0
+step bench_c4 600 python bench.py --config C4 --no-cpu-baseline --sampler-iters 0 --dropin-iters 0
+if [ -f hb_mcmc_amd/lib/variants/libhbmi_clkf.so ]; then
+  step wave_clocks 300 env HBMI_LIB=hb_mcmc_amd/lib/variants/libhbmi_clkf.so python -u scripts/wave_clocks.py --fused
+fi
 bash scripts/profile.sh $TAG
