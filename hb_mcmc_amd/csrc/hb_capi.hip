@@ -743,6 +743,8 @@ static int catalog_layout(hb_catalog* c, const int* walkers, hipStream_t s) {
 // the catalog's walkers, per-target phase tables in its tail), then every
 // size class's eval launch on its stream (forked at the call's start).  The
 // evals evaluate the per-target phase-table entries in place.
+// HB_CAT_FUSED=2 (A/B knob): a records launch per class on the class's stream
+// (launch_prep_list), so one class's records overlap another's eval.
 // HB_CAT_FUSED=1 (A/B knob): each one-wave class of up to 16 cadences per lane
 // is ONE fused launch (its walkers' records in the eval kernel's prologue),
 // the other classes a records launch for their walkers (launch_prep_list) and
@@ -752,8 +754,9 @@ static int catalog_layout(hb_catalog* c, const int* walkers, hipStream_t s) {
 // lengths and eccentricities) is done, where one-wave workgroups backfill.
 static int catalog_run(hb_catalog* c, const double* d_params, double* d_logl, hipStream_t s) {
   if (c->total == 0) return 0;
-  static const bool fused = cat_env("HB_CAT_FUSED", 0) != 0;
-  if (!fused) {
+  static const int mode = cat_env("HB_CAT_FUSED", 0);  // 0 one records launch, 1 fused classes, 2 per class
+  const bool fused = mode == 1, per_class = mode != 0;
+  if (!per_class) {
     MagArgs unused{};
     HB_TRY(hbk::launch_prep(d_params, c->total, unused, c->d_wc, s, c->d_tab, c->d_wt, c->d_t, 0, c->d_ph, c->d_w0,
                             c->ntargets),
@@ -800,9 +803,9 @@ static int catalog_run(hb_catalog* c, const double* d_params, double* d_logl, hi
              "fused eval launch");
       continue;
     }
-    if (fused)
+    if (per_class)
       HB_TRY(hbk::launch_prep_list(d_params, lst, cnt, c->d_wc, sj, c->d_tab, c->d_wt, c->d_w0), "records launch");
-    HB_TRY(hbk::launch_eval_multi(vpt, c->class_slab[cl], c->d_t, fused ? nullptr : c->d_ph, c->d_f, c->d_s, c->d_rows,
+    HB_TRY(hbk::launch_eval_multi(vpt, c->class_slab[cl], c->d_t, per_class ? nullptr : c->d_ph, c->d_f, c->d_s, c->d_rows,
                                   c->d_tab, c->d_wt,
                                   lst, cnt, c->d_wc, d_logl, sj, dq, wpw),
            "eval launch");
