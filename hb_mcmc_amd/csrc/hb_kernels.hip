@@ -823,6 +823,14 @@ __device__ __forceinline__ void model_pass_chain(const double* __restrict__ tT, 
 #ifndef HB_PIPE
 #define HB_PIPE 1
 #endif
+// the walker constants are reloaded (scalar loads) at every pipelined step
+// instead of being held in SGPRs across the loop: SGPR spills 138 -> 111
+// (fused C2 kernel) and 206 -> 142 (device-sampler eval + Hastings), time
+// unchanged (C2 41.38-41.43 vs 41.37-41.39 us per step, device loop 0.0925
+// vs 0.0929 ms; profiles/r04/r04n_*.json)
+#ifndef HB_PIPE_RELOAD
+#define HB_PIPE_RELOAD 1
+#endif
 template <int VPT, int NR = 64, bool VT = false>
 __device__ __forceinline__ void model_pass_chain_pipe(const double* __restrict__ tT, const double2* __restrict__ ph,
                                                       int n, const Rows& rw, const WalkerConst& w, double* vals,
@@ -866,6 +874,9 @@ __device__ __forceinline__ void model_pass_chain_pipe(const double* __restrict__
   pc.begin(lc);
   for (int j = 1; j < lc; ++j) {
     pc.step(j, lc);
+#if HB_PIPE_RELOAD
+    __asm__ volatile("" ::: "memory");
+#endif
 #pragma unroll
     for (int k = 0; k < KC; ++k) tk[k] = tT[min(k * lc + j, rw.rc - 1) * NR + lane];
     double m[KC], E[KC], s[KC], c[KC], ys[KC], v[KC], dd[KC], zz[KC];
