@@ -45,8 +45,10 @@ def is_eval(r):
     return "hb_eval_wave_kernel<" in k and ", true," in k
 
 
-# hb_prep_kernel: 64 / 32 / 16 walkers per 256-thread workgroup (hbk::launch_prep: the most that leave >= 256 groups)
-_pw = 64 if walkers >= 256 * 64 else 32 if walkers >= 256 * 32 else 16
+# hb_prep_kernel: 32 / 16 walkers per 256-thread workgroup (hbk::launch_prep: the most that leave >= 256
+# groups, at most 32 by default; HB_PREP_WMAX=64 for runs that allow 64)
+_wmax = int(os.environ.get("HB_PREP_WMAX", "32"))
+_pw = 64 if (_wmax >= 64 and walkers >= 256 * 64) else 32 if walkers >= 256 * 32 else 16
 prep_grid = ((walkers + _pw - 1) // _pw) * 256
 ev = collections.defaultdict(float)
 calls = collections.Counter()
