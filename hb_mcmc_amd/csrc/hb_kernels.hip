@@ -487,18 +487,28 @@ struct DeferQ {
   char* e;  // this wave's entries (the base is held in VGPRs: no SGPR spill reloads per push)
   int n;    // entries (wave-uniform)
 };
+// HB_DQ_SINK: the push is branch-free -- lanes that queue nothing store into
+// the wave's sink entry (the 16 B in front of its region, never read), so the
+// model pass's step stays one basic block that the scheduler can interleave
+// (an exec-mask branch per push split it); 0: the branching push.
+#ifndef HB_DQ_SINK
+#define HB_DQ_SINK 1
+#endif
+constexpr int kDqSink = HB_DQ_SINK ? 1 : 0;  // entries in front of a wave's region
 __device__ __forceinline__ void dq_push(DeferQ& q, bool push, double a, int code) {
   const unsigned long long bal = wave_ballot(push);
-  if (push) {
-    const uint32_t pos = __builtin_amdgcn_mbcnt_hi((unsigned)(bal >> 32),
-                                                   __builtin_amdgcn_mbcnt_lo((unsigned)bal, (unsigned)q.n));
-    // global address space spelled out (the VGPR base hides it from inference)
-    typedef __attribute__((address_space(1))) double gdouble;
-    typedef __attribute__((address_space(1))) long long glong;
-    gdouble* p = (gdouble*)(q.e + (size_t)(pos << 4));
-    p[0] = a;
-    ((glong*)p)[1] = (long long)code;
-  }
+  // global address space spelled out (the VGPR base hides it from inference)
+  typedef double d2v __attribute__((ext_vector_type(2)));
+  typedef __attribute__((address_space(1))) d2v gdouble2;
+  const uint32_t pos = __builtin_amdgcn_mbcnt_hi((unsigned)(bal >> 32),
+                                                 __builtin_amdgcn_mbcnt_lo((unsigned)bal, (unsigned)q.n));
+  const d2v ent = {a, __longlong_as_double((long long)code)};
+#if HB_DQ_SINK
+  const long off = push ? (long)pos << 4 : -16L;
+  *(gdouble2*)(q.e + off) = ent;
+#else
+  if (push) *(gdouble2*)(q.e + (size_t)(pos << 4)) = ent;
+#endif
   q.n += __popcll(bal);
 }
 // t: the light curve's times in cadence order (slow-path entries: the cadence
@@ -831,6 +841,12 @@ __device__ __forceinline__ void model_pass_chain(const double* __restrict__ tT, 
 #ifndef HB_PIPE_RELOAD
 #define HB_PIPE_RELOAD 1
 #endif
+#ifndef HB_EMIT_LATE
+#define HB_EMIT_LATE 1
+#endif
+#ifndef HB_POLY_PIN
+#define HB_POLY_PIN 1
+#endif
 template <int VPT, int NR = 64, bool VT = false>
 __device__ __forceinline__ void model_pass_chain_pipe(const double* __restrict__ tT, const double2* __restrict__ ph,
                                                       int n, const Rows& rw, const WalkerConst& w, double* vals,
@@ -883,8 +899,23 @@ __device__ __forceinline__ void model_pass_chain_pipe(const double* __restrict__
     bool ok = true, fine;
     chain_kepler_warm<KC>(tk, w, st, m, E, s, c, ys, fine, ok);  // step j
     flux_poly_inv_k<KC>(st.s, st.c, st.inv, w, v, dd, zz);      // step j - 1, same block
+#if HB_POLY_PIN
+    // the polynomial's values are materialised here, beside step j's solve:
+    // otherwise the compiler sinks them into emit's conditional blocks, after
+    // the solve, and the two no longer interleave
+#pragma unroll
+    for (int k = 0; k < KC; ++k) __asm__ volatile("" : "+v"(v[k]), "+v"(dd[k]), "+v"(zz[k]));
+#endif
+#if HB_EMIT_LATE
+    // step j - 1's stores and pushes after step j's finish: their branches
+    // (the wave-uniform row test) then do not split the solve and polynomial
+    const bool pbad = !pend_ok;
+    chain_finish_warm<KC>(tk, w, wave_all(fine), fine, m, E, s, c, ys, ok, st);
+    emit(j - 1, v, dd, zz, pbad);
+#else
     emit(j - 1, v, dd, zz, !pend_ok);
     chain_finish_warm<KC>(tk, w, wave_all(fine), fine, m, E, s, c, ys, ok, st);
+#endif
     pend_ok = ok;
   }
   {  // the last step's polynomial
@@ -1928,7 +1959,8 @@ __global__ __launch_bounds__(64 * WPB * WPW) HB_WPE_ATTR void hb_eval_wave_kerne
   PairShared* ps = reinterpret_cast<PairShared*>(smem + slab_bytes + 8 * kCandMax);  // WPW == 2 only
   DeferQ dq{nullptr, 0};
   if (HB_GQ) {  // this wave's region of the deferred queue (64 VPT entries of 16 B)
-    dq.e = reinterpret_cast<char*>(dqbuf) + ((size_t)slot * WPW + (size_t)h) * (size_t)(64 * VPT * 16);
+    dq.e = reinterpret_cast<char*>(dqbuf) + ((size_t)slot * WPW + (size_t)h) * (size_t)((64 * VPT + kDqSink) * 16) +
+           kDqSink * 16;
     __asm__ volatile("" : "+v"(dq.e));  // a VGPR pair, not one more scalar to spill
   }
   {
@@ -2955,7 +2987,7 @@ size_t wave_slab_bytes(long n) {
 // bytes of the one-wave kernel's deferred queue for `count` walkers of wpw
 // waves (HB_GQ)
 size_t wave_queue_bytes(int vpt, long count, int wpw) {
-  return HB_GQ ? (size_t)count * (size_t)wpw * (size_t)64 * (size_t)vpt * 16 : 0;
+  return HB_GQ ? (size_t)count * (size_t)wpw * ((size_t)64 * (size_t)vpt + kDqSink) * 16 : 0;
 }
 
 // slab | select candidates | eclipse queue (chain model pass only) | the
