@@ -611,6 +611,34 @@ def test_warm_start_paths_against_oracle(hbmi, oracle, order):
     assert (np.abs(tm - ref)[ok] <= tol[ok]).all()
 
 
+@pytest.mark.parametrize("n", [1024, 1500, 3000])
+def test_slow_path_full_deferred_queue(hbmi, oracle, n):
+    """Times shifted by 2.5e5 days put every cadence's angle outside the fast
+    reducer's domain (|x| >= 2^19 rad at P = 2.07 d), so every cadence of every
+    wave is queued for the reference-order slow path: each wave's deferred
+    queue fills to its capacity (64 VPT entries, with the branch-free push's
+    sink entry in front of it).  One-wave (N = 1024), pair (1500) and rows
+    (3000) plans; logL and templates against the oracle, and batch reversal
+    bit-identical."""
+    from hb_mcmc_amd import synth
+    from hb_mcmc_amd.likelihood import HBLikelihood
+
+    t, f, s = synth.dataset(n, oracle.light_curve)
+    t = t + 2.5e5
+    assert (2 * np.pi * t / 10.0 ** synth.THETA_STAR[2] >= 2.0 ** 19).all()
+    P = synth.walkers(64, seed=n + 3, roche_frac=0.1)
+    with HBLikelihood(t, f, s) as L:
+        ll = L.loglike(P)
+        rev = L.loglike(P[::-1].copy())[::-1]
+        tm = L.light_curve(P)
+    assert np.array_equal(ll, rev, equal_nan=True)
+    close_logl(ll, oracle.loglike_batch(t, f, s, P, synth.MAG_DEFAULT, synth.MAGERR_DEFAULT, 8))
+    ref = oracle.light_curve_batch(t, P, 8)
+    ok = ~np.isnan(ref).any(1)
+    tol = lc_tol(P[:, 3], ref)
+    assert (np.abs(tm - ref)[ok] <= tol[ok]).all()
+
+
 # ------------------------------------------------- write_lc_to_file
 def test_write_lc_to_file_bytes(hbmi, tmp_path):
     """write_lc_to_file (likelihood3.c:880-941) through libhbmi.so: the light
