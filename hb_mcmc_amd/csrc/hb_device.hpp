@@ -759,6 +759,12 @@ __device__ __forceinline__ bool newton_k(double e, const double (&m)[K], double 
 // The photometric polynomial of K cadences from (sin, cos) of the solved
 // eccentric anomaly, without the eclipse; dd = (projected separation / a)^2
 // and zz (sign carrier of Z1 - Z2) for the eclipse test.
+// HB_LEAN: the warm start's A and B with 0.5 e and e / 6 taken once per step
+// (two multiplies fewer per cadence), and the polynomial's cos 2u as
+// 1 - 2 sin^2 u (two fewer); 0: the round-3 expressions
+#ifndef HB_LEAN
+#define HB_LEAN 1
+#endif
 #ifndef HB_FLUX_V
 #define HB_FLUX_V 2  // 2: numerator form (beta = 1 / den); 1: through cos/sin nu
 #endif
@@ -796,8 +802,13 @@ __device__ __forceinline__ void flux_poly_inv_k(const double (&s)[K], const doub
     dd[k] = (den * den) * fma(cu, cu, sci * sci);  // sqrt only on eclipse lanes
     zz[k] = su * w.si;
 #endif
+#if HB_LEAN
+    const double su2 = su * su;
+    const double c2 = fma(-2.0, su2, 1.0);  // cos 2u (cu^2 + su^2 = 1 to rounding)
+#else
     const double c2 = (cu - su) * (cu + su);          // cos 2u
     const double su2 = su * su;
+#endif
     const double s3 = su * fma(-4.0, su2, 3.0);       // sin 3u
     const double c4 = fma(2.0 * c2, c2, -1.0);        // cos 4u
     const double b2 = b * b;
@@ -923,6 +934,9 @@ __device__ __forceinline__ void hb_cadence_flux_chain(const double (&t)[K], cons
                                                       double (&v)[K], double (&dd)[K], double (&zz)[K],
                                                       bool& bad) {
   const double e = w.e;
+#if HB_LEAN
+  const double he = 0.5 * e, e6 = e * (1.0 / 6.0);  // the series start's A = he s / f', B = e6 c / f'
+#endif
   double m[K], E[K], s[K], c[K], yk[K];
   bool ok = true, exact = false, plus[K];
 #ifndef HB_WARM
@@ -986,8 +1000,13 @@ __device__ __forceinline__ void hb_cadence_flux_chain(const double (&t)[K], cons
       r = fma(fma(-g, r, 1.0), r, r);
 #endif
       const double x = Dc * r;
+#if HB_LEAN
+      const double A = (he * st.s[k]) * r;
+      const double B = (e6 * st.c[k]) * r;
+#else
       const double A = (e * st.s[k]) * (0.5 * r);
       const double B = (e * st.c[k]) * (r * (1.0 / 6.0));
+#endif
       const double C = fma(2.0 * A, A, -B);
       const double dl = fma(x * x, fma(C, x, -A), x);
       double E0 = fma(q, kTwoPi, st.E[k]) + dl;
@@ -1156,6 +1175,9 @@ __device__ __forceinline__ void chain_kepler_warm(const double (&t)[K], const Wa
                                                   double (&m)[K], double (&E)[K], double (&s)[K], double (&c)[K],
                                                   double (&ys)[K], bool& fine, bool& ok) {
   const double e = w.e;
+#if HB_LEAN
+  const double he = 0.5 * e, e6 = e * (1.0 / 6.0);
+#endif
   fine = true;
 #pragma unroll
   for (int k = 0; k < K; ++k) {
@@ -1170,8 +1192,13 @@ __device__ __forceinline__ void chain_kepler_warm(const double (&t)[K], const Wa
     const double Dc = fma(-q, kTwoPi, D);
     const double r = st.inv[k];
     const double x = Dc * r;
+#if HB_LEAN
+    const double A = (he * st.s[k]) * r;
+    const double B = (e6 * st.c[k]) * r;
+#else
     const double A = (e * st.s[k]) * (0.5 * r);
     const double B = (e * st.c[k]) * (r * (1.0 / 6.0));
+#endif
     const double C = fma(2.0 * A, A, -B);
     const double dl = fma(x * x, fma(C, x, -A), x);
     double E0 = fma(q, kTwoPi, st.E[k]) + dl;
