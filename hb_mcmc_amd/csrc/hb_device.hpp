@@ -347,6 +347,35 @@ __device__ __forceinline__ StarCoef star_coef(double pd, double ma, double mb, d
 // ------------------------------------------------------------------------
 // per-walker preparation
 // ------------------------------------------------------------------------
+// HB_SU2: the polynomial's harmonics in x = sin^2 u.  cos 2u = 1 - 2x,
+// cos 4u = 1 - 8x + 8x^2, sin 3u = sin u (3 - 4x), so each beta-power's
+// coefficient is a polynomial in x (sin u) with the harmonic weights folded
+// into the record once per walker: 8 fp64 instructions per cadence instead of
+// 13.  The record's k* fields then hold the x-form (see su2_form).
+#ifndef HB_SU2
+#define HB_SU2 1
+#endif
+
+// the cos-harmonic coefficients (kr0, kr2 | kam2, kc21 | ks1, ks3 | kam3,
+// kc22, kc4 of 1, cos 2u, sin u, sin 3u, cos 4u) rewritten as polynomials in
+// x = sin^2 u (HB_SU2; identity otherwise)
+__host__ __device__ inline void su2_form(double& kr0, double& kr2, double& kam2, double& kc21, double& ks1, double& ks3,
+                                         double& kam3, double& kc22, double& kc4) {
+#if HB_SU2
+  kr0 = kr0 + kr2;  // kr0 + kr2 (1 - 2x)
+  kr2 = -2.0 * kr2;
+  kam2 = kam2 + kc21;  // kam2 + kc21 (1 - 2x)
+  kc21 = -2.0 * kc21;
+  ks1 = fma(3.0, ks3, ks1);  // sin u (ks1 + ks3 (3 - 4x))
+  ks3 = -4.0 * ks3;
+  kam3 = (kam3 + kc22) + kc4;  // kam3 + kc22 (1 - 2x) + kc4 (1 - 8x + 8x^2)
+  kc22 = fma(-8.0, kc4, -2.0 * kc22);
+  kc4 = 8.0 * kc4;
+#else
+  (void)kr0; (void)kr2; (void)kam2; (void)kc21; (void)ks1; (void)ks3; (void)kam3; (void)kc22; (void)kc4;
+#endif
+}
+
 __device__ inline void hb_prepare_walker(const double* __restrict__ p, const double* __restrict__ mag,
                                          const double* __restrict__ magerr, WalkerConst& w) {
   const double pd = exp10(p[2]);          // period [d]
@@ -399,6 +428,7 @@ __device__ inline void hb_prepare_walker(const double* __restrict__ p, const dou
   w.kam3 = n1 * c1.am3 + n2 * c2.am3;
   w.kc22 = n1 * c1.c22 + n2 * c2.c22;
   w.kc4 = n1 * c1.c4 + n2 * c2.c4;
+  su2_form(w.kr0, w.kr2, w.kam2, w.kc21, w.ks1, w.ks3, w.kam3, w.kc22, w.kc4);
 
   // eclipse
   w.r1 = st.r1;
@@ -552,17 +582,25 @@ __device__ __noinline__ double hb_cadence_flux_slow(double t, const WalkerConst*
 __device__ __forceinline__ double hb_cadence_flux(double t, const WalkerConst& w) {
   const Orbit o = hb_orbit(t, w);
   const double cu = o.cu, su = o.su;
-  const double c2 = (cu - su) * (cu + su);   // cos 2u
-  const double s3 = su * (3.0 - 4.0 * su * su);  // sin 3u
-  const double c4 = 2.0 * c2 * c2 - 1.0;     // cos 4u
   const double b = o.beta;
   const double b2 = b * b;
   const double b3 = b2 * b;
   double v = w.kconst + w.kb * cu;
+#if HB_SU2
+  const double x = su * su;  // the record's harmonics in x = sin^2 u (su2_form)
+  v += b2 * (w.kr0 + w.kr2 * x + w.krs * su);
+  v += b3 * (w.kam2 + w.kc21 * x);
+  v += (b2 * b2) * (su * (w.ks1 + w.ks3 * x));
+  v += (b3 * b2) * (w.kam3 + x * (w.kc22 + w.kc4 * x));
+#else
+  const double c2 = (cu - su) * (cu + su);   // cos 2u
+  const double s3 = su * (3.0 - 4.0 * su * su);  // sin 3u
+  const double c4 = 2.0 * c2 * c2 - 1.0;     // cos 4u
   v += b2 * (w.kr0 + w.kr2 * c2 + w.krs * su);
   v += b3 * (w.kam2 + w.kc21 * c2);
   v += (b2 * b2) * (w.ks1 * su + w.ks3 * s3);
   v += (b3 * b2) * (w.kam3 + w.kc22 * c2 + w.kc4 * c4);
+#endif
   // eclipse: only lanes with overlap take the branch
   if (o.dR < w.rbig + w.rsml && o.zz != 0.0) {
     const double area = overlap_area(w.rbig, w.rsml, w.dcrit, o.dR);
@@ -802,6 +840,15 @@ __device__ __forceinline__ void flux_poly_inv_k(const double (&s)[K], const doub
     dd[k] = (den * den) * fma(cu, cu, sci * sci);  // sqrt only on eclipse lanes
     zz[k] = su * w.si;
 #endif
+    const double b2 = b * b;
+    // b^2 [A2 + b (A3 + b (A4 + b A5))] + kconst + kb cos u
+#if HB_SU2
+    const double x = su * su;  // the harmonics as polynomials in sin^2 u (su2_form)
+    const double a5 = fma(fma(w.kc4, x, w.kc22), x, w.kam3);
+    const double a4 = su * fma(w.ks3, x, w.ks1);
+    const double a3 = fma(w.kc21, x, w.kam2);
+    const double a2 = fma(w.krs, su, fma(w.kr2, x, w.kr0));
+#else
 #if HB_LEAN
     const double su2 = su * su;
     const double c2 = fma(-2.0, su2, 1.0);  // cos 2u (cu^2 + su^2 = 1 to rounding)
@@ -811,12 +858,11 @@ __device__ __forceinline__ void flux_poly_inv_k(const double (&s)[K], const doub
 #endif
     const double s3 = su * fma(-4.0, su2, 3.0);       // sin 3u
     const double c4 = fma(2.0 * c2, c2, -1.0);        // cos 4u
-    const double b2 = b * b;
-    // b^2 [A2 + b (A3 + b (A4 + b A5))] + kconst + kb cos u
     const double a5 = fma(w.kc4, c4, fma(w.kc22, c2, w.kam3));
     const double a4 = fma(w.ks3, s3, w.ks1 * su);
     const double a3 = fma(w.kc21, c2, w.kam2);
     const double a2 = fma(w.krs, su, fma(w.kr2, c2, w.kr0));
+#endif
     double h = fma(b, a5, a4);
     h = fma(b, h, a3);
     h = fma(b, h, a2);
@@ -1296,5 +1342,6 @@ __device__ __forceinline__ void chain_first(const double (&t)[K], const double2 
 #else
 #define HB_CHAIN_SPLIT 0
 #endif
+
 
 }  // namespace hbdev

@@ -104,6 +104,8 @@ __device__ __forceinline__ void prep_coefficients(double* rec, WalkerConst* wc, 
   HB_REC(kam3) = tt[8];
   HB_REC(kc22) = tt[9];
   HB_REC(kc4) = tt[10];
+  su2_form(HB_REC(kr0), HB_REC(kr2), HB_REC(kam2), HB_REC(kc21), HB_REC(ks1), HB_REC(ks3), HB_REC(kam3), HB_REC(kc22),
+           HB_REC(kc4));
 #undef HB_REC
 }
 
