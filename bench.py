@@ -365,9 +365,10 @@ def roofline(config, kernel_ms, evals_per_call, hbm_bytes_per_call, extra):
     """The dominant kernel's roofline.  Bound: the fp64 VALU (the path is
     elementwise fp64 transcendental work + a select).  t/f/sigma
     stay L2-resident; the measured HBM traffic (`traffic`, PMC) is mostly the
-    deferred eclipse queue -- 30.8 MB per C2 launch against the 101 MB
+    deferred eclipse queue -- 31 MB per C2 launch against the 101 MB
     algorithmic figure, DESIGN.md section 3.  achieved = counted fp64 flops per call (PMC) / the call's
-    HIP-event duration; the VALU-issue fraction prices the counted fp64 (4
+    HIP-event duration (counted work: a build that removes instructions reads a
+    lower frac at the same time); the VALU-issue fraction prices the counted fp64 (4
     clk per wave64 instruction) and other VALU instructions (2 clk) against
     1024 SIMDs at 2.4 GHz.  The SURVEY 8(d) algorithmic-bytes figure is kept
     as roofline.hbm.  Without counters for this kernel build the HBM figure
