@@ -803,6 +803,12 @@ __device__ __forceinline__ bool newton_k(double e, const double (&m)[K], double 
 #ifndef HB_LEAN
 #define HB_LEAN 1
 #endif
+// HB_LEAN2 (split chain path): the chain carries its mean anomaly, so the warm
+// start's D needs no E - e sin E, and 0.5e, e/6 and 2^-51/e are taken once per
+// model pass (WarmK) -- two fp64 instructions fewer per cadence
+#ifndef HB_LEAN2
+#define HB_LEAN2 1
+#endif
 #ifndef HB_FLUX_V
 #define HB_FLUX_V 2  // 2: numerator form (beta = 1 / den); 1: through cos/sin nu
 #endif
@@ -970,7 +976,15 @@ struct ChainState {
 #if HB_RCP_REUSE
   double inv[K];
 #endif
+#if HB_LEAN2
+  double m[K];  // the mean anomaly E solved (split chain path): the next step's D = m' - m
+#endif
 };
+// per-walker factors of the split warm step, taken once per model pass
+struct WarmK {
+  double he, e6, ke;  // 0.5 e, e / 6, 2^-51 / e (the convergence test z <= ke den)
+};
+__device__ __forceinline__ WarmK warm_k(double e) { return WarmK{0.5 * e, e * (1.0 / 6.0), 0x1p-51 / e}; }
 
 // v: the polynomial part only; the caller applies the eclipse where
 // eclipse_lane(w, dd, zz) (compacted across the wave, see model_pass_chain)
@@ -1219,10 +1233,15 @@ __device__ __forceinline__ void hb_cadence_flux_chain(const double (&t)[K], cons
 template <int K>
 __device__ __forceinline__ void chain_kepler_warm(const double (&t)[K], const WalkerConst& w, const ChainState<K>& st,
                                                   double (&m)[K], double (&E)[K], double (&s)[K], double (&c)[K],
-                                                  double (&ys)[K], bool& fine, bool& ok) {
+                                                  double (&ys)[K], bool& fine, bool& ok, const WarmK& wk) {
   const double e = w.e;
-#if HB_LEAN
+#if HB_LEAN2
+  const double he = wk.he, e6 = wk.e6;
+#elif HB_LEAN
   const double he = 0.5 * e, e6 = e * (1.0 / 6.0);
+  (void)wk;
+#else
+  (void)wk;
 #endif
   fine = true;
 #pragma unroll
@@ -1233,7 +1252,11 @@ __device__ __forceinline__ void chain_kepler_warm(const double (&t)[K], const Wa
   }
 #pragma unroll
   for (int k = 0; k < K; ++k) {
+#if HB_LEAN2
+    const double D = m[k] - st.m[k];
+#else
     const double D = m[k] - fma(-e, st.s[k], st.E[k]);
+#endif
     const double q = rint(D * 0.15915494309189533577);
     const double Dc = fma(-q, kTwoPi, D);
     const double r = st.inv[k];
@@ -1266,7 +1289,11 @@ __device__ __forceinline__ void chain_kepler_warm(const double (&t)[K], const Wa
     const double d = ((E0 - e * s0) - m[k]) * y;
     E0 = E0 - d;
     const double z = d * d;
+#if HB_LEAN2
+    fine &= (fabs(d) <= 0x1p-22) & (z <= wk.ke * den);
+#else
     fine &= (fabs(d) <= 0x1p-22) & (e * z <= 0x1p-51 * den);
+#endif
     rotate_back_tiny(d, z, s0, c0);
     E[k] = E0;
     s[k] = s0;
@@ -1294,6 +1321,9 @@ __device__ __forceinline__ void chain_finish_warm(const double (&t)[K], const Wa
       st.E[k] = E[k];
       st.s[k] = s[k];
       st.c[k] = c[k];
+#if HB_LEAN2
+      st.m[k] = m[k];
+#endif
     }
     return;
   }
@@ -1319,6 +1349,9 @@ __device__ __forceinline__ void chain_finish_warm(const double (&t)[K], const Wa
     st.s[k] = s[k];
     st.c[k] = c[k];
     st.inv[k] = fast_rcp(fma(-e, c[k], 1.0));
+#if HB_LEAN2
+    st.m[k] = m[k];
+#endif
   }
 }
 // a chain's first cadence: the reference's start (table entries) and Newton
@@ -1337,6 +1370,9 @@ __device__ __forceinline__ void chain_first(const double (&t)[K], const double2 
     st.s[k] = s[k];
     st.c[k] = c[k];
     st.inv[k] = fast_rcp(fma(-e, c[k], 1.0));
+#if HB_LEAN2
+    st.m[k] = m[k];
+#endif
   }
 }
 #else

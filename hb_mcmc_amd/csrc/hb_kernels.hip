@@ -887,6 +887,7 @@ __device__ __forceinline__ void model_pass_chain_pipe(const double* __restrict__
       }
     }
   };
+  const WarmK wk = warm_k(w.e);
   pc.begin(lc);
   for (int j = 1; j < lc; ++j) {
     pc.step(j, lc);
@@ -897,7 +898,7 @@ __device__ __forceinline__ void model_pass_chain_pipe(const double* __restrict__
     for (int k = 0; k < KC; ++k) tk[k] = tT[min(k * lc + j, rw.rc - 1) * NR + lane];
     double m[KC], E[KC], s[KC], c[KC], ys[KC], v[KC], dd[KC], zz[KC];
     bool ok = true, fine;
-    chain_kepler_warm<KC>(tk, w, st, m, E, s, c, ys, fine, ok);  // step j
+    chain_kepler_warm<KC>(tk, w, st, m, E, s, c, ys, fine, ok, wk);  // step j
     flux_poly_inv_k<KC>(st.s, st.c, st.inv, w, v, dd, zz);      // step j - 1, same block
 #if HB_POLY_PIN
     // the polynomial's values are materialised here, beside step j's solve:
