@@ -384,9 +384,8 @@ extern "C" int hbx_loglik_accept_dev(hb_ctx* c, const double* d_params, int w, d
                    static_cast<const hbds::AccArgs*>(acc), false);
 }
 
-// internal (device sampler): LDS bytes each wave of the fused likelihood +
-// Hastings launch owns (the swap tail restages its segment there); 0 when the
-// plan has no one-wave path
+// internal (device sampler): LDS bytes each wave of the one-wave likelihood
+// kernel owns (slab, survivors); 0 when the plan has no one-wave path
 extern "C" long hbx_ctx_wave_lds(const hb_ctx* c) {
   if (!c || c->plan.vpt == 0) return 0;
   return (long)hbk::wave_lds_bytes(c->plan.slab_bytes, c->plan.vpt, c->plan.wpw);
@@ -486,6 +485,18 @@ static int catalog_class_of(long n) {
   for (int c = 0; c < kCatClasses; ++c)
     if (rc <= kCatRcHi[c]) return c;
   return -1;
+}
+
+// the launch geometry of class cl: cadences per lane (the kernel's VPT) and
+// waves per walker
+static void catalog_class_geometry(int cl, int& vpt, int& wpw) {
+  vpt = 1;
+  while (vpt < kCatRcHi[cl]) vpt <<= 1;
+  wpw = 1;
+  if (cl == kCatClasses - 1) {  // a pair of waves of <= 16 cadences per lane
+    vpt = 16;
+    wpw = 2;
+  }
 }
 
 struct hb_catalog {
@@ -700,9 +711,11 @@ static int catalog_layout(hb_catalog* c, const int* walkers, hipStream_t s) {
   }
   c->class_off[kCatClasses] = (int)list.size();
   size_t qb = 0;
-  for (int cl = 0; cl < kCatClasses; ++cl) {
+  for (int cl = 0; cl < kCatClasses; ++cl) {  // sized by the class's launch geometry
+    int vpt, wpw;
+    catalog_class_geometry(cl, vpt, wpw);
     c->class_dq[cl] = qb;
-    qb += (hbk::wave_queue_bytes(kCatRcHi[cl], c->class_off[cl + 1] - c->class_off[cl]) + 255) & ~(size_t)255;
+    qb += (hbk::wave_queue_bytes(vpt, c->class_off[cl + 1] - c->class_off[cl], wpw) + 255) & ~(size_t)255;
   }
   if (qb > c->dq_bytes) {
     if (c->d_dq) (void)hipFree(c->d_dq);
@@ -741,27 +754,17 @@ static int catalog_layout(hb_catalog* c, const int* walkers, hipStream_t s) {
 
 // One catalog call: one records launch for every walker (hb_prep_kernel over
 // the catalog's walkers, per-target phase tables in its tail), then every
-// size class's eval launch on its stream (forked at the call's start).  The
-// evals evaluate the per-target phase-table entries in place.
-// HB_CAT_FUSED=2 (A/B knob): a records launch per class on the class's stream
-// (launch_prep_list), so one class's records overlap another's eval.
-// HB_CAT_FUSED=1 (A/B knob): each one-wave class of up to 16 cadences per lane
-// is ONE fused launch (its walkers' records in the eval kernel's prologue),
-// the other classes a records launch for their walkers (launch_prep_list) and
-// the eval -- measured slower: 0.204 vs 0.168 ms per C5 call
-// (profiles/r04/r04f_bench_c5*.json): a class's 1024-thread workgroups hold
-// their CU until the slowest of their 16 walkers (targets of different
-// lengths and eccentricities) is done, where one-wave workgroups backfill.
+// size class's eval launch on its stream (forked at the call's start).
+// (Measured and removed in round 5: a records launch per class on the class's
+// stream, 0.197 vs 0.162 ms per C5 call; each one-wave class as ONE launch with
+// its walkers' records in the eval kernel's prologue, 0.204 vs 0.168 ms:
+// profiles/r04/r04f_bench_c5*.json, r04m_c5_*.json.)
 static int catalog_run(hb_catalog* c, const double* d_params, double* d_logl, hipStream_t s) {
   if (c->total == 0) return 0;
-  static const int mode = cat_env("HB_CAT_FUSED", 0);  // 0 one records launch, 1 fused classes, 2 per class
-  const bool fused = mode == 1, per_class = mode != 0;
-  if (!per_class) {
-    MagArgs unused{};
-    HB_TRY(hbk::launch_prep(d_params, c->total, unused, c->d_wc, s, c->d_tab, c->d_wt, c->d_t, 0, c->d_ph, c->d_w0,
-                            c->ntargets),
-           "prep launch");
-  }
+  MagArgs unused{};
+  HB_TRY(hbk::launch_prep(d_params, c->total, unused, c->d_wc, s, c->d_tab, c->d_wt, c->d_t, 0, c->d_ph, c->d_w0,
+                          c->ntargets),
+         "prep launch");
   // classes by descending work, dealt round-robin over the caller's stream
   // and the forked ones
   int order[kCatClasses], nc = 0;
@@ -780,34 +783,13 @@ static int catalog_run(hb_catalog* c, const double* d_params, double* d_logl, hi
   for (int j = 0; j < nc; ++j) {
     const int cl = order[j];
     const int cnt = c->class_off[cl + 1] - c->class_off[cl];
-    int vpt = 1;
-    while (vpt < kCatRcHi[cl]) vpt <<= 1;
-    int wpw = 1;
-    if (cl == kCatClasses - 1) {  // a pair of waves of <= 16 cadences per lane
-      vpt = 16;
-      wpw = 2;
-    }
+    int vpt, wpw;
+    catalog_class_geometry(cl, vpt, wpw);
     hipStream_t sj = (j % ns == 0) ? s : c->aux[j % ns - 1];
     const int* lst = c->d_list + c->class_off[cl];
     double* dq = reinterpret_cast<double*>(reinterpret_cast<unsigned char*>(c->d_dq) + c->class_dq[cl]);
-    if (fused && wpw == 1 && vpt <= 16) {
-      hbk::PreArgs pa{};
-      pa.params = d_params;
-      pa.wc = c->d_wc;
-      pa.list = lst;
-      pa.wt = c->d_wt;
-      pa.tab = c->d_tab;
-      pa.w0 = c->d_w0;
-      HB_TRY(hbk::launch_eval_multi_fused(vpt, c->class_slab[cl], pa, c->d_t, c->d_f, c->d_s, c->d_rows, cnt, d_logl,
-                                          sj, dq),
-             "fused eval launch");
-      continue;
-    }
-    if (per_class)
-      HB_TRY(hbk::launch_prep_list(d_params, lst, cnt, c->d_wc, sj, c->d_tab, c->d_wt, c->d_w0), "records launch");
-    HB_TRY(hbk::launch_eval_multi(vpt, c->class_slab[cl], c->d_t, per_class ? nullptr : c->d_ph, c->d_f, c->d_s, c->d_rows,
-                                  c->d_tab, c->d_wt,
-                                  lst, cnt, c->d_wc, d_logl, sj, dq, wpw),
+    HB_TRY(hbk::launch_eval_multi(vpt, c->class_slab[cl], c->d_t, c->d_ph, c->d_f, c->d_s, c->d_rows, c->d_tab,
+                                  c->d_wt, lst, cnt, c->d_wc, d_logl, sj, dq, wpw),
            "eval launch");
   }
   for (int i = 0; i < ns - 1; ++i) {

@@ -268,7 +268,12 @@ struct StarCoef {
 // coefficient's R^k), star_coef_r multiplies the star's own radius in, and
 // star_coef_finish the companion's radius (reflection) and alpha_beam
 // (beaming).  Each coefficient's operations and their order are those of the
-// one-expression form (left to right: the R^k factor and ppm come last).
+// one-expression form (left to right: the R^k factor and ppm come last), except
+// the beaming coefficient kb: alpha_beam comes from another prep wave, so it
+// multiplies the product last instead of second (likelihood3.c:233 has
+// -2830 * alpha_beam * ...): an ulp-level difference, well inside the template
+// tolerance (the reference's per-cadence product, fac4 included, is hoisted
+// here anyway).
 struct StarCoefX {
   double kb, am1, am2, c21, a3, a22, a4, x5, b1, b3, x4, kref;
 };
@@ -347,21 +352,17 @@ __device__ __forceinline__ StarCoef star_coef(double pd, double ma, double mb, d
 // ------------------------------------------------------------------------
 // per-walker preparation
 // ------------------------------------------------------------------------
-// HB_SU2: the polynomial's harmonics in x = sin^2 u.  cos 2u = 1 - 2x,
+// The polynomial's harmonics in x = sin^2 u: cos 2u = 1 - 2x,
 // cos 4u = 1 - 8x + 8x^2, sin 3u = sin u (3 - 4x), so each beta-power's
 // coefficient is a polynomial in x (sin u) with the harmonic weights folded
 // into the record once per walker: 8 fp64 instructions per cadence instead of
-// 13.  The record's k* fields then hold the x-form (see su2_form).
-#ifndef HB_SU2
-#define HB_SU2 1
-#endif
-
+// 13.  The record's k* fields hold the x-form (su2_form).
+//
 // the cos-harmonic coefficients (kr0, kr2 | kam2, kc21 | ks1, ks3 | kam3,
 // kc22, kc4 of 1, cos 2u, sin u, sin 3u, cos 4u) rewritten as polynomials in
-// x = sin^2 u (HB_SU2; identity otherwise)
+// x = sin^2 u
 __host__ __device__ inline void su2_form(double& kr0, double& kr2, double& kam2, double& kc21, double& ks1, double& ks3,
                                          double& kam3, double& kc22, double& kc4) {
-#if HB_SU2
   kr0 = kr0 + kr2;  // kr0 + kr2 (1 - 2x)
   kr2 = -2.0 * kr2;
   kam2 = kam2 + kc21;  // kam2 + kc21 (1 - 2x)
@@ -371,9 +372,6 @@ __host__ __device__ inline void su2_form(double& kr0, double& kr2, double& kam2,
   kam3 = (kam3 + kc22) + kc4;  // kam3 + kc22 (1 - 2x) + kc4 (1 - 8x + 8x^2)
   kc22 = fma(-8.0, kc4, -2.0 * kc22);
   kc4 = 8.0 * kc4;
-#else
-  (void)kr0; (void)kr2; (void)kam2; (void)kc21; (void)ks1; (void)ks3; (void)kam3; (void)kc22; (void)kc4;
-#endif
 }
 
 __device__ inline void hb_prepare_walker(const double* __restrict__ p, const double* __restrict__ mag,
@@ -481,11 +479,8 @@ __device__ inline void hb_prepare_walker(const double* __restrict__ p, const dou
 // within 2 ulp of asin over [0, 1]).  Branch-free, because one eclipse flush
 // mixes lanes of both ranges; ~35 instructions against ~95 for ocml's asin,
 // whose two calls were a third of the eclipse flush.  x > 1 (hh rounded past
-// r) and NaN give NaN, like libm.  Not used with HB_OCML_ASIN (A/B builds).
+// r) and NaN give NaN, like libm.
 __device__ __forceinline__ double asin01(double x) {
-#ifdef HB_OCML_ASIN
-  return asin(x);
-#else
   const bool big = x >= 0.5;
   const double t = big ? (1.0 - x) * 0.5 : x * x;
   const double s = big ? sqrt_fast(t) : x;  // t exact (Sterbenz); a few ulp of s are within asin01's 2 ulp
@@ -504,7 +499,6 @@ __device__ __forceinline__ double asin01(double x) {
   p = __builtin_fma(p, t, 0.16666666666666669);
   const double r = __builtin_fma(s * t, p, s);
   return big ? (1.5707963267948966 - 2.0 * r) + 6.123233995736766e-17 : r;
-#endif
 }
 
 __device__ __forceinline__ double overlap_partial(double ra, double rb, double d, bool inner) {
@@ -586,21 +580,11 @@ __device__ __forceinline__ double hb_cadence_flux(double t, const WalkerConst& w
   const double b2 = b * b;
   const double b3 = b2 * b;
   double v = w.kconst + w.kb * cu;
-#if HB_SU2
   const double x = su * su;  // the record's harmonics in x = sin^2 u (su2_form)
   v += b2 * (w.kr0 + w.kr2 * x + w.krs * su);
   v += b3 * (w.kam2 + w.kc21 * x);
   v += (b2 * b2) * (su * (w.ks1 + w.ks3 * x));
   v += (b3 * b2) * (w.kam3 + x * (w.kc22 + w.kc4 * x));
-#else
-  const double c2 = (cu - su) * (cu + su);   // cos 2u
-  const double s3 = su * (3.0 - 4.0 * su * su);  // sin 3u
-  const double c4 = 2.0 * c2 * c2 - 1.0;     // cos 4u
-  v += b2 * (w.kr0 + w.kr2 * c2 + w.krs * su);
-  v += b3 * (w.kam2 + w.kc21 * c2);
-  v += (b2 * b2) * (w.ks1 * su + w.ks3 * s3);
-  v += (b3 * b2) * (w.kam3 + w.kc22 * c2 + w.kc4 * c4);
-#endif
   // eclipse: only lanes with overlap take the branch
   if (o.dR < w.rbig + w.rsml && o.zz != 0.0) {
     const double area = overlap_area(w.rbig, w.rsml, w.dcrit, o.dR);
@@ -640,12 +624,6 @@ __device__ __noinline__ double hb_cadence_flux_slow(double t, const WalkerConst*
 // The light-curve polynomial is written with explicit FMAs (the build uses
 // -ffp-contract=off so that the reference-order paths keep their rounding).
 // ------------------------------------------------------------------------
-// 1: compiler barriers split the walker constants' live ranges between the
-// Kepler solve and the photometric polynomial (SGPR spills 100 -> 52, no VGPR
-// spills; eval 55.4 -> 54.1 us at C2)
-#ifndef HB_SPLIT_LIVE
-#define HB_SPLIT_LIVE 1
-#endif
 constexpr double kRotMaxK = 0.25;
 __device__ __forceinline__ void rotate_back_wide(double d, double z, double& s, double& c) {
   // sin d = d (1 + z S(z)), cos d = 1 + z C(z), z = d^2
@@ -742,18 +720,11 @@ __device__ __forceinline__ void cold_start_k(const double (&t)[K], const double2
 // Newton on E - e sin E = M (likelihood3.c:152-160), at most 5 steps; the
 // wave leaves once every lane's predicted next correction is <= 2^-52.
 // yk: the last step's 1/(1 - e cos E).  Returns whether it converged.
-#ifdef HB_CHAIN_STATS  // experiment builds only: warm-start bookkeeping counters
-__device__ unsigned long long hb_chain_stats[8];
-#define HB_STAT(i) do { if ((threadIdx.x & 63) == 0) atomicAdd(&hb_chain_stats[i], 1ull); } while (0)
-#else
-#define HB_STAT(i) do { } while (0)
-#endif
 template <int K>
 __device__ __forceinline__ bool newton_k(double e, const double (&m)[K], double (&E)[K], double (&s)[K],
                                          double (&c)[K], double (&yk)[K], bool& ok) {
 #pragma unroll
   for (int it = 0; it < 5; ++it) {
-    HB_STAT(5);
     bool small = true, mid = true, tiny = true, conv = true;
     double d[K], z[K];
 #pragma unroll
@@ -782,7 +753,6 @@ __device__ __forceinline__ bool newton_k(double e, const double (&m)[K], double 
 #pragma unroll
       for (int k = 0; k < K; ++k) rotate_back_wide(d[k], z[k], s[k], c[k]);
     } else {
-      HB_STAT(7);
 #pragma unroll
       for (int k = 0; k < K; ++k) {
         ok &= sincos_fast_ok(E[k]);
@@ -795,24 +765,12 @@ __device__ __forceinline__ bool newton_k(double e, const double (&m)[K], double 
 }
 
 // The photometric polynomial of K cadences from (sin, cos) of the solved
-// eccentric anomaly, without the eclipse; dd = (projected separation / a)^2
-// and zz (sign carrier of Z1 - Z2) for the eclipse test.
-// HB_LEAN: the warm start's A and B with 0.5 e and e / 6 taken once per step
-// (two multiplies fewer per cadence), and the polynomial's cos 2u as
-// 1 - 2 sin^2 u (two fewer); 0: the round-3 expressions
-#ifndef HB_LEAN
-#define HB_LEAN 1
-#endif
-// HB_LEAN2 (split chain path): the chain carries its mean anomaly, so the warm
-// start's D needs no E - e sin E, and 0.5e, e/6 and 2^-51/e are taken once per
-// model pass (WarmK) -- two fp64 instructions fewer per cadence
-#ifndef HB_LEAN2
-#define HB_LEAN2 1
-#endif
-#ifndef HB_FLUX_V
-#define HB_FLUX_V 2  // 2: numerator form (beta = 1 / den); 1: through cos/sin nu
-#endif
-// inv[k] = 1 / (1 - e cos E) of the caller (flux_poly_k computes it)
+// eccentric anomaly and inv[k] = 1 / (1 - e cos E), without the eclipse;
+// dd = (projected separation / a)^2 and zz (sign carrier of Z1 - Z2) for the
+// eclipse test.  u = omega0 + nu from the numerators of cos/sin nu (den > 0):
+// cos u (1 - e cos E) = cw (cos E - e) - sw sqrt(1-e^2) sin E, likewise sin u;
+// beta = (1 + e cos nu) / (1 - e^2) = 1 / (1 - e cos E) identically, and the
+// squared projected separation / a^2 is CU^2 + cos^2 i SU^2 (no atan/tan).
 template <int K>
 __device__ __forceinline__ void flux_poly_inv_k(const double (&s)[K], const double (&c)[K], const double (&invk)[K],
                                                 const WalkerConst& w, double (&v)[K], double (&dd)[K],
@@ -821,13 +779,6 @@ __device__ __forceinline__ void flux_poly_inv_k(const double (&s)[K], const doub
 #pragma unroll
   for (int k = 0; k < K; ++k) {
     const double inv = invk[k];
-#if HB_FLUX_V != 2
-    const double den = fma(-e, c[k], 1.0);
-#endif
-#if HB_FLUX_V == 2
-    // u = omega0 + nu from the numerators of cos/sin nu (den > 0): beta =
-    // (1 + e cos nu) / (1 - e^2) = 1 / (1 - e cos E) identically, and the
-    // squared projected separation / a^2 is CU^2 + cos^2 i SU^2
     const double P = c[k] - e;
     const double CU = fma(w.cw, P, -(w.swq * s[k]));
     const double SU = fma(w.sw, P, w.cwq * s[k]);
@@ -836,39 +787,14 @@ __device__ __forceinline__ void flux_poly_inv_k(const double (&s)[K], const doub
     const double b = inv;
     dd[k] = fma(CU, CU, w.ci2 * (SU * SU));  // sqrt only on eclipse lanes
     zz[k] = SU * w.si;
-#else
-    const double cnu = (c[k] - e) * inv;
-    const double snu = (w.sq1me2 * s[k]) * inv;
-    const double cu = fma(w.cw, cnu, -w.sw * snu);
-    const double su = fma(w.sw, cnu, w.cw * snu);
-    const double b = fma(e, cnu, 1.0) * w.inv1me2;
-    const double sci = su * w.ci;
-    dd[k] = (den * den) * fma(cu, cu, sci * sci);  // sqrt only on eclipse lanes
-    zz[k] = su * w.si;
-#endif
     const double b2 = b * b;
-    // b^2 [A2 + b (A3 + b (A4 + b A5))] + kconst + kb cos u
-#if HB_SU2
-    const double x = su * su;  // the harmonics as polynomials in sin^2 u (su2_form)
+    // b^2 [A2 + b (A3 + b (A4 + b A5))] + kconst + kb cos u, the harmonics as
+    // polynomials in x = sin^2 u (su2_form)
+    const double x = su * su;
     const double a5 = fma(fma(w.kc4, x, w.kc22), x, w.kam3);
     const double a4 = su * fma(w.ks3, x, w.ks1);
     const double a3 = fma(w.kc21, x, w.kam2);
     const double a2 = fma(w.krs, su, fma(w.kr2, x, w.kr0));
-#else
-#if HB_LEAN
-    const double su2 = su * su;
-    const double c2 = fma(-2.0, su2, 1.0);  // cos 2u (cu^2 + su^2 = 1 to rounding)
-#else
-    const double c2 = (cu - su) * (cu + su);          // cos 2u
-    const double su2 = su * su;
-#endif
-    const double s3 = su * fma(-4.0, su2, 3.0);       // sin 3u
-    const double c4 = fma(2.0 * c2, c2, -1.0);        // cos 4u
-    const double a5 = fma(w.kc4, c4, fma(w.kc22, c2, w.kam3));
-    const double a4 = fma(w.ks3, s3, w.ks1 * su);
-    const double a3 = fma(w.kc21, c2, w.kam2);
-    const double a2 = fma(w.krs, su, fma(w.kr2, c2, w.kr0));
-#endif
     double h = fma(b, a5, a4);
     h = fma(b, h, a3);
     h = fma(b, h, a2);
@@ -908,6 +834,12 @@ __device__ __forceinline__ void flux_from_sc_k(const double (&s)[K], const doubl
   }
 }
 
+// The asm barriers below split the walker constants' live ranges between the
+// Kepler solve and the photometric polynomial: the constants are (re)loaded
+// with scalar loads after the solve instead of being held in SGPRs across it,
+// which would spill the solve's polynomial constants (SGPR spills 100 -> 52,
+// no VGPR spills; eval 55.4 -> 54.1 us at C2, round 1).
+
 // the polynomial part of K cadences, dd / zz for the caller's eclipse test
 template <int K>
 __device__ __forceinline__ void hb_cadence_poly_k(const double (&t)[K], const double2 (&ph)[K], bool tab,
@@ -918,9 +850,7 @@ __device__ __forceinline__ void hb_cadence_poly_k(const double (&t)[K], const do
   mean_anomaly_k<K>(t, w, m, plus, ok, exact);
   cold_start_k<K>(t, ph, tab, exact, w, m, plus, E, s, c, ok);
   (void)newton_k<K>(w.e, m, E, s, c, yk, ok);
-#if HB_SPLIT_LIVE
   __asm__ volatile("" ::: "memory");
-#endif
   flux_poly_k<K>(s, c, w, v, dd, zz);
   bad = !ok;
 }
@@ -933,316 +863,63 @@ __device__ __forceinline__ void hb_cadence_flux_k(const double (&t)[K], const do
   mean_anomaly_k<K>(t, w, m, plus, ok, exact);
   cold_start_k<K>(t, ph, tab, exact, w, m, plus, E, s, c, ok);
   (void)newton_k<K>(w.e, m, E, s, c, yk, ok);
-#if HB_SPLIT_LIVE
-  // compiler barrier: the photometric constants below are (re)loaded here
-  // with scalar loads instead of being held in SGPRs across the Kepler
-  // solve, which would spill the solve's polynomial constants
   __asm__ volatile("" ::: "memory");
-#endif
   flux_from_sc_k<K>(s, c, w, v);
   bad = !ok;
 }
 
 // ------------------------------------------------------------------------
-// Warm-started Kepler solve along a lane's consecutive cadences (the wave
+// Warm-started Kepler solve along a lane's consecutive cadences (the one-wave
 // kernel, where lane l owns cadences l*VPT .. l*VPT + VPT - 1 as K chains).
-// Consecutive cadences of a light curve are close in phase, so the solved
-// anomaly of the previous cadence of the chain, advanced by the first-order
-// step dE = dM / (1 - e cos E), starts Newton within ~(dM)^2 of the root:
-// two steps (the second at the tiny rotation) instead of the reference
-// start's three or four.  The root is the one the reference's five steps
-// reach whenever those converge -- which holds for every M when e <= 0.85
-// (scripts/kepler_warm.py) -- so the warm start is taken only for e <= 0.8,
-// only when every lane's start step |dE| <= 0.25 and no lane needs the exact
-// fmod, and a warm solve that does not converge in five steps is redone from
-// the reference's start (wave-uniform decisions throughout).
+// Consecutive cadences of a light curve are close in phase, so the previous
+// cadence's root starts the next solve within O(dM^4) (third-order series
+// reversion below): one Newton step instead of the reference start's three
+// or four.  The root is the one the reference's five steps reach whenever
+// those converge -- which holds for every M when e <= 0.85
+// (scripts/kepler_warm.py) -- so the warm start is taken only for e <= 0.8
+// (chain_eligible), and a lane outside the fast path continues with the
+// general Newton loop, failing that from the reference's start
+// (wave-uniform decisions throughout).
+//
+// A chain step comes in two halves, so the model pass can software-pipeline
+// the chains (model_pass_chain_pipe, hb_kernels.hip): step j's Kepler solve
+// and step j-1's photometric polynomial read the same chain state and are
+// independent, so both sit in one basic block and interleave (twice the
+// independent fp64 chains per lane: the drain, where one or two waves are left
+// on a SIMD, is latency-bound).
 // ------------------------------------------------------------------------
 constexpr double kWarmEmax = 0.8;
-// The chain carries the previous cadence's solved E and (sin, cos)(E); its
-// mean anomaly is E - e sin E (Kepler's equation, to rounding) and its
-// 1 / (1 - e cos E) a bare v_rcp_f64 -- the start only needs dE to ~1e-8.
-// HB_RCP_REUSE: the chain also carries 1 / (1 - e cos E) of its last cadence
-// (the polynomial's beta), which is the warm start's 1 / f'(E_p); and the
-// polynomial's reciprocal is seeded with the Newton step's 1 / f' (one ulp
-// class from the final one: two Newton refinements make it full precision)
-// instead of a fresh v_rcp_f64 -- two quarter-rate transcendentals fewer per
-// warm cadence.
-#ifndef HB_RCP_REUSE
-#define HB_RCP_REUSE 1
-#endif
+// The chain carries the previous cadence's solved E, (sin, cos)(E), its mean
+// anomaly m and 1 / (1 - e cos E) (the polynomial's beta, which is also the
+// warm start's 1 / f'(E_p)); the polynomial's reciprocal is seeded with the
+// Newton step's 1 / f' (one ulp class from the final one: two Newton
+// refinements make it full precision) instead of a fresh v_rcp_f64.
 template <int K>
 struct ChainState {
   double E[K], s[K], c[K];
-#if HB_RCP_REUSE
   double inv[K];
-#endif
-#if HB_LEAN2
-  double m[K];  // the mean anomaly E solved (split chain path): the next step's D = m' - m
-#endif
+  double m[K];  // the mean anomaly E solved: the next step's D = m' - m
 };
-// per-walker factors of the split warm step, taken once per model pass
+// per-walker factors of the warm step, taken once per model pass
 struct WarmK {
   double he, e6, ke;  // 0.5 e, e / 6, 2^-51 / e (the convergence test z <= ke den)
 };
 __device__ __forceinline__ WarmK warm_k(double e) { return WarmK{0.5 * e, e * (1.0 / 6.0), 0x1p-51 / e}; }
 
-// v: the polynomial part only; the caller applies the eclipse where
-// eclipse_lane(w, dd, zz) (compacted across the wave, see model_pass_chain)
-template <int K>
-__device__ __forceinline__ void hb_cadence_flux_chain(const double (&t)[K], const double2 (&ph)[K], bool tab,
-                                                      bool first, const WalkerConst& w, ChainState<K>& st,
-                                                      double (&v)[K], double (&dd)[K], double (&zz)[K],
-                                                      bool& bad) {
-  const double e = w.e;
-#if HB_LEAN
-  const double he = 0.5 * e, e6 = e * (1.0 / 6.0);  // the series start's A = he s / f', B = e6 c / f'
-#endif
-  double m[K], E[K], s[K], c[K], yk[K];
-  bool ok = true, exact = false, plus[K];
-#ifndef HB_WARM
-#define HB_WARM 1
-#endif
-#ifndef HB_WARM_V
-#define HB_WARM_V 2  // 2: third-order start + one Newton step; 1: first-order start + two steps
-#endif
-#if HB_WARM_V == 2
-  // The warm step only needs M up to a multiple of 2pi (D is reduced by
-  // rint below), so the exactness flags and sign(sin M) of the reference's
-  // start are computed only when a cold start is taken.
-  bool have_flags = false;
-  if (first) {
-    mean_anomaly_k<K>(t, w, m, plus, ok, exact);
-    have_flags = true;
-  } else {
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-      const double x = fma(t[k], kDay, w.mB) * w.mA;
-      ok &= sincos_fast_ok(x);
-      m[k] = fma(-trunc(x * 0.15915494309189533577), kTwoPi, x);
-    }
-  }
-  bool warm = HB_WARM && !first;
-#else
-  mean_anomaly_k<K>(t, w, m, plus, ok, exact);
-  // e <= kWarmEmax is the caller's walker-uniform gate (model_pass_chain)
-  bool warm = HB_WARM && !first && !wave_any(exact);
-#endif
-  HB_STAT(0);
-  if (warm) {
-    // the common warm step as one basic block (the K chains' solves and
-    // polynomials interleave): start rotation of degree 9 (|dE| <= 1/16),
-    // Newton step 1 with the mid rotation (|d| <= 2^-9), step 2 with the tiny
-    // one (|d| <= 2^-22) and the convergence test.  A lane outside those
-    // bounds recomputes (sin, cos) of its current E directly and the wave
-    // continues with the general Newton loop from there (no restart).
-    bool fine = true;
-#if HB_WARM_V == 2
-    // Third-order start: series reversion of Kepler's equation about the
-    // previous cadence's root, E0 = E_p + x - A x^2 + (2 A^2 - B) x^3 with
-    // x = dM / f1, A = f2 / (2 f1), B = f3 / (6 f1) at E_p (derivatives of
-    // E - e sin E: f1 = 1 - e cos, f2 = e sin, f3 = e cos), error O(x^4);
-    // then (sin, cos)(E0) by the degree-9 rotation and ONE Newton step.
-    // |d| <= 2^-22 with e d^2 <= 2^-51 (1 - e cos E) means the next correction
-    // is below 2^-52 (converged, like the two-step path below).
-#if HB_RCP_REUSE
-    double ys[K];  // the Newton step's 1 / f' (seeds the polynomial's reciprocal)
-#endif
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-      const double D = m[k] - fma(-e, st.s[k], st.E[k]);
-      const double q = rint(D * 0.15915494309189533577);
-      const double Dc = fma(-q, kTwoPi, D);
-#if HB_RCP_REUSE
-      const double r = st.inv[k];
-#else
-      const double g = fma(-e, st.c[k], 1.0);
-      double r = __builtin_amdgcn_rcp(g);
-      r = fma(fma(-g, r, 1.0), r, r);
-#endif
-      const double x = Dc * r;
-#if HB_LEAN
-      const double A = (he * st.s[k]) * r;
-      const double B = (e6 * st.c[k]) * r;
-#else
-      const double A = (e * st.s[k]) * (0.5 * r);
-      const double B = (e * st.c[k]) * (r * (1.0 / 6.0));
-#endif
-      const double C = fma(2.0 * A, A, -B);
-      const double dl = fma(x * x, fma(C, x, -A), x);
-      double E0 = fma(q, kTwoPi, st.E[k]) + dl;
-      double s0 = st.s[k], c0 = st.c[k];
-      const double z0 = dl * dl;
-      fine &= fabs(dl) <= 0.0625;
-      {  // rotate forward by dl: sin dl = dl (1 + z S(z)), cos dl = 1 + z C(z)
-        const double sd = fma(dl * z0, fma(z0, fma(z0, fma(z0, 1.0 / 362880.0, -1.0 / 5040.0), 1.0 / 120.0),
-                                           -1.0 / 6.0), dl);
-        const double cd = fma(z0, fma(z0, fma(z0, fma(z0, 1.0 / 40320.0, -1.0 / 720.0), 1.0 / 24.0), -0.5), 1.0);
-        const double s1 = fma(s0, cd, c0 * sd);
-        const double c1 = fma(c0, cd, -(s0 * sd));
-        s0 = s1;
-        c0 = c1;
-      }
-      const double den = fma(-e, c0, 1.0);
-      double y = __builtin_amdgcn_rcp(den);
-      y = fma(fma(-den, y, 1.0), y, y);
-      const double d = ((E0 - e * s0) - m[k]) * y;
-      E0 = E0 - d;
-      const double z = d * d;
-      fine &= (fabs(d) <= 0x1p-22) & (e * z <= 0x1p-51 * den);
-      rotate_back_tiny(d, z, s0, c0);
-      E[k] = E0;
-      s[k] = s0;
-      c[k] = c0;
-#if HB_RCP_REUSE
-      ys[k] = y;
-#endif
-    }
-#else
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-      const double D = m[k] - fma(-e, st.s[k], st.E[k]);
-      const double q = rint(D * 0.15915494309189533577);
-      const double Dc = fma(-q, kTwoPi, D);
-      const double dl = Dc * __builtin_amdgcn_rcp(fma(-e, st.c[k], 1.0));
-      double E0 = fma(q, kTwoPi, st.E[k]) + dl;
-      double s0 = st.s[k], c0 = st.c[k];
-      const double z0 = dl * dl;
-      fine &= fabs(dl) <= 0.0625;
-      {  // rotate forward by dl: sin dl = dl (1 + z S(z)), cos dl = 1 + z C(z)
-        const double sd = fma(dl * z0, fma(z0, fma(z0, fma(z0, 1.0 / 362880.0, -1.0 / 5040.0), 1.0 / 120.0),
-                                           -1.0 / 6.0), dl);
-        const double cd = fma(z0, fma(z0, fma(z0, fma(z0, 1.0 / 40320.0, -1.0 / 720.0), 1.0 / 24.0), -0.5), 1.0);
-        const double s1 = fma(s0, cd, c0 * sd);
-        const double c1 = fma(c0, cd, -(s0 * sd));
-        s0 = s1;
-        c0 = c1;
-      }
-      // Newton step 1
-      double den = fma(-e, c0, 1.0);
-      double y = __builtin_amdgcn_rcp(den);
-      y = fma(fma(-den, y, 1.0), y, y);
-      double d = ((E0 - e * s0) - m[k]) * y;
-      E0 = E0 - d;
-      fine &= fabs(d) <= 0x1p-9;
-      rotate_back_mid(d, d * d, s0, c0);
-      // Newton step 2
-      den = fma(-e, c0, 1.0);
-      y = __builtin_amdgcn_rcp(den);
-      y = fma(fma(-den, y, 1.0), y, y);
-      d = ((E0 - e * s0) - m[k]) * y;
-      E0 = E0 - d;
-      const double z = d * d;
-      fine &= (fabs(d) <= 0x1p-22) & (e * z <= 0x1p-51 * den);
-      rotate_back_tiny(d, z, s0, c0);
-      E[k] = E0;
-      s[k] = s0;
-      c[k] = c0;
-    }
-#endif
-    if (wave_all(fine)) {
-      HB_STAT(2);
-#if HB_RCP_REUSE
-      double inv[K];
-#pragma unroll
-      for (int k = 0; k < K; ++k) {  // 1 / (1 - e cos E) from the seed: |d| <= 2^-22 moved den by <= e 2^-22
-        const double den = fma(-e, c[k], 1.0);
-        double y = ys[k];
-        y = fma(fma(-den, y, 1.0), y, y);
-        inv[k] = fma(fma(-den, y, 1.0), y, y);
-        st.inv[k] = inv[k];
-      }
-#endif
-#pragma unroll
-      for (int k = 0; k < K; ++k) {
-        st.E[k] = E[k];
-        st.s[k] = s[k];
-        st.c[k] = c[k];
-      }
-#if HB_SPLIT_LIVE
-      __asm__ volatile("" ::: "memory");
-#endif
-#if HB_RCP_REUSE
-      flux_poly_inv_k<K>(s, c, inv, w, v, dd, zz);
-#else
-      flux_poly_k<K>(s, c, w, v, dd, zz);
-#endif
-      bad = !ok;
-      return;
-    }
-    HB_STAT(1);
-    if (!fine) {  // (sin, cos) of the lane's current iterate, then Newton to convergence
-#pragma unroll
-      for (int k = 0; k < K; ++k) {
-        ok &= sincos_fast_ok(E[k]);
-        sincos_fast(E[k], &s[k], &c[k]);
-      }
-    }
-    warm = newton_k<K>(e, m, E, s, c, yk, ok);  // else: redo from the reference's start
-    if (warm) HB_STAT(3);
-  }
-  if (!warm) {
-    HB_STAT(4);
-#if HB_WARM_V == 2
-    if (!have_flags) {  // rare: the warm chain did not converge
-      ok = true;
-      mean_anomaly_k<K>(t, w, m, plus, ok, exact);
-    }
-#endif
-    cold_start_k<K>(t, ph, tab, exact, w, m, plus, E, s, c, ok);
-    (void)newton_k<K>(e, m, E, s, c, yk, ok);
-  }
-#pragma unroll
-  for (int k = 0; k < K; ++k) {
-    st.E[k] = E[k];
-    st.s[k] = s[k];
-    st.c[k] = c[k];
-  }
-#if HB_RCP_REUSE
-  double inv[K];
-#pragma unroll
-  for (int k = 0; k < K; ++k) {
-    inv[k] = fast_rcp(fma(-e, c[k], 1.0));
-    st.inv[k] = inv[k];
-  }
-#endif
-#if HB_SPLIT_LIVE
-  __asm__ volatile("" ::: "memory");
-#endif
-#if HB_RCP_REUSE
-  flux_poly_inv_k<K>(s, c, inv, w, v, dd, zz);
-#else
-  flux_poly_k<K>(s, c, w, v, dd, zz);
-#endif
-  bad = !ok;
-}
-
-// ------------------------------------------------------------------------
-// The same chain step in two halves, so the model pass can software-pipeline
-// the chains (model_pass_chain_pipe, hb_kernels.hip): step j's Kepler solve
-// and step j-1's photometric polynomial read the same chain state and are
-// independent, so both sit in one basic block and interleave (twice the
-// independent fp64 chains per lane: the drain, where one or two waves are
-// left on a SIMD, is latency-bound).  Same operations in the same order as
-// hb_cadence_flux_chain (HB_WARM_V == 2, HB_RCP_REUSE): bit-identical values.
-// ------------------------------------------------------------------------
-#if HB_WARM_V == 2 && HB_RCP_REUSE && HB_WARM
-#define HB_CHAIN_SPLIT 1
-// warm half: the mean anomaly up to a multiple of 2pi (no exactness flags),
-// the third-order start from the chain state, the degree-9 rotation and one
-// Newton step; fine: the lane's step converged (see hb_cadence_flux_chain)
+// Warm half: the mean anomaly up to a multiple of 2pi (no exactness flags:
+// D is reduced by rint), the third-order start -- series reversion of Kepler's
+// equation about the previous root, E0 = E_p + x - A x^2 + (2 A^2 - B) x^3
+// with x = dM / f1, A = f2 / (2 f1), B = f3 / (6 f1) at E_p (f1 = 1 - e cos,
+// f2 = e sin, f3 = e cos), error O(x^4) -- then (sin, cos)(E0) by a degree-9
+// rotation of the previous (sin, cos) and ONE Newton step.  fine: the lane's
+// step is |d| <= 2^-22 with e d^2 <= 2^-51 (1 - e cos E), i.e. its next
+// correction would be below 2^-52 (converged to rounding).
 template <int K>
 __device__ __forceinline__ void chain_kepler_warm(const double (&t)[K], const WalkerConst& w, const ChainState<K>& st,
                                                   double (&m)[K], double (&E)[K], double (&s)[K], double (&c)[K],
                                                   double (&ys)[K], bool& fine, bool& ok, const WarmK& wk) {
   const double e = w.e;
-#if HB_LEAN2
   const double he = wk.he, e6 = wk.e6;
-#elif HB_LEAN
-  const double he = 0.5 * e, e6 = e * (1.0 / 6.0);
-  (void)wk;
-#else
-  (void)wk;
-#endif
   fine = true;
 #pragma unroll
   for (int k = 0; k < K; ++k) {
@@ -1252,29 +929,20 @@ __device__ __forceinline__ void chain_kepler_warm(const double (&t)[K], const Wa
   }
 #pragma unroll
   for (int k = 0; k < K; ++k) {
-#if HB_LEAN2
     const double D = m[k] - st.m[k];
-#else
-    const double D = m[k] - fma(-e, st.s[k], st.E[k]);
-#endif
     const double q = rint(D * 0.15915494309189533577);
     const double Dc = fma(-q, kTwoPi, D);
     const double r = st.inv[k];
     const double x = Dc * r;
-#if HB_LEAN
     const double A = (he * st.s[k]) * r;
     const double B = (e6 * st.c[k]) * r;
-#else
-    const double A = (e * st.s[k]) * (0.5 * r);
-    const double B = (e * st.c[k]) * (r * (1.0 / 6.0));
-#endif
     const double C = fma(2.0 * A, A, -B);
     const double dl = fma(x * x, fma(C, x, -A), x);
     double E0 = fma(q, kTwoPi, st.E[k]) + dl;
     double s0 = st.s[k], c0 = st.c[k];
     const double z0 = dl * dl;
     fine &= fabs(dl) <= 0.0625;
-    {
+    {  // rotate forward by dl: sin dl = dl (1 + z S(z)), cos dl = 1 + z C(z)
       const double sd = fma(dl * z0, fma(z0, fma(z0, fma(z0, 1.0 / 362880.0, -1.0 / 5040.0), 1.0 / 120.0),
                                          -1.0 / 6.0), dl);
       const double cd = fma(z0, fma(z0, fma(z0, fma(z0, 1.0 / 40320.0, -1.0 / 720.0), 1.0 / 24.0), -0.5), 1.0);
@@ -1289,11 +957,7 @@ __device__ __forceinline__ void chain_kepler_warm(const double (&t)[K], const Wa
     const double d = ((E0 - e * s0) - m[k]) * y;
     E0 = E0 - d;
     const double z = d * d;
-#if HB_LEAN2
     fine &= (fabs(d) <= 0x1p-22) & (z <= wk.ke * den);
-#else
-    fine &= (fabs(d) <= 0x1p-22) & (e * z <= 0x1p-51 * den);
-#endif
     rotate_back_tiny(d, z, s0, c0);
     E[k] = E0;
     s[k] = s0;
@@ -1321,9 +985,7 @@ __device__ __forceinline__ void chain_finish_warm(const double (&t)[K], const Wa
       st.E[k] = E[k];
       st.s[k] = s[k];
       st.c[k] = c[k];
-#if HB_LEAN2
       st.m[k] = m[k];
-#endif
     }
     return;
   }
@@ -1349,9 +1011,7 @@ __device__ __forceinline__ void chain_finish_warm(const double (&t)[K], const Wa
     st.s[k] = s[k];
     st.c[k] = c[k];
     st.inv[k] = fast_rcp(fma(-e, c[k], 1.0));
-#if HB_LEAN2
     st.m[k] = m[k];
-#endif
   }
 }
 // a chain's first cadence: the reference's start (table entries) and Newton
@@ -1370,14 +1030,8 @@ __device__ __forceinline__ void chain_first(const double (&t)[K], const double2 
     st.s[k] = s[k];
     st.c[k] = c[k];
     st.inv[k] = fast_rcp(fma(-e, c[k], 1.0));
-#if HB_LEAN2
     st.m[k] = m[k];
-#endif
   }
 }
-#else
-#define HB_CHAIN_SPLIT 0
-#endif
-
 
 }  // namespace hbdev

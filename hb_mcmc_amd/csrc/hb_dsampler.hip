@@ -61,7 +61,6 @@ extern "C" int hbx_ctx_prep_args(hb_ctx* c, void** wc, void* mags, double** tab_
 extern "C" int hbx_loglik_accept_dev(hb_ctx* c, const double* d_params, int w, double* d_logl, const void* acc,
                                      void* stream);
 extern "C" long hbx_ctx_wave_lds(const hb_ctx* c);
-extern "C" int hbx_swap_tail_compiled(void);
 
 namespace hbds {
 
@@ -939,13 +938,7 @@ struct hb_dsampler {
   int nthreads = 0;
   int nseg = 1;  // swap segments (ds_swap_seg workgroups) over the owned slots
   bool fused_prep = true;  // walker records in ds_propose's epilogue (else an hb_prep_kernel launch)
-  // tempering swaps at the tail of the likelihood launch (hb_accept.hpp
-  // swap_tail_wave) instead of a ds_swap_seg launch: one-process samplers
-  // whose eval waves' LDS holds a segment (checked per iteration)
-  bool tail_ok = false;
-  bool tail_now = false;  // this iteration's swaps ran in the likelihood launch
-  int* d_tcnt = nullptr;     // [nseg + 2] the tail's counters (zero between launches)
-  double* d_lslot = nullptr; // [W + 1] logL by slot after the Hastings test (one-process samplers)
+  double* d_lslot = nullptr; // [W] logL by slot after the Hastings test (one-process samplers)
   bool lslot_now = false;    // this iteration's fused Hastings test wrote d_lslot
   // host timers [s]: producer work (all threads), waits for a schedule, issue
   double t_prod = 0.0, t_wait = 0.0, t_issue = 0.0;
@@ -1277,16 +1270,8 @@ static hb_dsampler* ds_create(hb_sampler* s, hb_ctx* ctx, const int* chain_of_sl
   // most min(G, 3 + 2 kMaxLevels / (smallest segment)) segments
   d->nseg = std::max(1, (d->nl + kSegSlots - 1) / kSegSlots);
   {
-    // the tail counts a slot in the cones of at most 64 segments (one per lane)
-    // experiment (measured slower): HB_DS_TAIL=1 with a library built with -DHB_SWAP_TAIL=1
-    const char* tl = getenv("HB_DS_TAIL");
     const bool one = !d->xchg && d->lo == 0 && d->nl == W;
-    d->tail_ok = one && d->nl / d->nseg >= 8 && tl && atoi(tl) != 0 && hbx_swap_tail_compiled();
-    if (one && (e = d->alloc(&d->d_lslot, Wz + 1))) return fail("hipMalloc", e);
-    if (d->tail_ok) {
-      if ((e = d->alloc(&d->d_tcnt, (size_t)d->nseg + 2))) return fail("hipMalloc", e);
-      if ((e = hipMemsetAsync(d->d_tcnt, 0, sizeof(int) * ((size_t)d->nseg + 2), d->st))) return fail("hipMemset", e);
-    }
+    if (one && (e = d->alloc(&d->d_lslot, Wz))) return fail("hipMalloc", e);
   }
   {
     const size_t G = (size_t)d->nseg, segmin = std::max<size_t>(1, (size_t)d->nl / G);
@@ -1624,30 +1609,8 @@ static long ds_begin(hb_dsampler* d, long iter, double* send, long cap) {
   // (hb_accept.hpp); ds_accept only where the plan has no one-wave kernel
   AccArgs acc{D.idx, D.logL, D.logP, D.logPy, D.temp, D.alpha2, D.jump, D.jtype, D.x, D.y, D.hist,
               D.DEacc_arr, D.ctr, D.ev, d->P.log_on, NPAST, (long long)iter, d->lo, 0,
-              D.ecnt, D.elist, nl, 0};
-  d->tail_now = false;
-  acc.Lslot = d->d_lslot;  // null for exchanging samplers
-  if (d->tail_ok) {  // the swaps at the launch's tail when a wave's LDS holds the largest segment
-    const int G = d->nseg;
-    const size_t wc_max = (size_t)(nl + G - 1) / G + 2 * (size_t)sl.nlv;
-    if ((long)tail_lds_bytes((size_t)sl.maxent, wc_max) <= hbx_ctx_wave_lds(d->ctx)) {
-      const unsigned char* base = d->d_sched[slot];
-      acc.tcnt = d->d_tcnt;
-      acc.soff = reinterpret_cast<const int*>(base);
-      acc.ent = reinterpret_cast<const SwapEnt*>(base + sched_ent_off((size_t)G, (size_t)sl.nlv));
-      acc.betas = reinterpret_cast<const double*>(base + sched_beta_off((size_t)G, (size_t)sl.nlv, (size_t)sl.nent));
-      acc.hs = D.hs;
-      acc.idx_out = D.idx_out;
-      acc.DEtrial_arr = D.DEtrial_arr;
-      acc.ecnt_w = D.ecnt;
-      acc.W = W;
-      acc.nlv = sl.nlv;
-      acc.G = G;
-      acc.nl = nl;
-    }
-  }
+              D.ecnt, D.elist, nl, 0, d->d_lslot};  // Lslot: null for exchanging samplers
   int rc = hbx_loglik_accept_dev(d->ctx, D.y, nl, D.logLy, &acc, (void*)s);
-  if (rc == 0 && acc.tcnt != nullptr) d->tail_now = true;
   d->lslot_now = rc == 0 && acc.Lslot != nullptr;
   if (rc == 1) {
     rc = hb_evaluate_dev(d->ctx, nl, D.logLy, 0, (void*)s);
@@ -1683,11 +1646,13 @@ static int ds_end(hb_dsampler* d, long iter, const double* recv, long n) {
   hipStream_t s = d->st;
   if (const int rc = ds_check_failed(d, "hb_dsampler_step_end")) return rc;
   if (d->cur_iter != iter) return hbx_set_error("hb_dsampler_step_end: no step_begin for this iteration");
+  // a caller mistake is recoverable (step_end may be called again with the
+  // right buffer): checked before the guard is armed
+  if (d->xchg && (!recv || n != d->cur_n))
+    return hbx_set_error("hb_dsampler_step_end: gathered buffer missing or of the wrong size");
   // the iteration's proposals and likelihood are enqueued: failing from here
   // on is sticky, like the second half of ds_begin
   DsFailGuard guard{d};
-  if (d->xchg && (!recv || n != d->cur_n))
-    return hbx_set_error("hb_dsampler_step_end: gathered buffer missing or of the wrong size");
   const double t0 = now_s();
   const int slot = d->cur_slot;
   const hb_dsampler::Slot sl = d->slots[slot];  // written by its producer before the ready flag
@@ -1703,9 +1668,7 @@ static int ds_end(hb_dsampler* d, long iter, const double* recv, long n) {
   // segment's attempts
   const size_t wc_max = (size_t)(d->nl + G - 1) / G + 2 * (size_t)sl.nlv;
   const size_t lds = sizeof(SwapEnt) * (size_t)sl.maxent + (2 * sizeof(double) + sizeof(int)) * wc_max;
-  if (d->tail_now) {
-    // the likelihood launch's waves ran the swaps and the bookkeeping
-  } else if (d->xchg) {
+  if (d->xchg) {
     const Gathered X{recv, (long long)n, d->R, d->rank, d->m, 0};
     ds_swap_seg<true><<<G, kSegThreads, lds, s>>>(D, W, d_soff, d_ent, d_beta, sl.nlv, G, (long long)iter, X, nullptr);
     DS_TRY(hipGetLastError(), "ds_swap_seg");

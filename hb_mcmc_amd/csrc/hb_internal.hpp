@@ -91,17 +91,10 @@ hipError_t preload_code_object();
 // DAY 2pi/P) for P = the period of the light curve's first walker (walker 0,
 // or catalog target k's w0[k]), written here and read by the eval launch;
 // walkers with another period get tab = 0
-// ord (optional, nwalk <= hbds::kEvalOrdMax): one more workgroup writes the
-// walkers by descending e (eccentricity) for the eval launch's waves, from the
-// bins ebin[w] = hbds::e_bin_desc(params[w][3]) the caller wrote
 hipError_t launch_prep(const double* d_params, int nwalk, const MagArgs& ma, hbdev::WalkerConst* d_wc,
                        hipStream_t s, const TargetDesc* tab = nullptr, const int* wt = nullptr,
                        const double* t = nullptr, long n = 0, double2* ph = nullptr, const int* w0 = nullptr,
                        int ntargets = 0, double* tab_pc = nullptr);
-// catalog mode: records of the walkers list[0..count) (one size class; the
-// per-target tables are not written: the catalog's evals evaluate them in place)
-hipError_t launch_prep_list(const double* d_params, const int* list, int count, hbdev::WalkerConst* d_wc,
-                            hipStream_t s, const TargetDesc* tab, const int* wt, const int* w0);
 // catalog mode: walkers list[0..count) of one size class (cadences per lane
 // vpt), each reading its target's slice through tab[wt[walker]]
 // (wpw = 2: a pair of waves per walker, vpt the cadences per lane of 128 rows)
@@ -119,27 +112,14 @@ struct PreArgs {
   hbdev::WalkerConst* wc;   // records out (then read back by the eval waves)
   double2* ph;              // the global phase table (each workgroup writes a slice)
   double* tab_pc;           // its period [s]
-  // catalog mode (launch_eval_multi_fused): the walkers of the launch are
-  // list[0..count), each of target wt[walker] (magnitudes in tab[]); a walker
-  // uses the phase table of its target's first walker w0[target] (evaluated
-  // in place, hbk vt_entry; ph / tab_pc unused)
-  const int* list;
-  const int* wt;
-  const TargetDesc* tab;
-  const int* w0;
 };
 // walkers per workgroup of the fused launch for w walkers on `cus` CUs (0: the
 // two-launch path: prep + eval)
 int fused_wpb(const EvalPlan& pl, int w, int cus);
 hipError_t launch_eval_fused(const EvalPlan& pl, int wpb, const PreArgs& pa, const double* t, const double* f,
                              const double* sg, const double* rows, int nwalk, double* logl, hipStream_t s, double* dq);
-// catalog mode, one size class of one-wave walkers (cadences per lane vpt <=
-// 16), records in the prologue: pa.list / wt / tab / w0 set, count walkers
-hipError_t launch_eval_multi_fused(int vpt, size_t slab, const PreArgs& pa, const double* t, const double* f,
-                                   const double* sg, const double* rows, int count, double* logl, hipStream_t s,
-                                   double* dq);
 int wave_vpt_for(long n);  // cadences per lane of the one-wave path, 0 if n > 2048
-int wave_nr_for(long n);   // lane rows per walker: 64, or 128 (a pair of waves) for 1024 < n <= 2048
+int wave_nr_for(long n);   // lane rows per walker: 64, 128 (a pair of waves, 1280 < n <= 2048), 256 (four, <= 4096), 0 above
 // device bytes of the one-wave kernel's deferred cadence queue for `count`
 // walkers at `vpt` cadences per lane (the dq argument of launch_eval*)
 size_t wave_queue_bytes(int vpt, long count, int wpw = 1);

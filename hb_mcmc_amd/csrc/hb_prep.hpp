@@ -116,8 +116,6 @@ __device__ __forceinline__ void prep_coefficients(double* rec, WalkerConst* wc, 
 // [s] of the phase table walker j may use (NaN: no table).  slack(): wave 2's
 // spare work (phase 2).  Waves past the four roles (a workgroup of more than
 // 256 threads: the fused eval kernel) run idle() before the first barrier.
-// mg (optional, [3][NW]): per-walker (distance, G, sigma_G) gathered by the
-// caller, in place of tab / wt.
 //
 // Phase 1 (before the first barrier) holds every chain that needs no other
 // wave's result, split so that no wave carries much more issue than another:
@@ -135,8 +133,7 @@ __device__ __forceinline__ void prep_coefficients(double* rec, WalkerConst* wc, 
 template <int NW, class TabPc, class Slack, class Idle = PrepNoIdle>
 __device__ __forceinline__ void prep_records(PrepShared<NW>& L, int nb, const MagArgs& ma,
                                              const TargetDesc* __restrict__ tab, const int* __restrict__ wt,
-                                             int base, TabPc tab_pc, Slack slack, Idle idle = Idle(),
-                                             const double* mg = nullptr) {
+                                             int base, TabPc tab_pc, Slack slack, Idle idle = Idle()) {
   static_assert(NW >= 1 && NW <= 64, "one walker per lane");
   constexpr int kPass = (2 * NW + 63) / 64;
   // one pass (NW <= 32): both stars' terms meet by lane shuffles in phase 2
@@ -375,11 +372,6 @@ __device__ __forceinline__ void prep_records(PrepShared<NW>& L, int nb, const Ma
       dist = td.dist;
       gobs = td.gmag;
       gerr = td.gerr;
-    }
-    if (mg != nullptr && live) {  // catalog mode, gathered by the caller
-      dist = mg[j];
-      gobs = mg[NW + j];
-      gerr = mg[2 * NW + j];
     }
     const double r1 = L.xs[0][1][jc], r2 = L.xs[1][1][jc];
     const double g = ab_mag(band_flux_terms(r1 * kRsun, r2 * kRsun, L.xs[0][0][jc], L.xs[1][0][jc], dist,

@@ -17,7 +17,7 @@ HDR = os.path.join(os.path.dirname(__file__), "..", "hb_mcmc_amd", "csrc", "hb_d
 def _coefs():
     src = open(HDR).read()
     body = src[src.index("double asin01(double x)"):]
-    body = body[:body.index("#endif")]
+    body = body[:body.index("\n}\n")]
     first = re.search(r"double p = ([-0-9.e]+);", body).group(1)
     rest = re.findall(r"p = __builtin_fma\(p, t, ([-0-9.e]+)\);", body)
     return [float(first)] + [float(c) for c in rest]
