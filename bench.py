@@ -80,6 +80,8 @@ def parse():
                     help="steps of the kernel-timing pass after the timed region: HIP events around every "
                          "step's prep and eval launches (an event pair costs ~5 us of stream time, so the "
                          "timed steps carry none)")
+    ap.add_argument("--prior-steps", type=int, default=100,
+                    help="C2 shape on prior-spread walkers (c2_prior_spread key; 0: skip)")
     ap.add_argument("--sampler-iters", type=int, default=100,
                     help="also time the whole PT-MCMC iteration (mcmc_wrapper2.c loop) at the workload's W and N: "
                          "device-resident sampler vs the host sampler + GPU likelihood (0 = skip)")
@@ -299,6 +301,45 @@ def sampler_e2e_sharded(L, w, iters, rank, world, warm=20):
                                     "exchange_bytes_per_rank_per_iter": 8.0 * exch / (warm + iters)}}
 
 
+def prior_spread(L, n, w, steps, stream, dev, timer, ks=50):
+    """The headline shape (one hb_loglik_batch_dev of w walkers over n
+    cadences per step) on walkers drawn from the set_limits box like the
+    reference's random initial state (mcmc_wrapper2.c:236-252, synth.
+    prior_walkers): the spread of e, masses and Roche overflow the sampler's
+    hot rungs keep proposing, where the headline walkers sit near the truth
+    (every one on the warm Kepler chains).  Reported beside the headline, not
+    as `value`."""
+    nb = 4
+    Ph = [synth.prior_walkers(w, seed=3000 + k) for k in range(nb)]
+    P = [torch.from_numpy(x).to(dev) for x in Ph]
+    out = torch.empty(w, dtype=torch.float64, device=dev)
+    for k in range(10):
+        L.loglike_dev(P[k % nb], out, stream)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(steps):
+        L.loglike_dev(P[k % nb], out, stream)
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    evs = [[make_event(timer) for _ in range(2)] for _ in range(ks)]
+    for k in range(ks):
+        evs[k][0].record(stream)
+        L.loglike_dev(P[k % nb], out, stream)
+        evs[k][1].record(stream)
+    torch.cuda.synchronize()
+    kms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
+    lv = out.cpu().numpy()
+    x = Ph[(ks - 1) % nb]
+    roche = lv == -5e14
+    return {"walkers": w, "ncad": n, "steps": steps, "value": w * steps / wall, "unit": "evals/s",
+            "ms_per_step": wall / steps * 1e3, "kernel_ms": kms, "kernel_event_samples": ks,
+            "last_batch": {"roche_frac": float(roche.mean()),
+                           "e_gt_0p8_not_roche_frac": float(((x[:, 3] > 0.8) & ~roche).mean()),
+                           "nonfinite": int((~np.isfinite(lv)).sum())},
+            "walkers_from": "synth.prior_walkers: uniform over the set_limits box (mcmc_wrapper2.c:236-252), "
+                            "log P fixed, T0 folded"}
+
+
 def dropin_rate(niter):
     """The literal north_star drop-in: the reference's OWN sampler
     (src/mcmc_wrapper2.c, unmodified, 25 OpenMP threads) relinked against
@@ -361,6 +402,15 @@ def counters_for(config):
     return bid, c
 
 
+def shader_clock_for(config):
+    """The in-kernel shader clock measured on this workload (profiles/
+    shader_clock.json, written from scripts/wave_clocks.py's median), or None."""
+    try:
+        return json.load(open(os.path.join(ROOT, "profiles", "shader_clock.json"))).get(config)
+    except (OSError, ValueError):
+        return None
+
+
 def roofline(config, kernel_ms, evals_per_call, hbm_bytes_per_call, extra):
     """The dominant kernel's roofline.  Bound: the fp64 VALU (the path is
     elementwise fp64 transcendental work + a select).  t/f/sigma
@@ -386,6 +436,11 @@ def roofline(config, kernel_ms, evals_per_call, hbm_bytes_per_call, extra):
                "fp64_flop_per_eval_counted": c["fp64_flop_per_call"] / evals_per_call}
         if "valu_issue_cycles_per_call" in c:
             out["valu_issue_frac"] = c["valu_issue_cycles_per_call"] / (SIMDS * CLOCK_HZ * sec)
+            clk = shader_clock_for(config)
+            if clk:  # priced at the clock the chip held on this workload, not the 2.4 GHz peak
+                out["shader_clock_ghz"] = clk["ghz"]
+                out["shader_clock_source"] = clk.get("source")
+                out["valu_issue_frac_at_clock"] = c["valu_issue_cycles_per_call"] / (SIMDS * clk["ghz"] * 1e9 * sec)
         out["hbm"] = hbm
         out["counters"] = {"build": bid, "source": c.get("source")}
     else:
@@ -657,6 +712,8 @@ def main():
             "kernel_only_evals_per_s": w / ((eval_ms + prep_ms) * 1e-3),
             "nonfinite_logl_last_batch": nonfinite,
         }
+        if world == 1 and a.prior_steps > 0 and n <= 2048:
+            line["c2_prior_spread"] = prior_spread(L, n, w, a.prior_steps, stream, dev, a.timer)
         if world == 1 and a.sampler_iters > 0:
             line["sampler_end_to_end"] = sampler_e2e(L, w, a.sampler_iters)
         if world > 1 and e2e is not None:

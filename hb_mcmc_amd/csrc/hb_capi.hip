@@ -391,6 +391,28 @@ extern "C" long hbx_ctx_wave_lds(const hb_ctx* c) {
   return (long)hbk::wave_lds_bytes(c->plan.slab_bytes, c->plan.vpt, c->plan.wpw);
 }
 
+// internal (device sampler): the one-wave likelihood's inputs (hbk::
+// WaveEvalArgs; valid until the next hb_reserve that grows the workspace)
+extern "C" int hbx_ctx_wave_eval_args(hb_ctx* c, void* out) {
+  if (!c || !out) return set_err_msg("null argument");
+  hbk::WaveEvalArgs e{};
+  e.t = c->d_t;
+  e.ph = c->d_ph;
+  e.f = c->d_f;
+  e.isg = c->d_s;
+  e.rows = c->d_rows;
+  e.n = c->plan.n;
+  e.kth = c->plan.kth;
+  e.gap = c->plan.gap;
+  e.dq = c->d_dq;
+  e.vpt = c->plan.vpt;
+  e.wpw = c->plan.wpw;
+  e.slab_bytes = (int)c->plan.slab_bytes;
+  e.lds_per = c->plan.vpt > 0 ? (int)hbk::wave_lds_bytes(c->plan.slab_bytes, c->plan.vpt, c->plan.wpw) : 0;
+  memcpy(out, &e, sizeof e);
+  return 0;
+}
+
 // internal (device sampler): where its propose epilogue writes the walker
 // records (valid until the next hb_reserve that grows the workspace), the
 // magnitude data of the Gaia term, and the device word holding the period of
@@ -765,8 +787,10 @@ static int catalog_run(hb_catalog* c, const double* d_params, double* d_logl, hi
   HB_TRY(hbk::launch_prep(d_params, c->total, unused, c->d_wc, s, c->d_tab, c->d_wt, c->d_t, 0, c->d_ph, c->d_w0,
                           c->ntargets),
          "prep launch");
-  // classes by descending work, dealt round-robin over the caller's stream
-  // and the forked ones
+  // classes by descending work, each to the stream with the least work so
+  // far (longest-processing-time first; C5: the pair class alone is 43% of
+  // the cadence work, so round-robin left one stream with 110k of the 170k
+  // walker-cadences); HB_CAT_DEAL=0 (A/B knob): round-robin
   int order[kCatClasses], nc = 0;
   for (int cl = 0; cl < kCatClasses; ++cl)
     if (c->class_off[cl + 1] > c->class_off[cl]) order[nc++] = cl;
@@ -775,17 +799,26 @@ static int catalog_run(hb_catalog* c, const double* d_params, double* d_logl, hi
   // (profiles/r04/r04c_bench_c5_s*.json, two-launch path: the forked streams'
   // event waits cost more than the extra overlap buys)
   static const int kns = std::max(1, std::min(kCatStreams, cat_env("HB_CAT_STREAMS", kCatDefaultStreams)));
+  static const bool lpt = cat_env("HB_CAT_DEAL", 1) != 0;
   const int ns = nc < kns ? nc : kns;
   if (ns > 1) {
     HB_TRY(hipEventRecord(c->ev_fork, s), "fork event");
     for (int i = 0; i < ns - 1; ++i) HB_TRY(hipStreamWaitEvent(c->aux[i], c->ev_fork, 0), "fork wait");
   }
+  long load[kCatStreams] = {0};
   for (int j = 0; j < nc; ++j) {
     const int cl = order[j];
     const int cnt = c->class_off[cl + 1] - c->class_off[cl];
     int vpt, wpw;
     catalog_class_geometry(cl, vpt, wpw);
-    hipStream_t sj = (j % ns == 0) ? s : c->aux[j % ns - 1];
+    int si = j % ns;
+    if (lpt) {
+      si = 0;
+      for (int i = 1; i < ns; ++i)
+        if (load[i] < load[si]) si = i;
+    }
+    load[si] += c->class_work[cl];
+    hipStream_t sj = si == 0 ? s : c->aux[si - 1];
     const int* lst = c->d_list + c->class_off[cl];
     double* dq = reinterpret_cast<double*>(reinterpret_cast<unsigned char*>(c->d_dq) + c->class_dq[cl]);
     HB_TRY(hbk::launch_eval_multi(vpt, c->class_slab[cl], c->d_t, c->d_ph, c->d_f, c->d_s, c->d_rows, c->d_tab,

@@ -54,6 +54,7 @@
 #include "hb_prep.hpp"
 #include "hb_sampler_view.hpp"
 #include "hb_walls.hpp"
+#include "hb_wave.hpp"
 
 extern "C" int hbx_set_error(const char* msg);
 extern "C" int hbx_ctx_device(const hb_ctx* c);
@@ -61,6 +62,7 @@ extern "C" int hbx_ctx_prep_args(hb_ctx* c, void** wc, void* mags, double** tab_
 extern "C" int hbx_loglik_accept_dev(hb_ctx* c, const double* d_params, int w, double* d_logl, const void* acc,
                                      void* stream);
 extern "C" long hbx_ctx_wave_lds(const hb_ctx* c);
+extern "C" int hbx_ctx_wave_eval_args(hb_ctx* c, void* out);
 
 namespace hbds {
 
@@ -402,18 +404,30 @@ static_assert(kPW == hbk::kPrepRoles, "the propose workgroup is one prep group")
 #else
 #define HB_DS_PROPOSE_ATTR
 #endif
+constexpr bool kDsStepDefault = false;  // ds_step until measured on the GPU (HB_DS_STEP=1 turns it on)
+// LDS of a propose workgroup (ds_propose; ds_step's slabs alias it once the
+// records are written)
+struct ProposeShared {
+  uint64_t tab[hbglibc::kTabWords];  // exp / log / pow tables (divergent lookups)
+  double gs[kPW][32];
+  hbk::PrepShared<kPW> PL;
+  int jl[kPW];
+};
+// the body of ds_propose: every wave of the workgroup calls it (it holds the
+// prep group's barriers); j_out: the wave's global slot, act_out: whether it
+// has one (the grid's last workgroup may hold fewer than kPW)
 template <bool PREP>
-__global__ __launch_bounds__(64 * kPW) HB_DS_PROPOSE_ATTR void ds_propose(Dev D, int W, int NPAST, long long iter,
-                                                       const unsigned long long* __restrict__ sch_src,
-                                                       unsigned long long* __restrict__ sch_dst, long long n8) {
+__device__ __forceinline__ void propose_group(const Dev& D, int W, int NPAST, long long iter,
+                                              const unsigned long long* __restrict__ sch_src,
+                                              unsigned long long* __restrict__ sch_dst, long long n8,
+                                              ProposeShared& Ls, int& j_out, bool& act_out) {
   const long long sgt = (long long)(gridDim.x - 1 - blockIdx.x) * blockDim.x + threadIdx.x;
   const long long sgs = (long long)gridDim.x * blockDim.x;
   unsigned long long sv = 0;
   if (sgt < n8) sv = __hip_atomic_load(sch_src + sgt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  __shared__ uint64_t tab_s[hbglibc::kTabWords];  // exp / log / pow tables (divergent lookups)
-  __shared__ double gs_s[kPW][32];
-  __shared__ hbk::PrepShared<kPW> PL;
-  __shared__ int jl_s[kPW];
+  uint64_t* tab_s = Ls.tab;
+  hbk::PrepShared<kPW>& PL = Ls.PL;
+  int* jl_s = Ls.jl;
   const Params* P = D.P;
   const hbglibc::Tabs T{tab_s, tab_s + 256, tab_s + 512};
   {
@@ -432,7 +446,9 @@ __global__ __launch_bounds__(64 * kPW) HB_DS_PROPOSE_ATTR void ds_propose(Dev D,
   const bool act = k < D.nl;
   const int j = act ? D.order[k] : D.lo;  // global slot
   const int jl = j - D.lo;                // local slot (arrays by slot)
-  double* gs = gs_s[wv];
+  double* gs = Ls.gs[wv];
+  j_out = j;
+  act_out = act;
   const double pc_tab = PREP ? *D.tab_pc : 0.0;
 #ifdef HB_DS_TIMING  // experiment builds only: per-phase shader clocks of two slots at iteration 100
   long long tclk[8], tw0 = wall_clock64();
@@ -577,6 +593,56 @@ __global__ __launch_bounds__(64 * kPW) HB_DS_PROPOSE_ATTR void ds_propose(Dev D,
     const int w = q / hbk::kWcDoubles, f = q - w * hbk::kWcDoubles;
     D.wc[(size_t)jl_s[w] * hbk::kWcDoubles + f] = PL.so[w * hbk::kSoStride + f];
   }
+}
+template <bool PREP>
+__global__ __launch_bounds__(64 * kPW) HB_DS_PROPOSE_ATTR void ds_propose(Dev D, int W, int NPAST, long long iter,
+                                                       const unsigned long long* __restrict__ sch_src,
+                                                       unsigned long long* __restrict__ sch_dst, long long n8) {
+  __shared__ ProposeShared S;
+  int j;
+  bool act;
+  propose_group<PREP>(D, W, NPAST, iter, sch_src, sch_dst, n8, S, j, act);
+}
+
+// The whole iteration up to the swaps in ONE launch (propose -> records ->
+// likelihood -> Hastings test), for a shard of at most one resident round
+// (nl <= 16 per CU) on the one-wave plan: each workgroup's four waves propose
+// their slots (hot rungs first, order[]), turn into the prep group for their
+// records, then each evaluates its own slot's proposal and tests it.  A hot
+// slot's long wall run no longer holds the whole likelihood launch back at a
+// kernel boundary: the SIMD it shares with colder slots' waves runs their
+// likelihoods meanwhile.  The likelihood and the test are those of the
+// separate launch (hb_wave.hpp eval_wave_body, hb_accept.hpp), on the same
+// records, so every result is bit-identical.  LDS: the propose stage's tables
+// and prep scratch, then (after the barrier that publishes the records) the
+// four waves' slabs over the same bytes.  prio: the propose stage's wave
+// priority (s_setprio; the likelihood starts at 3, lowered by the pacer).
+template <int VPT>
+__global__ __launch_bounds__(64 * kPW) __attribute__((amdgpu_waves_per_eu(4))) void ds_step(
+    Dev D, int W, int NPAST, long long iter, const unsigned long long* __restrict__ sch_src,
+    unsigned long long* __restrict__ sch_dst, long long n8, hbk::WaveEvalArgs E, AccArgs A, int prio) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_all[];
+  ProposeShared& S = *reinterpret_cast<ProposeShared*>(smem_all);
+  if (prio == 3) __builtin_amdgcn_s_setprio(3);
+  else if (prio == 2) __builtin_amdgcn_s_setprio(2);
+  else if (prio == 1) __builtin_amdgcn_s_setprio(1);
+  int j;
+  bool act;
+  propose_group<true>(D, W, NPAST, iter, sch_src, sch_dst, n8, S, j, act);
+  __builtin_amdgcn_s_waitcnt(0);  // the group's records acknowledged (L2) before any wave's scalar loads
+  __syncthreads();                // and the propose / prep LDS is dead: the slabs take it
+  if (!act) return;
+  const int jl = __builtin_amdgcn_readfirstlane(j - D.lo);
+  const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  // the records just written: scalar loads (constant address space), issued
+  // only after the barrier (the pointer passes through asm)
+  typedef const __attribute__((address_space(4))) hbdev::WalkerConst cwc_t;
+  uint64_t a = (uint64_t)D.wc;
+  __asm__ volatile("" : "+s"(a));
+  const hbdev::WalkerConst* wcs = (const hbdev::WalkerConst*)(cwc_t*)a;
+  hbk::eval_wave_body<VPT, true, 1>(E.t, E.ph, E.f, E.isg, E.rows, E.n, E.kth, wcs[jl], jl, jl, D.logLy, nullptr, 0,
+                                    E.slab_bytes, E.slab_bytes, E.gap, A, smem_all + (size_t)wv * (size_t)E.lds_per,
+                                    E.dq);
 }
 
 // Hastings test and history (:492-546); 64 slots per block (one lane each),
@@ -938,6 +1004,12 @@ struct hb_dsampler {
   int nthreads = 0;
   int nseg = 1;  // swap segments (ds_swap_seg workgroups) over the owned slots
   bool fused_prep = true;  // walker records in ds_propose's epilogue (else an hb_prep_kernel launch)
+  // propose, records, likelihood and Hastings test in ONE launch (ds_step):
+  // one resident round of slots on the one-wave plan at 4, 8 or 16 cadences
+  // per lane whose four slabs fit a quarter of the CU's LDS; HB_DS_STEP=1 / 0
+  // (A/B knob): on / off
+  bool step = false;
+  int step_prio = 0;  // the propose stage's s_setprio (HB_DS_STEP_PRIO, A/B knob)
   double* d_lslot = nullptr; // [W] logL by slot after the Hastings test (one-process samplers)
   bool lslot_now = false;    // this iteration's fused Hastings test wrote d_lslot
   // host timers [s]: producer work (all threads), waits for a schedule, issue
@@ -1252,6 +1324,16 @@ static hb_dsampler* ds_create(hb_sampler* s, hb_ctx* ctx, const int* chain_of_sl
       cus = 256;
     const char* fp = getenv("HB_DS_FUSED_PREP");
     d->fused_prep = fp ? atoi(fp) != 0 : d->nl <= 16 * cus;
+    hbk::WaveEvalArgs E{};
+    const char* st = getenv("HB_DS_STEP");
+    const char* sp = getenv("HB_DS_STEP_PRIO");
+    d->step_prio = sp ? std::max(0, std::min(3, atoi(sp))) : 0;
+    const bool step_on = st ? atoi(st) != 0 : kDsStepDefault;
+    if (d->fused_prep && step_on && hbx_ctx_wave_eval_args(ctx, &E) == 0 && E.wpw == 1 &&
+        (E.vpt == 4 || E.vpt == 8 || E.vpt == 16)) {
+      const size_t lds = std::max((size_t)kPW * (size_t)E.lds_per, sizeof(ProposeShared));
+      d->step = lds <= 163840 / 4;
+    }
   }
   if (const char* ee = getenv("HB_DS_EV_EVERY")) {  // experiment knob
     // a producer reuses ring slot q % R_RING once the event after iteration
@@ -1596,29 +1678,50 @@ static long ds_begin(hb_dsampler* d, long iter, double* send, long cap) {
   auto* sch_src = reinterpret_cast<const unsigned long long*>(d->pin[slot]);
   auto* sch_dst = reinterpret_cast<unsigned long long*>(d->d_sched[slot]);
   const long long n8 = (long long)(used_bytes / 8);
-  if (d->fused_prep)
-    ds_propose<true><<<(nl + kPW - 1) / kPW, 64 * kPW, 0, s>>>(Dp, W, NPAST, (long long)iter, sch_src, sch_dst, n8);
-  else
-    ds_propose<false><<<(nl + kPW - 1) / kPW, 64 * kPW, 0, s>>>(Dp, W, NPAST, (long long)iter, sch_src, sch_dst, n8);
-  DS_TRY(hipGetLastError(), "ds_propose");
-  if (!d->fused_prep) {
-    const int rc = hb_prepare_dev(d->ctx, D.y, nl, (void*)s);
-    if (rc) return rc;
-  }
-  // likelihood with the Hastings test fused into its waves' epilogue
-  // (hb_accept.hpp); ds_accept only where the plan has no one-wave kernel
-  AccArgs acc{D.idx, D.logL, D.logP, D.logPy, D.temp, D.alpha2, D.jump, D.jtype, D.x, D.y, D.hist,
-              D.DEacc_arr, D.ctr, D.ev, d->P.log_on, NPAST, (long long)iter, d->lo, 0,
-              D.ecnt, D.elist, nl, 0, d->d_lslot};  // Lslot: null for exchanging samplers
-  int rc = hbx_loglik_accept_dev(d->ctx, D.y, nl, D.logLy, &acc, (void*)s);
-  d->lslot_now = rc == 0 && acc.Lslot != nullptr;
-  if (rc == 1) {
-    rc = hb_evaluate_dev(d->ctx, nl, D.logLy, 0, (void*)s);
-    if (rc) return rc;
-    ds_accept<<<(nl + 63) / 64, kAccThreads, 0, s>>>(D, W, NPAST, (long long)iter);
-    DS_TRY(hipGetLastError(), "ds_accept");
-  } else if (rc) {
-    return rc;
+  if (d->step) {
+    // propose -> records -> likelihood -> Hastings test, one launch
+    hbk::WaveEvalArgs E{};
+    if (const int rc = hbx_ctx_wave_eval_args(d->ctx, &E)) return rc;
+    Dev Ds = Dp;
+    Ds.ecnt = nullptr;  // the waves evaluate their own slots: no e-order lists
+    const AccArgs acc{D.idx, D.logL, D.logP, D.logPy, D.temp, D.alpha2, D.jump, D.jtype, D.x, D.y, D.hist,
+                      D.DEacc_arr, D.ctr, D.ev, d->P.log_on, NPAST, (long long)iter, d->lo, 0,
+                      nullptr, nullptr, nl, 0, d->d_lslot};  // Lslot: null for exchanging samplers
+    const size_t lds = std::max((size_t)kPW * (size_t)E.lds_per, sizeof(ProposeShared));
+    const dim3 grid((nl + kPW - 1) / kPW), blk(64 * kPW);
+    if (E.vpt == 16)
+      ds_step<16><<<grid, blk, lds, s>>>(Ds, W, NPAST, (long long)iter, sch_src, sch_dst, n8, E, acc, d->step_prio);
+    else if (E.vpt == 8)
+      ds_step<8><<<grid, blk, lds, s>>>(Ds, W, NPAST, (long long)iter, sch_src, sch_dst, n8, E, acc, d->step_prio);
+    else
+      ds_step<4><<<grid, blk, lds, s>>>(Ds, W, NPAST, (long long)iter, sch_src, sch_dst, n8, E, acc, d->step_prio);
+    DS_TRY(hipGetLastError(), "ds_step");
+    d->lslot_now = acc.Lslot != nullptr;
+  } else {
+    if (d->fused_prep)
+      ds_propose<true><<<(nl + kPW - 1) / kPW, 64 * kPW, 0, s>>>(Dp, W, NPAST, (long long)iter, sch_src, sch_dst, n8);
+    else
+      ds_propose<false><<<(nl + kPW - 1) / kPW, 64 * kPW, 0, s>>>(Dp, W, NPAST, (long long)iter, sch_src, sch_dst, n8);
+    DS_TRY(hipGetLastError(), "ds_propose");
+    if (!d->fused_prep) {
+      const int rc = hb_prepare_dev(d->ctx, D.y, nl, (void*)s);
+      if (rc) return rc;
+    }
+    // likelihood with the Hastings test fused into its waves' epilogue
+    // (hb_accept.hpp); ds_accept only where the plan has no one-wave kernel
+    AccArgs acc{D.idx, D.logL, D.logP, D.logPy, D.temp, D.alpha2, D.jump, D.jtype, D.x, D.y, D.hist,
+                D.DEacc_arr, D.ctr, D.ev, d->P.log_on, NPAST, (long long)iter, d->lo, 0,
+                D.ecnt, D.elist, nl, 0, d->d_lslot};  // Lslot: null for exchanging samplers
+    int rc = hbx_loglik_accept_dev(d->ctx, D.y, nl, D.logLy, &acc, (void*)s);
+    d->lslot_now = rc == 0 && acc.Lslot != nullptr;
+    if (rc == 1) {
+      rc = hb_evaluate_dev(d->ctx, nl, D.logLy, 0, (void*)s);
+      if (rc) return rc;
+      ds_accept<<<(nl + 63) / 64, kAccThreads, 0, s>>>(D, W, NPAST, (long long)iter);
+      DS_TRY(hipGetLastError(), "ds_accept");
+    } else if (rc) {
+      return rc;
+    }
   }
   long n = 0;
   if (d->xchg) {

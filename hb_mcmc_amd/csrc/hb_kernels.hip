@@ -48,27 +48,35 @@ using namespace hbdev;
 // Experiment builds only (HB_WAVE_CLOCKS): per-wave shader clock at entry and
 // exit plus HW_ID / XCC_ID, read back by hb_debug_wave_clocks().
 #ifdef HB_WAVE_CLOCKS
-// 8 words per wave: start, phase marks 0..2 (after the model pass, the keys,
+// 10 words per wave: start, phase marks 0..2 (after the model pass, the keys,
 // the select; 0 if not reached), end, HW_ID, XCC_ID, mark 3 (the model loop's
-// end, before the deferred queue is applied)
-__device__ unsigned long long hb_wave_clk[8 * 65536];
-#define HB_CLK_BEGIN()                                     \
-  const unsigned long long clk0_ = __builtin_amdgcn_s_memtime(); \
+// end, before the deferred queue is applied), s_memrealtime (100 MHz) at start
+// and end: the in-kernel shader clock is d memtime / d memrealtime x 100 MHz
+// (MI355X_MICROARCH.md, DVFS give-back item 6)
+constexpr int kClkWords = 10;
+__device__ unsigned long long hb_wave_clk[kClkWords * 65536];
+#define HB_CLK_BEGIN()                                                 \
+  const unsigned long long rt0_ = __builtin_amdgcn_s_memrealtime();    \
+  const unsigned long long clk0_ = __builtin_amdgcn_s_memtime();       \
   unsigned long long clkm_[4] = {0ull, 0ull, 0ull, 0ull}
 #define HB_CLK_MARK(i) clkm_[(i)] = __builtin_amdgcn_s_memtime()
-#define HB_CLK_END(wv)                                                                  \
-  do {                                                                                  \
-    const unsigned long long clk1_ = __builtin_amdgcn_s_memtime();                      \
-    if ((threadIdx.x & 63) == 0 && (wv) < 65536) {                                      \
-      hb_wave_clk[8 * (wv) + 0] = clk0_;                                                \
-      hb_wave_clk[8 * (wv) + 1] = clkm_[0];                                             \
-      hb_wave_clk[8 * (wv) + 2] = clkm_[1];                                             \
-      hb_wave_clk[8 * (wv) + 3] = clkm_[2];                                             \
-      hb_wave_clk[8 * (wv) + 4] = clk1_;                                                \
-      hb_wave_clk[8 * (wv) + 5] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);  \
-      hb_wave_clk[8 * (wv) + 6] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 20); \
-      hb_wave_clk[8 * (wv) + 7] = clkm_[3];                                             \
-    }                                                                                   \
+#define HB_CLK_END(wv)                                                                          \
+  do {                                                                                          \
+    const unsigned long long clk1_ = __builtin_amdgcn_s_memtime();                              \
+    const unsigned long long rt1_ = __builtin_amdgcn_s_memrealtime();                           \
+    if ((threadIdx.x & 63) == 0 && (wv) < 65536) {                                              \
+      unsigned long long* o_ = hb_wave_clk + kClkWords * (wv);                                  \
+      o_[0] = clk0_;                                                                            \
+      o_[1] = clkm_[0];                                                                         \
+      o_[2] = clkm_[1];                                                                         \
+      o_[3] = clkm_[2];                                                                         \
+      o_[4] = clk1_;                                                                            \
+      o_[5] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);                              \
+      o_[6] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 20);                             \
+      o_[7] = clkm_[3];                                                                         \
+      o_[8] = rt0_;                                                                             \
+      o_[9] = rt1_;                                                                             \
+    }                                                                                           \
   } while (0)
 // the fused launch's prologue (wave 0 of each workgroup): 0 entry, 1 parameters
 // in LDS, 2 records in LDS (prep_records done), 3 after the last barrier,
@@ -484,6 +492,10 @@ __device__ __forceinline__ void fused_prologue(const PreArgs& pa, int count, int
   PrepShared<WPB>& L = *reinterpret_cast<PrepShared<WPB>*>(smem_all);
   const int tid = threadIdx.x;
   HB_PCLK(0, 0);
+#ifndef HB_PRO_PRIO
+#define HB_PRO_PRIO 0  // A/B knob: 1 = the prep role waves at priority 3 over the table waves
+#endif
+  if (HB_PRO_PRIO && (tid >> 6) < kPrepRoles) __builtin_amdgcn_s_setprio(3);
   const int base = blockIdx.x * WPB;
   const int nb = min(WPB, count - base);
   {  // parameters, all loads in flight before the first LDS write
@@ -1431,7 +1443,7 @@ extern "C" int hb_debug_prologue_clocks(unsigned long long* out, int nwg) {
 }
 extern "C" int hb_debug_wave_clocks(unsigned long long* out, int nwaves) {
   if (nwaves > 65536) nwaves = 65536;
-  hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(hb_wave_clk), 8 * sizeof(unsigned long long) * nwaves);
+  hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(hb_wave_clk), kClkWords * sizeof(unsigned long long) * nwaves);
   return e == hipSuccess ? 0 : -1;
 }
 #endif

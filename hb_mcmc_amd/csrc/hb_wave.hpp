@@ -159,7 +159,10 @@ __device__ __forceinline__ void dq_apply(const WalkerConst& w, double* vals, con
 // nearly every cadence.  Otherwise (high e, sparse or shuffled cadences) the
 // cold path with four interleaved cadences per lane is faster.
 constexpr double kWarmD1 = 0x1p-10;
-constexpr int kChainVptMin = 8, kChainVptMax = 32;  // cadences per lane of the chain path
+#ifndef HB_CHAIN_VPT_MIN
+#define HB_CHAIN_VPT_MIN 8  // A/B knob (catalog classes of 4 cadences per lane)
+#endif
+constexpr int kChainVptMin = HB_CHAIN_VPT_MIN, kChainVptMax = 32;  // cadences per lane of the chain path
 __device__ __forceinline__ bool chain_eligible(const WalkerConst& w, double gap) {
   const double e = w.e;
   const double dm = gap * kDay * fabs(w.mA);

@@ -7,6 +7,10 @@
 * walkers theta_w = THETA_STAR + 0.1 * sigma_prop * z_w reflected into the
   set_limits prior box (likelihood3.c:986-1121), slot 2 (log P) fixed, with a
   fraction pushed into Roche-lobe overflow (e -> 0.9x, logL = -5e14).
+* prior-spread walkers (``prior_walkers``): uniform over the set_limits box
+  like the reference's random initial state (mcmc_wrapper2.c:236-252) -- the
+  spread the sampler's hot rungs keep: e over [0, 1), cold-path and Roche
+  walkers.
 * mag_data = {1000, 1, 1, 1, 1}, magerr = 1e15 (mcmc_wrapper2.c:321-327).
 """
 from __future__ import annotations
@@ -87,6 +91,20 @@ def walkers(w: int, seed: int = 7, roche_frac: float = 0.05, scale: float = 0.1,
     if nro:
         idx = g.choice(w, size=nro, replace=False)
         x[idx, 3] = 0.9 + 0.09 * g.random(nro)  # tight periastron -> Roche overflow
+    return np.ascontiguousarray(x)
+
+
+def prior_walkers(w: int, seed: int = 11, theta: np.ndarray | None = None) -> np.ndarray:
+    """W x 21 walkers drawn uniformly from the set_limits box, slot 2 = the
+    light curve's log P and slot 6 folded into [0, P), as the reference's
+    random initial state (mcmc_wrapper2.c:236-252: x = lo + u (hi - lo))."""
+    th = THETA_STAR if theta is None else np.asarray(theta, dtype=np.float64)
+    lc_period = 10.0 ** th[2]
+    lo, hi, _, _ = prior_box(lc_period)
+    u = np.random.Generator(np.random.PCG64(seed)).random((w, NPARS))
+    x = lo[None, :] + u * (hi - lo)[None, :]
+    x[:, 2] = th[2]
+    x[:, 6] = np.fmod(x[:, 6], lc_period)
     return np.ascontiguousarray(x)
 
 

@@ -1,6 +1,8 @@
 """Per-wave lifetimes of the C2 eval kernel (experiment build with
 -DHB_WAVE_CLOCKS, loaded through HBMI_LIB): start/end shader clocks, SIMD and
-CU of every wave, then per-SIMD occupancy over the kernel's span.
+CU of every wave, then per-SIMD occupancy over the kernel's span, and the
+in-kernel shader clock (d s_memtime / d s_memrealtime x 100 MHz per wave,
+median; after >= 2 s of back-to-back launches, MI355X_MICROARCH.md DVFS item 6).
 
     HBMI_LIB=.../libhbmi_clk.so python scripts/wave_clocks.py [--ncad 1024] [--walkers 4096]
 """
@@ -16,6 +18,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--ncad", type=int, default=1024)
 ap.add_argument("--walkers", type=int, default=4096)
 ap.add_argument("--reps", type=int, default=20)
+ap.add_argument("--seconds", type=float, default=2.5, help="back-to-back launches before the sampled one")
 ap.add_argument("--fused", action="store_true", help="time hb_loglik_batch_dev (the fused launch when it applies)")
 a = ap.parse_args()
 n, w = a.ncad, a.walkers
@@ -29,13 +32,18 @@ L.reserve(w)
 P = torch.from_numpy(synth.walkers(w, seed=1000)).cuda()
 out = torch.empty(w, dtype=torch.float64, device="cuda")
 st = torch.cuda.current_stream()
-for _ in range(a.reps):
-    if a.fused:
-        L.loglike_dev(P, out, st)
-    else:
-        L.prepare_dev(P, st)
-        L.evaluate_dev(w, out, 0, st)
-torch.cuda.synchronize()
+import time  # noqa: E402
+t_end = time.perf_counter() + a.seconds
+k = 0
+while k < a.reps or time.perf_counter() < t_end:
+    for _ in range(50):
+        if a.fused:
+            L.loglike_dev(P, out, st)
+        else:
+            L.prepare_dev(P, st)
+            L.evaluate_dev(w, out, 0, st)
+    k += 50
+    torch.cuda.synchronize()
 lib = _lib.lib()
 prologue = None
 if a.fused and L.fused_wpb(w) > 0:  # the fused prologue's marks, wave 0 of every workgroup
@@ -51,9 +59,11 @@ if a.fused and L.fused_wpb(w) > 0:  # the fused prologue's marks, wave 0 of ever
                 "mean_cycles_from_entry": [float(x) for x in d.mean(axis=0)],
                 "max_cycles_from_entry": [float(x) for x in d.max(axis=0)],
                 "entry_spread_cycles": float(pc[:, 0].max() - pc[:, 0].min())}
-buf = (C.c_ulonglong * (8 * w))()
+NW = 10  # words per wave (hb_kernels.hip kClkWords)
+buf = (C.c_ulonglong * (NW * w))()
 assert lib.hb_debug_wave_clocks(buf, w) == 0
-c = np.frombuffer(buf, dtype=np.uint64).reshape(w, 8).astype(np.int64)
+c = np.frombuffer(buf, dtype=np.uint64).reshape(w, NW).astype(np.int64)
+rt = c[:, 9] - c[:, 8]  # 100 MHz ticks
 t0, t1, hw, xcc = c[:, 0], c[:, 4], c[:, 5], c[:, 6]
 marks = c[:, 1:4]
 if (c[:, 7] > 0).any():  # mark 3: the model loop's end, before the deferred queue
@@ -72,7 +82,11 @@ if marks.shape[1] == 4:
 res = {"phase_names": names,
        "phase_mean_cycles": [float(x) for x in ph.mean(axis=0)] if len(ph) else None,
        "waves": int(w), "life_mean": float(life.mean()), "life_min": int(life.min()), "life_max": int(life.max()),
-       "life_pct": [float(x) for x in np.percentile(life, [5, 25, 50, 75, 95])]}
+       "life_pct": [float(x) for x in np.percentile(life, [5, 25, 50, 75, 95])],
+       "launches_before_sample": int(k),
+       "shader_clock_ghz_median": float(np.median((life / np.maximum(rt, 1))[rt > 100]) * 0.1),
+       "shader_clock_ghz_pct": [float(x) for x in np.percentile((life / np.maximum(rt, 1))[rt > 100] * 0.1,
+                                                                 [5, 25, 50, 75, 95])]}
 spans, occ, order = [], [], []
 for k in np.unique(key):
     m = key == k

@@ -521,6 +521,31 @@ def test_full_size_c2_against_oracle_and_properties(hbmi, oracle):
     assert np.isfinite(a[~roche]).all()
 
 
+@pytest.mark.parametrize("seed", [11, 12])
+def test_prior_spread_walkers_c2(hbmi, oracle, seed):
+    """W = 4096, N = 1024 on walkers drawn from the set_limits box like the
+    reference's random initial state (mcmc_wrapper2.c:236-252): e over
+    [0, 1), masses over the whole prior range -- cold-path (e > 0.8) and
+    Roche walkers, the spread the sampler's hot rungs feed the likelihood
+    (the bench's c2_prior_spread key).  Every walker against the oracle (NaN
+    pattern and Roche sentinel exact, 1e-10 relative otherwise), and each
+    walker bit-identical when the batch is reversed."""
+    from hb_mcmc_amd import synth
+    from hb_mcmc_amd.likelihood import HBLikelihood
+
+    t, f, s = synth.dataset(1024, oracle.light_curve)
+    P = synth.prior_walkers(4096, seed=seed)
+    with HBLikelihood(t, f, s) as L:
+        a = L.loglike(P)
+        rev = L.loglike(P[::-1].copy())[::-1]
+    assert np.array_equal(a, rev, equal_nan=True)
+    ref = oracle.loglike_batch(t, f, s, P, synth.MAG_DEFAULT, synth.MAGERR_DEFAULT, 8)
+    close_logl(a, ref)
+    roche = ref == -5e14
+    assert 0.3 < roche.mean() < 0.8
+    assert ((P[:, 3] > 0.8) & ~roche).sum() >= 20  # cold-path walkers are exercised
+
+
 # ------------------------------------------------- full-size (config C4)
 def test_full_size_c4_against_oracle_and_properties(hbmi, oracle):
     """W = 65 536, N = 1024 (BASELINE config C4's whole ensemble on one GPU):
