@@ -99,7 +99,10 @@ struct AccArgs {
 // so it lasts as long as the SIMD whose walkers cost most; cost follows e
 // (high e leaves the warm Kepler chains for the cold path), and waves taking
 // the walkers by descending e give every SIMD walkers from the whole e range
-// (sampler states of a 200-iteration run: 53 us in slot order, 47 us sorted).
+// (sampler states of a 200-iteration run: 53 us in slot order, 47 us sorted;
+// bins by expected cost from the records instead -- cold path by e, warm
+// chains, Roche walkers last -- measured the same: 0.0918-0.0923 ms per
+// iteration either way, profiles/r05/r05d_ds_cost_order_ab.txt).
 // The order within a bin is immaterial: a wave's result depends on its
 // walker only.  One load and a wave scan over the 64 bin counts.
 __device__ __forceinline__ int eval_slot_by_e(const AccArgs& A, int s, int lane) {

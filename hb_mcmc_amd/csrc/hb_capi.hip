@@ -787,10 +787,11 @@ static int catalog_run(hb_catalog* c, const double* d_params, double* d_logl, hi
   HB_TRY(hbk::launch_prep(d_params, c->total, unused, c->d_wc, s, c->d_tab, c->d_wt, c->d_t, 0, c->d_ph, c->d_w0,
                           c->ntargets),
          "prep launch");
-  // classes by descending work, each to the stream with the least work so
-  // far (longest-processing-time first; C5: the pair class alone is 43% of
-  // the cadence work, so round-robin left one stream with 110k of the 170k
-  // walker-cadences); HB_CAT_DEAL=0 (A/B knob): round-robin
+  // classes by descending work, dealt round-robin over the caller's stream
+  // and the forked ones.  (Longest-processing-time dealing -- each class to
+  // the stream with the least work so far -- measured slower: C5 162-164 vs
+  // 152-154 us per call, profiles/r05/r05c_c5_ab.txt: it leaves the
+  // LDS-limited 32-cadences-per-lane class running alone at the end.)
   int order[kCatClasses], nc = 0;
   for (int cl = 0; cl < kCatClasses; ++cl)
     if (c->class_off[cl + 1] > c->class_off[cl]) order[nc++] = cl;
@@ -799,26 +800,17 @@ static int catalog_run(hb_catalog* c, const double* d_params, double* d_logl, hi
   // (profiles/r04/r04c_bench_c5_s*.json, two-launch path: the forked streams'
   // event waits cost more than the extra overlap buys)
   static const int kns = std::max(1, std::min(kCatStreams, cat_env("HB_CAT_STREAMS", kCatDefaultStreams)));
-  static const bool lpt = cat_env("HB_CAT_DEAL", 1) != 0;
   const int ns = nc < kns ? nc : kns;
   if (ns > 1) {
     HB_TRY(hipEventRecord(c->ev_fork, s), "fork event");
     for (int i = 0; i < ns - 1; ++i) HB_TRY(hipStreamWaitEvent(c->aux[i], c->ev_fork, 0), "fork wait");
   }
-  long load[kCatStreams] = {0};
   for (int j = 0; j < nc; ++j) {
     const int cl = order[j];
     const int cnt = c->class_off[cl + 1] - c->class_off[cl];
     int vpt, wpw;
     catalog_class_geometry(cl, vpt, wpw);
-    int si = j % ns;
-    if (lpt) {
-      si = 0;
-      for (int i = 1; i < ns; ++i)
-        if (load[i] < load[si]) si = i;
-    }
-    load[si] += c->class_work[cl];
-    hipStream_t sj = si == 0 ? s : c->aux[si - 1];
+    hipStream_t sj = (j % ns == 0) ? s : c->aux[j % ns - 1];
     const int* lst = c->d_list + c->class_off[cl];
     double* dq = reinterpret_cast<double*>(reinterpret_cast<unsigned char*>(c->d_dq) + c->class_dq[cl]);
     HB_TRY(hbk::launch_eval_multi(vpt, c->class_slab[cl], c->d_t, c->d_ph, c->d_f, c->d_s, c->d_rows, c->d_tab,

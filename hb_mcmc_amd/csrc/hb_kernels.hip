@@ -16,6 +16,7 @@
 // All launches are asynchronous on the caller's stream and allocation-free
 // once hb_reserve() sized the workspace.
 #include <hip/hip_runtime.h>
+#include <stddef.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
@@ -492,10 +493,6 @@ __device__ __forceinline__ void fused_prologue(const PreArgs& pa, int count, int
   PrepShared<WPB>& L = *reinterpret_cast<PrepShared<WPB>*>(smem_all);
   const int tid = threadIdx.x;
   HB_PCLK(0, 0);
-#ifndef HB_PRO_PRIO
-#define HB_PRO_PRIO 0  // A/B knob: 1 = the prep role waves at priority 3 over the table waves
-#endif
-  if (HB_PRO_PRIO && (tid >> 6) < kPrepRoles) __builtin_amdgcn_s_setprio(3);
   const int base = blockIdx.x * WPB;
   const int nb = min(WPB, count - base);
   {  // parameters, all loads in flight before the first LDS write

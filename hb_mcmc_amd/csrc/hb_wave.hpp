@@ -159,10 +159,9 @@ __device__ __forceinline__ void dq_apply(const WalkerConst& w, double* vals, con
 // nearly every cadence.  Otherwise (high e, sparse or shuffled cadences) the
 // cold path with four interleaved cadences per lane is faster.
 constexpr double kWarmD1 = 0x1p-10;
-#ifndef HB_CHAIN_VPT_MIN
-#define HB_CHAIN_VPT_MIN 8  // A/B knob (catalog classes of 4 cadences per lane)
-#endif
-constexpr int kChainVptMin = HB_CHAIN_VPT_MIN, kChainVptMax = 32;  // cadences per lane of the chain path
+// cadences per lane of the chain path (4: catalog classes of 129-256 cadences
+// on warm chains measured within noise, profiles/r05/r05c_c5_ab.txt)
+constexpr int kChainVptMin = 8, kChainVptMax = 32;
 __device__ __forceinline__ bool chain_eligible(const WalkerConst& w, double gap) {
   const double e = w.e;
   const double dm = gap * kDay * fabs(w.mA);
@@ -244,29 +243,41 @@ __device__ __forceinline__ void model_pass_cold(const double* __restrict__ t, co
 // request instead of 64 strided ones.  NR: lane rows of the walker (the
 // arrays' pitch: 64, or 128 / 256 for 2 / 4 waves, each passing tT offset by
 // its first row); row: this lane's row.
+template <int VPT>
+constexpr int chain_kc() { return VPT < HB_KC ? VPT : HB_KC; }
+// The chains' first cadences (step 0 of model_pass_chain_pipe): the
+// reference's start from the phase-table entries, Newton to convergence.
+template <int VPT, int NR = 64>
+__device__ __forceinline__ void chain_step0(const double* __restrict__ tT, const double2* __restrict__ ph, int n,
+                                            const Rows& rw, const WalkerConst& w, int lane, int row,
+                                            ChainState<chain_kc<VPT>()>& st, bool& ok) {
+  constexpr int KC = chain_kc<VPT>();
+  const int lc = (rw.rc + KC - 1) / KC;
+  const bool tab = (ph != nullptr) && (w.tab != 0.0);  // walker-uniform
+  const int last = n - 1;
+  const int base = row * rw.rc;
+  double tk[KC];
+  double2 p0[KC];
+#pragma unroll
+  for (int k = 0; k < KC; ++k) tk[k] = tT[min(k * lc, rw.rc - 1) * NR + lane];
+#pragma unroll
+  for (int k = 0; k < KC; ++k) p0[k] = tab ? ph[min(base + k * lc, last)] : make_double2(0.0, 1.0);
+  ok = true;
+  chain_first<KC>(tk, p0, tab, w, st, ok);
+}
 template <int VPT, int NR = 64>
 __device__ __forceinline__ void model_pass_chain_pipe(const double* __restrict__ tT, const double2* __restrict__ ph,
                                                       int n, const Rows& rw, const WalkerConst& w, double* vals,
                                                       int lane, int row, Pacer pc, DeferQ& dq) {
-  constexpr int KC = VPT < HB_KC ? VPT : HB_KC;
+  constexpr int KC = chain_kc<VPT>();
   const int lc = (rw.rc + KC - 1) / KC;  // chain length (wave-uniform)
-  const bool tab = (ph != nullptr) && (w.tab != 0.0);  // walker-uniform
-  const int last = n - 1;
-  const int base = row * rw.rc;
   const int rs = row * rw.stride;  // slab_pos = rs + c
   const bool live = NR <= 128 || row < rw.live;
   ChainState<KC> st;
   double tk[KC];
-#pragma unroll
-  for (int k = 0; k < KC; ++k) tk[k] = tT[min(k * lc, rw.rc - 1) * NR + lane];
   // the step whose polynomial is pending: its (s, c, 1/den) are the chain state
   bool pend_ok = true;
-  {  // step 0: the chains' first cadences (the reference's start, table entries)
-    double2 p0[KC];
-#pragma unroll
-    for (int k = 0; k < KC; ++k) p0[k] = tab ? ph[min(base + k * lc, last)] : make_double2(0.0, 1.0);
-    chain_first<KC>(tk, p0, tab, w, st, pend_ok);
-  }
+  chain_step0<VPT, NR>(tT, ph, n, rw, w, lane, row, st, pend_ok);
   // store the pending step jp's values and queue its eclipse / slow-path
   // cadences; cadences past n (the last row's padding) store harmless values
   // (their keys are masked); the rows kernel (NR > 128) sizes its slab to the

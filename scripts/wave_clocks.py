@@ -95,6 +95,13 @@ for k in np.unique(key):
     occ.append(life[m].sum() / max(1, (a1 - a0)))
     srt = np.argsort(t0[m])
     order.append(list((t1[m][srt] - a0)))
+# wall-clock view (s_memrealtime, 100 MHz, one counter for the whole chip):
+# the launch's span from its first wave's start to its last wave's end, and
+# how the wave starts and ends spread over it
+r0, r1 = c[:, 8], c[:, 9]
+res["realtime_span_us"] = float((r1.max() - r0.min()) / 100.0)
+res["wave_start_us_pct"] = [float(x) for x in np.percentile((r0 - r0.min()) / 100.0, [0, 50, 90, 100])]
+res["wave_end_us_pct"] = [float(x) for x in np.percentile((r1 - r0.min()) / 100.0, [0, 50, 90, 100])]
 res["simds"] = len(spans)
 res["waves_per_simd"] = float(w / len(spans))
 res["simd_span_mean"] = float(np.mean(spans))
