@@ -604,6 +604,13 @@ __global__ __launch_bounds__(64 * kPW) HB_DS_PROPOSE_ATTR void ds_propose(Dev D,
   propose_group<PREP>(D, W, NPAST, iter, sch_src, sch_dst, n8, S, j, act);
 }
 
+#ifdef HB_DS_CLOCKS
+// experiment builds only: per wave of the last ds_step launch: s_memtime and
+// s_memrealtime at entry, after the records barrier and at the end, the slot,
+// its temperature and e (read back by hb_debug_ds_clocks)
+constexpr int kDsClkWords = 9;
+__device__ unsigned long long ds_clk[kDsClkWords * 65536];
+#endif
 // The whole iteration up to the swaps in ONE launch (propose -> records ->
 // likelihood -> Hastings test), for a shard of at most one resident round
 // (nl <= 16 per CU) on the one-wave plan: each workgroup's four waves propose
@@ -623,6 +630,9 @@ __global__ __launch_bounds__(64 * kPW) __attribute__((amdgpu_waves_per_eu(4))) v
     unsigned long long* __restrict__ sch_dst, long long n8, hbk::WaveEvalArgs E, AccArgs A, int prio) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_all[];
   ProposeShared& S = *reinterpret_cast<ProposeShared*>(smem_all);
+#ifdef HB_DS_CLOCKS
+  const unsigned long long c0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
+#endif
   if (prio == 3) __builtin_amdgcn_s_setprio(3);
   else if (prio == 2) __builtin_amdgcn_s_setprio(2);
   else if (prio == 1) __builtin_amdgcn_s_setprio(1);
@@ -634,6 +644,9 @@ __global__ __launch_bounds__(64 * kPW) __attribute__((amdgpu_waves_per_eu(4))) v
   if (!act) return;
   const int jl = __builtin_amdgcn_readfirstlane(j - D.lo);
   const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+#ifdef HB_DS_CLOCKS
+  const unsigned long long c1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+#endif
   // the records just written: scalar loads (constant address space), issued
   // only after the barrier (the pointer passes through asm)
   typedef const __attribute__((address_space(4))) hbdev::WalkerConst cwc_t;
@@ -643,6 +656,16 @@ __global__ __launch_bounds__(64 * kPW) __attribute__((amdgpu_waves_per_eu(4))) v
   hbk::eval_wave_body<VPT, true, 1>(E.t, E.ph, E.f, E.isg, E.rows, E.n, E.kth, wcs[jl], jl, jl, D.logLy, nullptr, 0,
                                     E.slab_bytes, E.slab_bytes, E.gap, A, smem_all + (size_t)wv * (size_t)E.lds_per,
                                     E.dq);
+#ifdef HB_DS_CLOCKS
+  const unsigned long long c2 = __builtin_amdgcn_s_memtime(), r2 = __builtin_amdgcn_s_memrealtime();
+  if ((threadIdx.x & 63) == 0 && jl < 65536) {
+    unsigned long long* o = ds_clk + kDsClkWords * jl;
+    o[0] = c0; o[1] = c1; o[2] = c2; o[3] = r0; o[4] = r1; o[5] = r2;
+    o[6] = (unsigned long long)j;
+    o[7] = __double_as_longlong(D.temp[j]);
+    o[8] = __double_as_longlong(D.y[(size_t)jl * kNp + 3]);
+  }
+#endif
 }
 
 // Hastings test and history (:492-546); 64 slots per block (one lane each),
@@ -1842,6 +1865,13 @@ extern "C" int hb_dsampler_gather(hb_dsampler* d, double* x_slots, double* logl_
   return 0;
 }
 
+#ifdef HB_DS_CLOCKS
+extern "C" int hb_debug_ds_clocks(unsigned long long* out, int nslots) {
+  if (nslots > 65536) nslots = 65536;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(ds_clk), kDsClkWords * sizeof(unsigned long long) * nslots) == hipSuccess
+             ? 0 : -1;
+}
+#endif
 extern "C" int hb_dsampler_sync(hb_dsampler* d) {
   if (!d) return hbx_set_error("hb_dsampler_sync: null");
   DS_TRY(hipStreamSynchronize(d->st), "sync");
