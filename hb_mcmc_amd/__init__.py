@@ -7,8 +7,8 @@ heartbeat-binary light-curve log-likelihood path.
 * ``hb_mcmc_amd.pyHB``: drop-in for the reference Cython module ``pyHB``.
 * ``hb_mcmc_amd.sampler``: the parallel-tempered MCMC caller (mcmc_wrapper2.c).
 * ``hb_mcmc_amd.dist``: temperature slots sharded over GPUs with an RCCL all-gather.
-* ``hb_mcmc_amd.catalog``: catalog-sweep mode (many targets per GPU, one
-  batched launch per size class; targets dealt over GPUs).
+* ``hb_mcmc_amd.catalog``: catalog-sweep mode (many targets per GPU, every
+  size class in one eval launch; targets dealt over GPUs).
 
 Importing the package does not touch the GPU.
 """

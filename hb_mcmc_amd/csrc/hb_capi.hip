@@ -481,44 +481,35 @@ static int host_batch(hb_ctx* c, const double* params, int w, double* out, void*
 }
 
 // ---------------------------------------------------------------------------
-// catalog mode: many light curves, one batched launch per size class
+// catalog mode: many light curves, every size class in one eval launch
 //
-// A class is a power-of-two range of cadences per lane rc = ceil(N/64) (the
-// kernel's VPT).  The class launches go to kCatStreams streams (largest work
-// first) and join back into the caller's stream: the small classes run beside
-// the large ones' tails (C5: 0.322 -> 0.319 ms).  Finer classes (halves and
-// quarters of each range, for smaller LDS slabs) measured slower: 0.424 ms on
-// one stream, 0.322-0.341 on 2-4 (launch tails dominate).
+// A class is a power-of-two range of cadences per lane rc = ceil(N/64) up to
+// N = 1024 (the kernel's VPT, one wave per walker), and N > 1024 as a pair of
+// waves of <= 16 cadences per lane (128 lane rows: the catalog's rows arrays
+// use cat_nr).  One call = the records launch, then hb_eval_catalog_kernel
+// with the classes as segments of its grid, the pair class first and the
+// smallest last (hbk::CatSegs).  Replaced in round 5: one launch per class
+// dealt over two streams with fork/join events -- C5 0.150 ms per call, of
+// which 7-14 us went between the records launch and the first class launches
+// and the last 20 us to two small classes running alone
+// (profiles/r05/r05g_c5_timeline.json).
 // ---------------------------------------------------------------------------
-// class 6: N > 1280, a pair of waves per walker (hbk::wave_nr_for); its queue
-// and slab sizes are those of 32 cadences per lane of one wave
-static constexpr int kCatClasses = 7;
-static constexpr int kCatRcHi[kCatClasses] = {1, 2, 4, 8, 16, 32, 32};
-static constexpr int kCatStreams = 4;  // at most: the caller's + 3 forked
-static constexpr int kCatDefaultStreams = 2;
-// experiment knob (A/B only): HB_CAT_STREAMS = streams used (1..4)
-static int cat_env(const char* k, int def) {
-  const char* v = getenv(k);
-  return v ? atoi(v) : def;
-}
+static constexpr int kCatClasses = hbk::kCatSegs;
+static constexpr int kCatPair = kCatClasses - 1;  // N > 1024
+static constexpr int kCatRcHi[kCatClasses] = {1, 2, 4, 8, 16, 16};
+// lane rows of a catalog target's rows arrays
+static long cat_nr(long n) { return n > 1024 ? 128 : 64; }
 static int catalog_class_of(long n) {
-  if (hbk::wave_nr_for(n) == 128) return kCatClasses - 1;
+  if (n > 1024) return kCatPair;
   const int rc = (int)((n + 63) / 64);
-  for (int c = 0; c < kCatClasses; ++c)
+  for (int c = 0; c < kCatPair; ++c)
     if (rc <= kCatRcHi[c]) return c;
   return -1;
 }
-
-// the launch geometry of class cl: cadences per lane (the kernel's VPT) and
-// waves per walker
+// the class's cadences per lane (the kernel's VPT) and waves per walker
 static void catalog_class_geometry(int cl, int& vpt, int& wpw) {
-  vpt = 1;
-  while (vpt < kCatRcHi[cl]) vpt <<= 1;
-  wpw = 1;
-  if (cl == kCatClasses - 1) {  // a pair of waves of <= 16 cadences per lane
-    vpt = 16;
-    wpw = 2;
-  }
+  vpt = kCatRcHi[cl];
+  wpw = cl == kCatPair ? 2 : 1;
 }
 
 struct hb_catalog {
@@ -531,7 +522,9 @@ struct hb_catalog {
   double* d_s = nullptr;         // 1 / max(sigma, 1e-5)
   double2* d_ph = nullptr;       // per-target phase tables (concatenated like d_t)
   double* d_rows = nullptr;      // per-target lane-row t, f, 1/sigma (TargetDesc::roff)
-  int* d_w0 = nullptr;           // first walker of each target in the current layout, -1 if none
+  long ncad = 0;                 // cadences of all targets
+  int* d_cw0 = nullptr;          // per cadence: its target's first walker in the current layout, -1 if none
+  int* d_wf = nullptr;           // per walker: its target's first walker
   hbk::TargetDesc* d_tab = nullptr;
   // walker layout cache (walkers per target as last seen)
   std::vector<int> layout;
@@ -539,36 +532,24 @@ struct hb_catalog {
   int cap = 0;
   int* d_wt = nullptr;           // target of each walker
   int* d_list = nullptr;         // walkers grouped by size class
-  int class_off[kCatClasses + 1] = {0};  // class c: list[class_off[c] .. class_off[c+1])
-  size_t class_slab[kCatClasses] = {0};
-  long class_work[kCatClasses] = {0};    // walkers x cadences, for the launch order
-  hipStream_t aux[kCatStreams - 1] = {};
-  hipEvent_t ev_fork = nullptr;
-  hipEvent_t ev_join[kCatStreams - 1] = {};
+  hbk::CatSegs segs{};                   // the eval launch's grid segments (catalog_layout)
   WalkerConst* d_wc = nullptr;
   double* d_params = nullptr;    // host-API staging
   double* d_out = nullptr;
-  // the one-wave kernel's deferred cadence queues, one region per class (the
-  // classes run concurrently on the forked streams)
-  double* d_dq = nullptr;
+  // the deferred cadence queues, one region per class (CatSegs::dq)
+  unsigned char* d_dq = nullptr;
   size_t dq_bytes = 0;
-  size_t class_dq[kCatClasses] = {0};    // byte offset of class c's region
   std::mutex mu;
 };
 
 extern "C" void hb_catalog_destroy(hb_catalog* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
-  for (void* p : {(void*)c->d_t, (void*)c->d_f, (void*)c->d_s, (void*)c->d_ph, (void*)c->d_rows, (void*)c->d_w0,
+  for (void* p : {(void*)c->d_t, (void*)c->d_f, (void*)c->d_s, (void*)c->d_ph, (void*)c->d_rows, (void*)c->d_cw0,
                   (void*)c->d_tab,
-                  (void*)c->d_wt, (void*)c->d_list,
+                  (void*)c->d_wt, (void*)c->d_wf, (void*)c->d_list,
                   (void*)c->d_wc, (void*)c->d_params, (void*)c->d_out, (void*)c->d_dq})
     if (p) (void)hipFree(p);
-  for (int i = 0; i < kCatStreams - 1; ++i) {
-    if (c->aux[i]) (void)hipStreamDestroy(c->aux[i]);
-    if (c->ev_join[i]) (void)hipEventDestroy(c->ev_join[i]);
-  }
-  if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
   delete c;
 }
 
@@ -604,7 +585,7 @@ extern "C" hb_catalog* hb_catalog_create(int ntargets, const double* const* t, c
     memset(&d, 0, sizeof d);
     d.off = total;
     d.roff = rtotal;
-    rtotal += hbk::wave_rows_doubles(n[k]);
+    rtotal += hbk::wave_rows_doubles(n[k], cat_nr(n[k]));
     d.n = n[k];
     d.kth = (n[k] % 2 == 0) ? n[k] / 2 : n[k] / 2 + 1;  // likelihood3.c:97-99
     d.dist = mag5 ? mag5[5 * k + 0] : 1000.;             // mcmc_wrapper2.c:321-327 fallback
@@ -614,6 +595,7 @@ extern "C" hb_catalog* hb_catalog_create(int ntargets, const double* const* t, c
     c->cls[k] = catalog_class_of(n[k]);
     total += n[k];
   }
+  c->ncad = total;
   std::vector<double> ht((size_t)total), hf((size_t)total), hs((size_t)total);
   for (int k = 0; k < ntargets; ++k) {
     const long o = c->tab[k].off;
@@ -627,7 +609,7 @@ extern "C" hb_catalog* hb_catalog_create(int ntargets, const double* const* t, c
   std::vector<double> hr((size_t)rtotal);
   for (int k = 0; k < ntargets; ++k) {
     const long o = c->tab[k].off;
-    hbk::build_rows(&ht[o], &hf[o], &hs[o], n[k], &hr[(size_t)c->tab[k].roff]);
+    hbk::build_rows(&ht[o], &hf[o], &hs[o], n[k], &hr[(size_t)c->tab[k].roff], cat_nr(n[k]));
   }
   if (hipSetDevice(device) != hipSuccess) { set_err_msg("hb_catalog_create: hipSetDevice failed"); return nullptr; }
   const size_t b = sizeof(double) * (size_t)total;
@@ -638,19 +620,9 @@ extern "C" hb_catalog* hb_catalog_create(int ntargets, const double* const* t, c
   }
   if (hipMalloc(&c->d_t, b) != hipSuccess || hipMalloc(&c->d_f, b) != hipSuccess ||
       hipMalloc(&c->d_s, b) != hipSuccess || hipMalloc(&c->d_ph, 2 * b) != hipSuccess ||
-      hipMalloc(&c->d_w0, sizeof(int) * ntargets) != hipSuccess ||
+      hipMalloc(&c->d_cw0, sizeof(int) * (size_t)total) != hipSuccess ||
       hipMalloc(&c->d_tab, sizeof(hbk::TargetDesc) * ntargets) != hipSuccess) {
     set_err_msg("hb_catalog_create: hipMalloc failed");
-    return nullptr;
-  }
-  for (int i = 0; i < kCatStreams - 1; ++i)
-    if (hipStreamCreateWithFlags(&c->aux[i], hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreateWithFlags(&c->ev_join[i], hipEventDisableTiming) != hipSuccess) {
-      set_err_msg("hb_catalog_create: stream/event creation failed");
-      return nullptr;
-    }
-  if (hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess) {
-    set_err_msg("hb_catalog_create: event creation failed");
     return nullptr;
   }
   if (hipMemcpy(c->d_t, ht.data(), b, hipMemcpyHostToDevice) != hipSuccess ||
@@ -676,29 +648,48 @@ static int catalog_layout(hb_catalog* c, const int* walkers, hipStream_t s) {
     total += walkers[k];
   }
   if (total > (1 << 30)) return set_err_msg("hb_catalog: too many walkers");
-  std::vector<int> wt((size_t)total), list, w0(c->ntargets);
+  std::vector<int> wt((size_t)total), list, w0(c->ntargets), wf((size_t)total), cw0((size_t)c->ncad);
   list.reserve((size_t)total);
   long w = 0;
   for (int k = 0; k < c->ntargets; ++k) {
     w0[k] = walkers[k] > 0 ? (int)w : -1;
-    for (int i = 0; i < walkers[k]; ++i) wt[(size_t)w++] = k;
+    for (int i = 0; i < walkers[k]; ++i) {
+      wf[(size_t)w] = w0[k];
+      wt[(size_t)w++] = k;
+    }
+    std::fill(cw0.begin() + c->tab[k].off, cw0.begin() + c->tab[k].off + c->tab[k].n, w0[k]);
   }
-  for (int cl = 0; cl < kCatClasses; ++cl) {
-    c->class_off[cl] = (int)list.size();
-    long nmax = 0, work = 0;
-    w = 0;
-    // XCD-aware order: workgroup b of a launch runs on XCD b mod 8, so the
-    // class list puts all walkers of one target at positions of one residue
-    // mod 8 -- that target's light curve then fills one XCD's L2 instead of
-    // all eight.  Targets go to the least-loaded residue, largest work first;
-    // a residue whose queue runs dry takes from the longest one.
+  // grid order: the pair class first, then by descending cadences per lane
+  // (CatSegs); a class's first workgroup is known before its list is built
+  int counts[kCatClasses] = {0};
+  for (int k = 0; k < c->ntargets; ++k) counts[c->cls[k]] += walkers[k];
+  hbk::CatSegs sg{};
+  int blocks = 0;
+  for (int cl = kCatClasses - 1; cl >= 0; --cl) {
+    if (counts[cl] == 0) continue;
+    const int q = sg.nseg++;
+    catalog_class_geometry(cl, sg.vpt[q], sg.wpw[q]);
+    sg.first[q] = blocks;
+    sg.cnt[q] = counts[cl];
+    blocks += sg.wpw[q] == 2 ? counts[cl] : (counts[cl] + 1) / 2;
+    sg.first[q + 1] = blocks;
+  }
+  size_t qb = 0;
+  for (int q = 0, cl = kCatClasses - 1; cl >= 0; --cl) {
+    if (counts[cl] == 0) continue;
+    sg.off[q] = (int)list.size();
+    long nmax = 0;
+    // XCD-aware order: workgroup b runs on XCD b mod 8, so the class list puts
+    // all walkers of one target in workgroups of one residue mod 8 -- that
+    // target's light curve then fills one XCD's L2 instead of all eight.
+    // Targets go to the least-loaded residue, largest work first; a residue
+    // whose queue runs dry takes from the longest one.
     constexpr int kXcd = 8;
     std::vector<std::pair<long, int>> tw;  // (work, target)
     for (int k = 0; k < c->ntargets; ++k) {
-      if (c->cls[k] == cl) {
-        if (walkers[k] > 0 && c->tab[k].n > nmax) nmax = c->tab[k].n;
-        work += (long)walkers[k] * c->tab[k].n;
-        if (walkers[k] > 0) tw.push_back({(long)walkers[k] * c->tab[k].n, k});
+      if (c->cls[k] == cl && walkers[k] > 0) {
+        nmax = std::max(nmax, c->tab[k].n);
+        tw.push_back({(long)walkers[k] * c->tab[k].n, k});
       }
     }
     std::vector<long> first((size_t)c->ntargets + 1, 0);
@@ -706,39 +697,35 @@ static int catalog_layout(hb_catalog* c, const int* walkers, hipStream_t s) {
     std::stable_sort(tw.begin(), tw.end(), [](const std::pair<long, int>& a, const std::pair<long, int>& b) {
       return a.first > b.first;
     });
-    std::vector<std::vector<int>> q(kXcd);
+    std::vector<std::vector<int>> xq(kXcd);
     std::vector<long> load(kXcd, 0);
     for (const auto& e : tw) {
       const int x = (int)(std::min_element(load.begin(), load.end()) - load.begin());
       load[(size_t)x] += e.first;
-      for (int i = 0; i < walkers[e.second]; ++i) q[(size_t)x].push_back((int)(first[(size_t)e.second] + i));
+      for (int i = 0; i < walkers[e.second]; ++i) xq[(size_t)x].push_back((int)(first[(size_t)e.second] + i));
     }
     std::vector<size_t> head(kXcd, 0);
-    long left = 0;
-    for (int x = 0; x < kXcd; ++x) left += (long)q[(size_t)x].size();
-    for (long p = 0; p < left; ++p) {
-      int x = (int)(p % kXcd);
-      if (head[(size_t)x] == q[(size_t)x].size()) {  // dry: take from the longest remaining queue
+    for (long p = 0; p < counts[cl]; ++p) {
+      const long blk = sg.first[q] + (sg.wpw[q] == 2 ? p : p / 2);
+      int x = (int)(blk % kXcd);
+      if (head[(size_t)x] == xq[(size_t)x].size()) {  // dry: take from the longest remaining queue
         size_t best = 0;
         for (int y = 0; y < kXcd; ++y)
-          if (q[(size_t)y].size() - head[(size_t)y] > best) {
-            best = q[(size_t)y].size() - head[(size_t)y];
+          if (xq[(size_t)y].size() - head[(size_t)y] > best) {
+            best = xq[(size_t)y].size() - head[(size_t)y];
             x = y;
           }
       }
-      list.push_back(q[(size_t)x][head[(size_t)x]++]);
+      list.push_back(xq[(size_t)x][head[(size_t)x]++]);
     }
-    c->class_slab[cl] = hbk::wave_slab_bytes(nmax > 0 ? nmax : 2);
-    c->class_work[cl] = work;
+    const size_t slab = hbk::wave_slab_bytes(nmax, cat_nr(nmax));
+    sg.slab[q] = (int)slab;
+    sg.lds_per[q] = (int)hbk::wave_lds_bytes(slab, sg.vpt[q], sg.wpw[q]);
+    sg.dq[q] = (long long)qb;
+    qb += (hbk::wave_queue_bytes(sg.vpt[q], counts[cl], sg.wpw[q]) + 255) & ~(size_t)255;
+    ++q;
   }
-  c->class_off[kCatClasses] = (int)list.size();
-  size_t qb = 0;
-  for (int cl = 0; cl < kCatClasses; ++cl) {  // sized by the class's launch geometry
-    int vpt, wpw;
-    catalog_class_geometry(cl, vpt, wpw);
-    c->class_dq[cl] = qb;
-    qb += (hbk::wave_queue_bytes(vpt, c->class_off[cl + 1] - c->class_off[cl], wpw) + 255) & ~(size_t)255;
-  }
+  c->segs = sg;
   if (qb > c->dq_bytes) {
     if (c->d_dq) (void)hipFree(c->d_dq);
     c->d_dq = nullptr;
@@ -747,14 +734,16 @@ static int catalog_layout(hb_catalog* c, const int* walkers, hipStream_t s) {
     c->dq_bytes = qb;
   }
   if ((int)total > c->cap) {
-    for (void* p : {(void*)c->d_wt, (void*)c->d_list, (void*)c->d_wc, (void*)c->d_params, (void*)c->d_out})
+    for (void* p : {(void*)c->d_wt, (void*)c->d_wf, (void*)c->d_list, (void*)c->d_wc, (void*)c->d_params,
+                    (void*)c->d_out})
       if (p) (void)hipFree(p);
-    c->d_wt = c->d_list = nullptr;
+    c->d_wt = c->d_wf = c->d_list = nullptr;
     c->d_wc = nullptr;
     c->d_params = c->d_out = nullptr;
     c->cap = 0;
     const size_t nw = (size_t)total;
-    if (hipMalloc(&c->d_wt, sizeof(int) * nw) != hipSuccess || hipMalloc(&c->d_list, sizeof(int) * nw) != hipSuccess ||
+    if (hipMalloc(&c->d_wt, sizeof(int) * nw) != hipSuccess || hipMalloc(&c->d_wf, sizeof(int) * nw) != hipSuccess ||
+        hipMalloc(&c->d_list, sizeof(int) * nw) != hipSuccess ||
         hipMalloc(&c->d_wc, sizeof(WalkerConst) * nw) != hipSuccess ||
         hipMalloc(&c->d_params, sizeof(double) * 21 * nw) != hipSuccess ||
         hipMalloc(&c->d_out, sizeof(double) * nw) != hipSuccess)
@@ -762,7 +751,9 @@ static int catalog_layout(hb_catalog* c, const int* walkers, hipStream_t s) {
     c->cap = (int)total;
   }
   if (total > 0) {
-    HB_TRY(hipMemcpyAsync(c->d_w0, w0.data(), sizeof(int) * (size_t)c->ntargets, hipMemcpyHostToDevice, s),
+    HB_TRY(hipMemcpyAsync(c->d_cw0, cw0.data(), sizeof(int) * (size_t)c->ncad, hipMemcpyHostToDevice, s),
+           "upload first walkers");
+    HB_TRY(hipMemcpyAsync(c->d_wf, wf.data(), sizeof(int) * (size_t)total, hipMemcpyHostToDevice, s),
            "upload first walkers");
     HB_TRY(hipMemcpyAsync(c->d_wt, wt.data(), sizeof(int) * (size_t)total, hipMemcpyHostToDevice, s), "upload map");
     HB_TRY(hipMemcpyAsync(c->d_list, list.data(), sizeof(int) * (size_t)total, hipMemcpyHostToDevice, s),
@@ -775,52 +766,18 @@ static int catalog_layout(hb_catalog* c, const int* walkers, hipStream_t s) {
 }
 
 // One catalog call: one records launch for every walker (hb_prep_kernel over
-// the catalog's walkers, per-target phase tables in its tail), then every
-// size class's eval launch on its stream (forked at the call's start).
-// (Measured and removed in round 5: a records launch per class on the class's
-// stream, 0.197 vs 0.162 ms per C5 call; each one-wave class as ONE launch with
-// its walkers' records in the eval kernel's prologue, 0.204 vs 0.168 ms:
-// profiles/r04/r04f_bench_c5*.json, r04m_c5_*.json.)
+// the catalog's walkers, per-target phase tables in its tail), then the one
+// eval launch of every size class (hb_eval_catalog_kernel), both on the
+// caller's stream.
 static int catalog_run(hb_catalog* c, const double* d_params, double* d_logl, hipStream_t s) {
   if (c->total == 0) return 0;
   MagArgs unused{};
-  HB_TRY(hbk::launch_prep(d_params, c->total, unused, c->d_wc, s, c->d_tab, c->d_wt, c->d_t, 0, c->d_ph, c->d_w0,
-                          c->ntargets),
+  HB_TRY(hbk::launch_prep(d_params, c->total, unused, c->d_wc, s, c->d_tab, c->d_wt, c->d_t, c->ncad, c->d_ph,
+                          c->d_cw0, c->d_wf),
          "prep launch");
-  // classes by descending work, dealt round-robin over the caller's stream
-  // and the forked ones.  (Longest-processing-time dealing -- each class to
-  // the stream with the least work so far -- measured slower: C5 162-164 vs
-  // 152-154 us per call, profiles/r05/r05c_c5_ab.txt: it leaves the
-  // LDS-limited 32-cadences-per-lane class running alone at the end.)
-  int order[kCatClasses], nc = 0;
-  for (int cl = 0; cl < kCatClasses; ++cl)
-    if (c->class_off[cl + 1] > c->class_off[cl]) order[nc++] = cl;
-  std::sort(order, order + nc, [&](int a, int b) { return c->class_work[a] > c->class_work[b]; });
-  // two streams: C5 0.164 ms per call against 0.183 on four and 0.196 on one
-  // (profiles/r04/r04c_bench_c5_s*.json, two-launch path: the forked streams'
-  // event waits cost more than the extra overlap buys)
-  static const int kns = std::max(1, std::min(kCatStreams, cat_env("HB_CAT_STREAMS", kCatDefaultStreams)));
-  const int ns = nc < kns ? nc : kns;
-  if (ns > 1) {
-    HB_TRY(hipEventRecord(c->ev_fork, s), "fork event");
-    for (int i = 0; i < ns - 1; ++i) HB_TRY(hipStreamWaitEvent(c->aux[i], c->ev_fork, 0), "fork wait");
-  }
-  for (int j = 0; j < nc; ++j) {
-    const int cl = order[j];
-    const int cnt = c->class_off[cl + 1] - c->class_off[cl];
-    int vpt, wpw;
-    catalog_class_geometry(cl, vpt, wpw);
-    hipStream_t sj = (j % ns == 0) ? s : c->aux[j % ns - 1];
-    const int* lst = c->d_list + c->class_off[cl];
-    double* dq = reinterpret_cast<double*>(reinterpret_cast<unsigned char*>(c->d_dq) + c->class_dq[cl]);
-    HB_TRY(hbk::launch_eval_multi(vpt, c->class_slab[cl], c->d_t, c->d_ph, c->d_f, c->d_s, c->d_rows, c->d_tab,
-                                  c->d_wt, lst, cnt, c->d_wc, d_logl, sj, dq, wpw),
-           "eval launch");
-  }
-  for (int i = 0; i < ns - 1; ++i) {
-    HB_TRY(hipEventRecord(c->ev_join[i], c->aux[i]), "join event");
-    HB_TRY(hipStreamWaitEvent(s, c->ev_join[i], 0), "join wait");
-  }
+  HB_TRY(hbk::launch_eval_catalog(c->segs, c->d_t, c->d_ph, c->d_f, c->d_s, c->d_rows, c->d_tab, c->d_wt, c->d_list,
+                                  c->d_wc, d_logl, c->d_dq, s),
+         "eval launch");
   return 0;
 }
 

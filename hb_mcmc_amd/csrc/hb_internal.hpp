@@ -89,19 +89,35 @@ double cadence_gap(const double* t, long n);
 hipError_t preload_code_object();
 // ph (optional): the shared-period phase table of the batch, (sin, cos)(t_i
 // DAY 2pi/P) for P = the period of the light curve's first walker (walker 0,
-// or catalog target k's w0[k]), written here and read by the eval launch;
-// walkers with another period get tab = 0
+// or in catalog mode the first walker of cadence i's target, cw0[i]; wf: each
+// walker's target's first walker), written here and read by the eval launch;
+// walkers with another period get tab = 0.  Catalog mode: n = all cadences.
 hipError_t launch_prep(const double* d_params, int nwalk, const MagArgs& ma, hbdev::WalkerConst* d_wc,
                        hipStream_t s, const TargetDesc* tab = nullptr, const int* wt = nullptr,
-                       const double* t = nullptr, long n = 0, double2* ph = nullptr, const int* w0 = nullptr,
-                       int ntargets = 0, double* tab_pc = nullptr);
-// catalog mode: walkers list[0..count) of one size class (cadences per lane
-// vpt), each reading its target's slice through tab[wt[walker]]
-// (wpw = 2: a pair of waves per walker, vpt the cadences per lane of 128 rows)
-hipError_t launch_eval_multi(int vpt, size_t slab_bytes, const double* t, const double2* ph, const double* f,
-                             const double* sg, const double* rows,
-                             const TargetDesc* tab, const int* wt, const int* list, int count,
-                             const hbdev::WalkerConst* wc, double* logl, hipStream_t s, double* dq, int wpw = 1);
+                       const double* t = nullptr, long n = 0, double2* ph = nullptr, const int* cw0 = nullptr,
+                       const int* wf = nullptr, double* tab_pc = nullptr);
+// Catalog mode: ONE eval launch for every size class of the call.  Segment s
+// of the grid (workgroups first[s] .. first[s+1]) evaluates the walkers
+// list[off[s] .. off[s] + cnt[s]), each reading its target's slice through
+// tab[wt[walker]]: wpw 1 -- two walkers per 128-thread workgroup, a wave each,
+// vpt cadences per lane (64 lane rows); wpw 2 -- one walker per workgroup, a
+// pair of waves of 16 cadences per lane (128 lane rows, N > 1024).
+constexpr int kCatSegs = 6;
+struct CatSegs {
+  int nseg;
+  int first[kCatSegs + 1];
+  int vpt[kCatSegs];
+  int wpw[kCatSegs];
+  int off[kCatSegs];
+  int cnt[kCatSegs];
+  int slab[kCatSegs];     // slab bytes per walker
+  int lds_per[kCatSegs];  // LDS bytes per walker (a wave's slice, or the pair's)
+  long long dq[kCatSegs]; // byte offset of the segment's deferred queues in the dq buffer
+};
+hipError_t launch_eval_catalog(const CatSegs& sg, const double* t, const double2* ph, const double* f,
+                               const double* isg, const double* rows, const TargetDesc* tab, const int* wt,
+                               const int* list, const hbdev::WalkerConst* wc, double* logl, unsigned char* dq,
+                               hipStream_t s);
 // The fused launch: per-walker records (hb_prep.hpp) in the prologue of the
 // one-wave eval kernel, WPB walkers per workgroup (hb_kernels.hip
 // launch_eval_fused); the records and the shared-period phase table are also
@@ -138,11 +154,11 @@ int wave_nr_for(long n);   // lane rows per walker: 64, 128 (a pair of waves, 12
 // device bytes of the one-wave kernel's deferred cadence queue for `count`
 // walkers at `vpt` cadences per lane (the dq argument of launch_eval*)
 size_t wave_queue_bytes(int vpt, long count, int wpw = 1);
-size_t wave_slab_bytes(long n);
+size_t wave_slab_bytes(long n, long nr = 0);  // nr: lane rows (0: wave_nr_for(n))
 size_t wave_lds_bytes(size_t slab, int vpt, int wpw = 1);
 // t, f, 1/sigma in the one-wave kernel's lane-row order (3 x nr x ceil(n/nr) doubles)
-long wave_rows_doubles(long n);
-void build_rows(const double* t, const double* f, const double* isg, long n, double* out);
+long wave_rows_doubles(long n, long nr = 0);
+void build_rows(const double* t, const double* f, const double* isg, long n, double* out, long nr = 0);
 // acc (device sampler, one-wave path only): each wave also runs its slot's
 // Hastings test and history write (hb_accept.hpp); hipErrorNotSupported on the
 // multi-wave path

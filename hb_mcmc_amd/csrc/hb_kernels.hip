@@ -114,7 +114,8 @@ __global__ __launch_bounds__(kPrepThreads) void hb_prep_kernel(const double* __r
                                                               const int* __restrict__ wt,
                                                               const double* __restrict__ tcad, int ncad,
                                                               double2* __restrict__ ph,
-                                                              const int* __restrict__ w0, int ntargets,
+                                                              const int* __restrict__ cw0,
+                                                              const int* __restrict__ wf,
                                                               double* __restrict__ tab_pc_out) {
   constexpr int kPrepWalkers = NW;
   __shared__ PrepShared<kPrepWalkers> L;
@@ -132,6 +133,16 @@ __global__ __launch_bounds__(kPrepThreads) void hb_prep_kernel(const double* __r
     if (i0 < ncad) t_first = tcad[i0];
     lp0 = params[2];
   }
+  // catalog phase tables: cadence ic of the concatenated arrays (grid-wide,
+  // one or two per thread), its time and its target's first walker in flight now
+  const bool cattab = ph != nullptr && tab != nullptr;
+  const int ic = blockIdx.x * kPrepThreads + tid;
+  int cw_first = -1;
+  double tc_first = 0.0;
+  if (cattab && ic < ncad) {
+    cw_first = cw0[ic];
+    tc_first = tcad[ic];
+  }
   {  // all loads in flight before the first LDS write (a rolled loop serialises on vmcnt(0))
     constexpr int U = (kPrepWalkers * kNpars + kPrepThreads - 1) / kPrepThreads;
     double v[U];
@@ -147,11 +158,12 @@ __global__ __launch_bounds__(kPrepThreads) void hb_prep_kernel(const double* __r
     }
   }
   __syncthreads();
+  const double lpc_first = cw_first >= 0 ? params[(size_t)cw_first * kNpars + 2] : 0.0;
   // the table period: walker 0's (single context) or the first walker's of
   // the walker's target in this batch (catalog)
   auto tab_pc = [&](int j) -> double {
     if (ph == nullptr) return __builtin_nan("");
-    return exp10(params[(tab ? (size_t)w0[wt[base + j]] * kNpars : 0) + 2]) * kDay;
+    return exp10(params[(tab ? (size_t)wf[base + j] * kNpars : 0) + 2]) * kDay;
   };
   // ph[i] = (sin, cos)(t_i DAY 2pi/Pc0) for the period of walker 0, entries
   // dealt round-robin over the workgroups' wave-2 lanes
@@ -185,21 +197,23 @@ __global__ __launch_bounds__(kPrepThreads) void hb_prep_kernel(const double* __r
       if (i < nb * kWcDoubles) dst[i] = v[u];
     }
   }
-  // Catalog phase table (WalkerConst::tab), written after the walker records
-  // so its latency overlaps their stores: per target k, for the period of its
-  // first walker w0[k] in this batch (-1: no walkers), ph[i] = (sin, cos)(t_i
-  // DAY 2pi/Pc0) over its slice of the concatenated arrays.  (A single
+  // Catalog phase tables (WalkerConst::tab), written after the walker records
+  // so their latency overlaps the stores: cadence i of target k, for the
+  // period of k's first walker cw0[i] in this batch (-1: no walkers), ph[i] =
+  // (sin, cos)(t_i DAY 2pi/Pc0).  Spread over the whole grid, operands loaded
+  // at entry: one per thread at C5 (a target per workgroup, up to 8 cadences
+  // per thread in turn, measured 12.2 us per records launch).  (A single
   // context's table is written by wave 2 above.)
-  if (ph && tab != nullptr) {
-    for (int k = blockIdx.x; k < ntargets; k += G) {
-      if (w0[k] < 0) continue;
-      const double mA0 = kTwoPi / (exp10(params[(size_t)w0[k] * kNpars + 2]) * kDay);
-      const long off = tab[k].off;
-      for (int i = tid; i < (int)tab[k].n; i += blockDim.x) {
-        double sv, cv;
-        sincos_table((tcad[off + i] * kDay) * mA0, sv, cv);
-        ph[off + i] = make_double2(sv, cv);
-      }
+  if (cattab) {
+    const int gs = G * kPrepThreads;
+    for (int i = ic; i < ncad; i += gs) {
+      const bool fst = i == ic;
+      const int cw = fst ? cw_first : cw0[i];
+      if (cw < 0) continue;
+      const double mA0 = kTwoPi / (exp10(fst ? lpc_first : params[(size_t)cw * kNpars + 2]) * kDay);
+      double sv, cv;
+      sincos_table(((fst ? tc_first : tcad[i]) * kDay) * mA0, sv, cv);
+      ph[i] = make_double2(sv, cv);
     }
   }
 }
@@ -564,8 +578,6 @@ __device__ __forceinline__ void fused_prologue(const PreArgs& pa, int count, int
 // One wave per walker (WPB walkers per workgroup, one wave each; a wave's LDS
 // is its lds_per-byte slice; the waves of a workgroup meet only in the fused
 // prologue, everything else syncs per wave: HB_WSYNC).
-// MULTI (catalog mode): the walker is list[slot] and its light curve is its
-// target's slice (tab[wt[walker]]); n and kth come from the descriptor.
 // ACC (device sampler): the wave then runs the Hastings test and history write
 // of its slot (hb_accept.hpp) on the logL it just computed, in place of a
 // separate ds_accept launch; its operands are loaded when the wave starts.
@@ -574,16 +586,15 @@ __device__ __forceinline__ void fused_prologue(const PreArgs& pa, int count, int
 // the cadences per lane of the walker's rows (<= 16).
 // PRE: the fused launch (fused_prologue above): WPB walkers per workgroup, the
 // records computed in the prologue, the phase table read from LDS.
-template <int VPT, bool MULTI, bool ACC = false, int WPB = 1, int WPW = 1, bool PRE = false>
+template <int VPT, bool ACC = false, int WPB = 1, int WPW = 1, bool PRE = false>
 __global__ __launch_bounds__(64 * WPB * WPW) HB_WPE_ATTR void hb_eval_wave_kernel(
     const double* __restrict__ t, const double2* __restrict__ ph, const double* __restrict__ f,
     const double* __restrict__ isg, const double* __restrict__ rows,
     long n, long kth, const WalkerConst* __restrict__ wcs, double* __restrict__ logl,
-    double* __restrict__ tmpl_out, int mode, int slab_bytes, double gap, const TargetDesc* __restrict__ tab,
-    const int* __restrict__ wt, const int* __restrict__ list, hbds::AccArgs hst, int count, int lds_per,
+    double* __restrict__ tmpl_out, int mode, int slab_bytes, double gap, hbds::AccArgs hst, int count, int lds_per,
     double* __restrict__ dqbuf, PreArgs pre) {
   static_assert(WPW == 1 || (WPW <= kMaxWPW && WPB == 1 && !ACC), "pair/rows: plain batched path");
-  static_assert(!PRE || (WPW == 1 && !ACC && !MULTI && WPB >= kPrepRoles), "fused launch: plain one-wave batched path");
+  static_assert(!PRE || (WPW == 1 && !ACC && WPB >= kPrepRoles), "fused launch: plain one-wave batched path");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_all[];
   const int lane = threadIdx.x & 63;
   const int wib = WPB > 1 ? __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) : 0;
@@ -603,24 +614,62 @@ __global__ __launch_bounds__(64 * WPB * WPW) HB_WPE_ATTR void hb_eval_wave_kerne
   }
   int wv = slot;
   if (ACC && hst.ecnt != nullptr && valid) wv = hbds::eval_slot_by_e(hst, slot, lane);  // device sampler
-  if (MULTI && valid) {
-    wv = list[slot];
-    const TargetDesc& td = tab[wt[wv]];
-    t += td.off;
-    if (ph) ph += td.off;
-    f += td.off;
-    isg += td.off;
-    rows += td.roff;
-    n = td.n;
-    kth = td.kth;
-    gap = td.gap;
-  }
   if (!valid) return;
   // the select's survivors: past the slab, or (fused launch) inside it, past
   // the histogram (the slab is dead once the keys are in registers)
   const int cand_off = PRE && slab_bytes >= kCandInSlab ? (4 << kSelBits) : slab_bytes;
   eval_wave_body<VPT, ACC, WPW>(t, ph, f, isg, rows, n, kth, wcs[wv], wv, slot, logl, tmpl_out, mode, slab_bytes,
                                 cand_off, gap, hst, smem, dqbuf);
+}
+
+// ---------------------------------------------------------------------------
+// The catalog's eval launch (CatSegs, hb_internal.hpp): every size class in
+// one grid, largest walkers first.  Workgroups start in grid order as earlier
+// ones retire, so the short walkers of the later segments fill the SIMDs the
+// long ones leave idle while they drain -- no per-class launches, no streams
+// or events between them.  128 threads per workgroup in every segment (two
+// one-wave walkers, or a pair of waves for one walker), so the launch's one
+// LDS size fits eight workgroups, four waves per SIMD, on a CU.
+// ---------------------------------------------------------------------------
+template <int VPT, int WPW>
+__device__ __forceinline__ void cat_walker(const double* __restrict__ t, const double2* __restrict__ ph,
+                                           const double* __restrict__ f, const double* __restrict__ isg,
+                                           const double* __restrict__ rows, const TargetDesc& td,
+                                           const WalkerConst& w, int wv, int pos, double* __restrict__ logl,
+                                           int slab, unsigned char* smem, double* dq) {
+  eval_wave_body<VPT, false, WPW>(t + td.off, ph + td.off, f + td.off, isg + td.off, rows + td.roff, td.n, td.kth, w,
+                                  wv, pos, logl, nullptr, 0, slab, slab, td.gap, hbds::AccArgs{}, smem, dq);
+}
+__global__ __launch_bounds__(128) HB_WPE_ATTR void hb_eval_catalog_kernel(
+    const double* __restrict__ t, const double2* __restrict__ ph, const double* __restrict__ f,
+    const double* __restrict__ isg, const double* __restrict__ rows, const TargetDesc* __restrict__ tab,
+    const int* __restrict__ wt, const int* __restrict__ list, const WalkerConst* __restrict__ wcs,
+    double* __restrict__ logl, unsigned char* __restrict__ dqb, CatSegs sg) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_all[];
+  const int b = (int)blockIdx.x;
+  int s = 0;
+#pragma unroll
+  for (int q = 1; q < kCatSegs; ++q) s += (q < sg.nseg && b >= sg.first[q]) ? 1 : 0;
+  const int h = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int wpw = sg.wpw[s];
+  const int pos = wpw == 2 ? b - sg.first[s] : 2 * (b - sg.first[s]) + h;
+  if (pos >= sg.cnt[s]) return;  // the last one-wave workgroup's second wave (a pair: both waves)
+  const int wv = list[sg.off[s] + pos];
+  const TargetDesc& td = tab[wt[wv]];
+  unsigned char* smem = smem_all + (wpw == 2 ? 0 : h * sg.lds_per[s]);
+  double* dq = reinterpret_cast<double*>(dqb + sg.dq[s]);
+  const int slab = sg.slab[s];
+  if (wpw == 2) {
+    cat_walker<16, 2>(t, ph, f, isg, rows, td, wcs[wv], wv, pos, logl, slab, smem, dq);
+    return;
+  }
+  switch (sg.vpt[s]) {
+    case 16: cat_walker<16, 1>(t, ph, f, isg, rows, td, wcs[wv], wv, pos, logl, slab, smem, dq); break;
+    case 8: cat_walker<8, 1>(t, ph, f, isg, rows, td, wcs[wv], wv, pos, logl, slab, smem, dq); break;
+    case 4: cat_walker<4, 1>(t, ph, f, isg, rows, td, wcs[wv], wv, pos, logl, slab, smem, dq); break;
+    case 2: cat_walker<2, 1>(t, ph, f, isg, rows, td, wcs[wv], wv, pos, logl, slab, smem, dq); break;
+    default: cat_walker<1, 1>(t, ph, f, isg, rows, td, wcs[wv], wv, pos, logl, slab, smem, dq); break;
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -973,9 +1022,9 @@ __global__ __launch_bounds__(1024) void hb_sort_step_kernel(uint64_t* __restrict
 // ---------------------------------------------------------------------------
 hipError_t launch_prep(const double* d_params, int nwalk, const MagArgs& ma, WalkerConst* d_wc,
                        hipStream_t s, const TargetDesc* tab, const int* wt, const double* t, long n,
-                       double2* ph, const int* w0, int ntargets, double* tab_pc) {
+                       double2* ph, const int* cw0, const int* wf, double* tab_pc) {
   if (nwalk <= 0) return hipSuccess;
-  if (t == nullptr || (tab != nullptr && w0 == nullptr)) ph = nullptr;
+  if (t == nullptr || (tab != nullptr && (cw0 == nullptr || wf == nullptr))) ph = nullptr;
   // the most walkers per workgroup that still leave >= 256 workgroups (one per CU),
   // at most 32: both stars' lane tasks then fit one pass (prep_records); 64
   // walkers (two passes) measured 0.1648 vs 0.1640 ms per C5 call
@@ -985,7 +1034,7 @@ hipError_t launch_prep(const double* d_params, int nwalk, const MagArgs& ma, Wal
   const int nb = (nwalk + nw - 1) / nw;
   auto kern = nw == 64 ? hb_prep_kernel<64> : nw == 32 ? hb_prep_kernel<32> : hb_prep_kernel<kPrepWalkers>;
   hipLaunchKernelGGL(kern, dim3(nb), dim3(kPrepThreads), 0, s, d_params, nwalk, ma, d_wc, tab, wt, t,
-                     (int)n, ph, w0, ntargets, tab_pc);
+                     (int)n, ph, cw0, wf, tab_pc);
   return hipGetLastError();
 }
 
@@ -1027,13 +1076,12 @@ static hipError_t launch_eval_t(const EvalPlan& pl, const double* t, const doubl
 
 constexpr size_t kLdsCap = 163840;
 
-template <int VPT, bool MULTI, bool ACC, int WPB, int WPW = 1, bool PRE = false>
+template <int VPT, bool ACC, int WPB, int WPW = 1, bool PRE = false>
 static hipError_t launch_wave_g(size_t lds_per, int count, hipStream_t s, const double* t, const double2* ph,
                                 const double* f, const double* sg, const double* rows, long n, long kth, const WalkerConst* wc,
                                 double* logl, double* tmpl, int mode, size_t slab, double gap,
-                                const TargetDesc* tab, const int* wt, const int* list,
                                 const hbds::AccArgs& acc, double* dq, const PreArgs* pre = nullptr) {
-  auto kern = hb_eval_wave_kernel<VPT, MULTI, ACC, WPB, WPW, PRE>;
+  auto kern = hb_eval_wave_kernel<VPT, ACC, WPB, WPW, PRE>;
   // PRE: the slices, then the LDS phase table (16 B per cadence)
   const size_t lds = (size_t)WPB * lds_per + (PRE ? (((size_t)n * 16 + 15) & ~(size_t)15) : 0);
   if (lds > kLdsCap) return hipErrorInvalidValue;
@@ -1045,7 +1093,7 @@ static hipError_t launch_wave_g(size_t lds_per, int count, hipStream_t s, const 
     attr_set = true;
   }
   hipLaunchKernelGGL(kern, dim3((count + WPB - 1) / WPB), dim3(64 * WPB * WPW), lds, s, t, ph, f, sg, rows, n, kth, wc, logl,
-                     tmpl, mode, (int)slab, gap, tab, wt, list, acc, count, (int)lds_per, dq, pre ? *pre : PreArgs{});
+                     tmpl, mode, (int)slab, gap, acc, count, (int)lds_per, dq, pre ? *pre : PreArgs{});
   return hipGetLastError();
 }
 
@@ -1094,9 +1142,8 @@ static hipError_t launch_fused_t(const EvalPlan& pl, int wpb, const PreArgs& pa,
   const hbds::AccArgs none{};
 #define HB_FCASE(WV)                                                                                               \
   if (wpb == WV)                                                                                                   \
-    return launch_wave_g<VPT, false, false, WV, 1, true>(per, nwalk, s, t, pa.ph, f, sg, rows, pl.n, pl.kth, pa.wc, \
-                                                         logl, nullptr, 0, pl.slab_bytes, pl.gap, nullptr, nullptr,  \
-                                                         nullptr, none, dq, &pa);
+    return launch_wave_g<VPT, false, WV, 1, true>(per, nwalk, s, t, pa.ph, f, sg, rows, pl.n, pl.kth, pa.wc, logl, \
+                                                  nullptr, 0, pl.slab_bytes, pl.gap, none, dq, &pa);
   HB_FCASE(16)
   HB_FCASE(8)
   HB_FCASE(4)
@@ -1119,14 +1166,13 @@ hipError_t launch_eval_fused(const EvalPlan& pl, int wpb, const PreArgs& pa, con
 }
 
 // one walker per workgroup (WPW waves)
-template <int VPT, bool MULTI, bool ACC, int WPW = 1>
+template <int VPT, bool ACC, int WPW = 1>
 static hipError_t launch_wave_w(size_t slab, int count, hipStream_t s, const double* t, const double2* ph,
                                 const double* f, const double* sg, const double* rows, long n, long kth, const WalkerConst* wc,
-                                double* logl, double* tmpl, int mode, double gap, const TargetDesc* tab,
-                                const int* wt, const int* list, const hbds::AccArgs& acc, double* dq) {
+                                double* logl, double* tmpl, int mode, double gap, const hbds::AccArgs& acc, double* dq) {
   const size_t per = wave_lds_bytes(slab, VPT, WPW);
-  return launch_wave_g<VPT, MULTI, ACC, 1, WPW>(per, count, s, t, ph, f, sg, rows, n, kth, wc, logl, tmpl, mode, slab,
-                                                gap, tab, wt, list, acc, dq);
+  return launch_wave_g<VPT, ACC, 1, WPW>(per, count, s, t, ph, f, sg, rows, n, kth, wc, logl, tmpl, mode, slab, gap, acc,
+                                         dq);
 }
 
 template <int VPT>
@@ -1136,8 +1182,8 @@ static hipError_t launch_wave_t(const EvalPlan& pl, const double* t, const doubl
                                 hipStream_t s, double* dq) {
 #define HB_WPW_CASE(WV)                                                                                      \
   if (pl.wpw == WV)                                                                                          \
-    return launch_wave_w<VPT, false, false, WV>(pl.slab_bytes, nwalk, s, t, ph, f, sg, rows, pl.n, pl.kth, wc, logl, \
-                                                tmpl, mode, pl.gap, nullptr, nullptr, nullptr, hbds::AccArgs{}, dq);
+    return launch_wave_w<VPT, false, WV>(pl.slab_bytes, nwalk, s, t, ph, f, sg, rows, pl.n, pl.kth, wc, logl, tmpl, \
+                                         mode, pl.gap, hbds::AccArgs{}, dq);
   if constexpr (VPT == 16 || VPT == 8) {
     HB_WPW_CASE(2)
   }
@@ -1146,46 +1192,46 @@ static hipError_t launch_wave_t(const EvalPlan& pl, const double* t, const doubl
   }
 #undef HB_WPW_CASE
   if (pl.wpw != 1) return hipErrorInvalidValue;
-  return launch_wave_w<VPT, false, false>(pl.slab_bytes, nwalk, s, t, ph, f, sg, rows, pl.n, pl.kth, wc, logl, tmpl,
-                                          mode, pl.gap, nullptr, nullptr, nullptr, hbds::AccArgs{}, dq);
+  return launch_wave_w<VPT, false>(pl.slab_bytes, nwalk, s, t, ph, f, sg, rows, pl.n, pl.kth, wc, logl, tmpl, mode,
+                                   pl.gap, hbds::AccArgs{}, dq);
 }
 
 template <int VPT>
 static hipError_t launch_wave_acc_t(const EvalPlan& pl, const double* t, const double2* ph, const double* f,
                                     const double* sg, const double* rows, const WalkerConst* wc, int nwalk,
                                     double* logl, hipStream_t s, const hbds::AccArgs& acc, double* dq) {
-  return launch_wave_w<VPT, false, true>(pl.slab_bytes, nwalk, s, t, ph, f, sg, rows, pl.n, pl.kth, wc, logl, nullptr,
-                                         0, pl.gap, nullptr, nullptr, nullptr, acc, dq);
+  return launch_wave_w<VPT, true>(pl.slab_bytes, nwalk, s, t, ph, f, sg, rows, pl.n, pl.kth, wc, logl, nullptr, 0,
+                                  pl.gap, acc, dq);
 }
 
-template <int VPT>
-static hipError_t launch_multi_t(size_t slab, const double* t, const double2* ph, const double* f,
-                                 const double* sg, const double* rows,
-                                 const TargetDesc* tab, const int* wt, const int* list, int count,
-                                 const WalkerConst* wc, double* logl, hipStream_t s, double* dq, int wpw) {
-  if constexpr (VPT == 16 || VPT == 8)
-    if (wpw == 2)
-      return launch_wave_w<VPT, true, false, 2>(slab, count, s, t, ph, f, sg, rows, 0L, 0L, wc, logl, nullptr, 0, 0.0,
-                                                tab, wt, list, hbds::AccArgs{}, dq);
-  if (wpw != 1) return hipErrorInvalidValue;
-  return launch_wave_w<VPT, true, false>(slab, count, s, t, ph, f, sg, rows, 0L, 0L, wc, logl, nullptr, 0, 0.0, tab, wt,
-                                         list, hbds::AccArgs{}, dq);
-}
-
-hipError_t launch_eval_multi(int vpt, size_t slab, const double* t, const double2* ph, const double* f,
-                             const double* sg, const double* rows,
-                             const TargetDesc* tab, const int* wt, const int* list, int count,
-                             const WalkerConst* wc, double* logl, hipStream_t s, double* dq, int wpw) {
-  if (count <= 0) return hipSuccess;
-  switch (vpt) {
-    case 1: return launch_multi_t<1>(slab, t, ph, f, sg, rows, tab, wt, list, count, wc, logl, s, dq, wpw);
-    case 2: return launch_multi_t<2>(slab, t, ph, f, sg, rows, tab, wt, list, count, wc, logl, s, dq, wpw);
-    case 4: return launch_multi_t<4>(slab, t, ph, f, sg, rows, tab, wt, list, count, wc, logl, s, dq, wpw);
-    case 8: return launch_multi_t<8>(slab, t, ph, f, sg, rows, tab, wt, list, count, wc, logl, s, dq, wpw);
-    case 16: return launch_multi_t<16>(slab, t, ph, f, sg, rows, tab, wt, list, count, wc, logl, s, dq, wpw);
-    case 32: return launch_multi_t<32>(slab, t, ph, f, sg, rows, tab, wt, list, count, wc, logl, s, dq, wpw);
-    default: return hipErrorInvalidValue;
+hipError_t launch_eval_catalog(const CatSegs& sg, const double* t, const double2* ph, const double* f,
+                               const double* isg, const double* rows, const TargetDesc* tab, const int* wt,
+                               const int* list, const WalkerConst* wc, double* logl, unsigned char* dq,
+                               hipStream_t s) {
+  if (sg.nseg <= 0 || sg.nseg > kCatSegs) return sg.nseg == 0 ? hipSuccess : hipErrorInvalidValue;
+  size_t lds = 0;
+  for (int q = 0; q < sg.nseg; ++q) {
+    const bool ok1 = sg.wpw[q] == 1 && (sg.vpt[q] == 1 || sg.vpt[q] == 2 || sg.vpt[q] == 4 || sg.vpt[q] == 8 ||
+                                        sg.vpt[q] == 16);
+    const bool ok2 = sg.wpw[q] == 2 && sg.vpt[q] == 16;
+    if (!(ok1 || ok2) || sg.first[q + 1] < sg.first[q] || sg.cnt[q] < 0) return hipErrorInvalidValue;
+    if ((long)sg.first[q + 1] - sg.first[q] != (sg.wpw[q] == 2 ? (long)sg.cnt[q] : ((long)sg.cnt[q] + 1) / 2))
+      return hipErrorInvalidValue;
+    if ((size_t)sg.lds_per[q] < wave_lds_bytes((size_t)sg.slab[q], sg.vpt[q], sg.wpw[q])) return hipErrorInvalidValue;
+    lds = std::max(lds, (size_t)sg.lds_per[q] * (sg.wpw[q] == 2 ? 1 : 2));
   }
+  if (sg.first[0] != 0 || sg.first[sg.nseg] <= 0) return sg.first[sg.nseg] == 0 ? hipSuccess : hipErrorInvalidValue;
+  if (lds > kLdsCap) return hipErrorInvalidValue;
+  static bool attr_set = false;  // benign race (idempotent)
+  if (!attr_set && lds > 65536) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&hb_eval_catalog_kernel),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsCap);
+    if (e != hipSuccess) return e;
+    attr_set = true;
+  }
+  hipLaunchKernelGGL(hb_eval_catalog_kernel, dim3(sg.first[sg.nseg]), dim3(128), lds, s, t, ph, f, isg, rows, tab, wt,
+                     list, wc, logl, dq, sg);
+  return hipGetLastError();
 }
 
 hipError_t launch_eval(const EvalPlan& pl, const double* t, const double2* ph, const double* f, const double* sg,
@@ -1327,8 +1373,8 @@ int wave_vpt_for(long n) {
 
 // the template slab (nr lane rows of VPT doubles) doubles as the
 // 2^kSelBits-bin histogram of the select
-size_t wave_slab_bytes(long n) {
-  const long nr = wave_nr_for(n);
+size_t wave_slab_bytes(long n, long nr) {
+  if (nr <= 0) nr = wave_nr_for(n);
   const int rc = (int)((n + nr - 1) / nr);
   const long live = (n + rc - 1) / rc;
   int stride = rows_stride(rc);
@@ -1355,12 +1401,12 @@ size_t wave_lds_bytes(size_t slab, int vpt, int wpw) {
 // t, f and 1/sigma in the one-wave kernel's lane-row order: row block c holds
 // cadence l * rc + c for lane rows l = 0..nr-1 (nr = wave_nr_for(n), rc =
 // ceil(n / nr); cadences past the end repeat the last one and are never used)
-long wave_rows_doubles(long n) {
-  const long nr = wave_nr_for(n);
+long wave_rows_doubles(long n, long nr) {
+  if (nr <= 0) nr = wave_nr_for(n);
   return 3L * nr * ((n + nr - 1) / nr);
 }
-void build_rows(const double* t, const double* f, const double* isg, long n, double* out) {
-  const long nr = wave_nr_for(n);
+void build_rows(const double* t, const double* f, const double* isg, long n, double* out, long nr) {
+  if (nr <= 0) nr = wave_nr_for(n);
   const long rc = (n + nr - 1) / nr;
   for (long c = 0; c < rc; ++c)
     for (long l = 0; l < nr; ++l) {

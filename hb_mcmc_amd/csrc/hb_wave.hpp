@@ -196,12 +196,13 @@ struct Pacer {
 // lanes of an iteration are neighbours in phase.  Values are stored at the
 // lane-row slab positions (slab_pos_of) that the key load reads; eclipsing
 // and slow-path cadences go to the deferred queue.
-// NT threads per walker (64, or 128 for a pair of waves), thread tid
-template <int NT = 64>
+// NT threads per walker (64, or 128 for a pair of waves), thread tid; K
+// interleaved cadences per lane (at most the walker's cadences per lane: a
+// 2-per-lane light curve runs 2, not 4 with two of them padding)
+template <int NT = 64, int K = kK>
 __device__ __forceinline__ void model_pass_cold(const double* __restrict__ t, const double2* __restrict__ ph,
                                                 int n, const Rows& rw, const WalkerConst& w, double* vals,
                                                 int lane, Pacer pc, DeferQ& dq) {
-  constexpr int K = kK;
   const bool tab = (ph != nullptr) && (w.tab != 0.0);  // walker-uniform
   const int last = n - 1;
   const int nit = (n + K * NT - 1) / (K * NT);
@@ -800,7 +801,7 @@ __device__ __forceinline__ void eval_wave_body(const double* __restrict__ t, con
   if (VPT >= kChainVptMin && VPT <= kChainVptMax && chain_eligible(w, gap))
     model_pass_chain_pipe<VPT, NR>(tT, ph, (int)n, rw, w, vals, lane, row, pc, dq);
   else
-    model_pass_cold<NR>(t, ph, (int)n, rw, w, vals, row, pc, dq);
+    model_pass_cold<NR, (VPT < kK ? VPT : kK)>(t, ph, (int)n, rw, w, vals, row, pc, dq);
   HB_CLK_MARK(3);
   HB_WSYNC();  // the slab values of every lane are in place
   // a pair's cold pass writes cadences of either wave's rows, and its queued

@@ -1,12 +1,15 @@
 """Catalog-sweep mode (config C5, hb_mcmc_amd/catalog.py, include/hbmi.h
-hb_catalog_*): many targets on one GPU, one batched launch per size class.
+hb_catalog_*): many targets on one GPU, every size class in one eval launch.
 
 CPU: the lockstep multi-target sampler driven by the oracle likelihood writes,
 for every target, exactly the files the single-target sampler writes for it
 alone (byte for byte); targets are dealt over ranks by cadence count.
-GPU: the batched catalog equals per-target contexts bit for bit and the
-oracle within 1e-10 (every size class N = 2..2048, zero-walker targets, per-
-target magnitude data); the GPU sweep equals the single-target GPU runs.
+GPU: the batched catalog equals per-target contexts bit for bit (within
+the oracle tolerance for N = 1025..1280, where the catalog runs a pair of
+waves and a lone context one wave: other chain starts, chi^2 summed in
+another order) and the oracle within 1e-10
+(every size class N = 2..2048, zero-walker targets, per-target magnitude
+data); the GPU sweep equals the single-target GPU runs.
 """
 import filecmp
 import os
@@ -93,9 +96,9 @@ def test_catalog_equals_per_target_contexts_and_oracle(hbmi, oracle):
 
     real = [golden("lc_real231937440.npz"), golden("lc_real237957506.npz")]
     targets = [synth_target(n, i, oracle, gmag=(12.0 + 0.1 * i) if i % 3 == 0 else None)
-               for i, n in enumerate((2, 7, 63, 64, 65, 128, 300, 1024, 2048))]
+               for i, n in enumerate((2, 7, 63, 64, 65, 128, 300, 1024, 2048, 1025, 1280))]
     targets += [(r["t"], r["f"], r["s"], r["mag"], r["magerr"]) for r in real]
-    walkers = np.array([3, 5, 0, 64, 1, 17, 33, 128, 9, 40, 24], dtype=np.int32)
+    walkers = np.array([3, 5, 0, 64, 1, 17, 33, 128, 9, 20, 7, 40, 24], dtype=np.int32)
     P = synth.walkers(int(walkers.sum()), seed=11)
     with Catalog(targets) as cat:
         got = cat.loglike(P, walkers)
@@ -114,7 +117,16 @@ def test_catalog_equals_per_target_contexts_and_oracle(hbmi, oracle):
             # context would take the multi-wave latency plan (other chi2 order)
             with HBLikelihood(tg[0], tg[1], tg[2], mag, err, latency_plan=False) as L:
                 single = L.loglike(P[o:o + w])
-            assert np.array_equal(got[o:o + w], single, equal_nan=True), k
+            if 1024 < len(tg[0]) < 1281:
+                # the catalog's pair of waves (128 lane rows) against one wave of
+                # 32 cadences per lane in a lone context: other warm-chain
+                # starts, chi^2 summed in another order
+                assert np.array_equal(np.isnan(got[o:o + w]), np.isnan(single)), k
+                ok = ~np.isnan(single)
+                d = np.abs(got[o:o + w][ok] - single[ok]) / np.maximum(1.0, np.abs(single[ok]))
+                assert d.max(initial=0) <= LOGL_RTOL, (k, d.max())
+            else:
+                assert np.array_equal(got[o:o + w], single, equal_nan=True), k
             ref = oracle.loglike_batch(tg[0], tg[1], tg[2], P[o:o + w], mag, err, 8)
             ok = ~np.isnan(ref)
             assert np.array_equal(np.isnan(got[o:o + w]), ~ok)
@@ -128,7 +140,12 @@ def test_catalog_equals_per_target_contexts_and_oracle(hbmi, oracle):
             mag = tg[3] if len(tg) > 3 else synth.MAG_DEFAULT
             err = tg[4] if len(tg) > 4 else synth.MAGERR_DEFAULT
             with HBLikelihood(tg[0], tg[1], tg[2], mag, err) as L:
-                assert np.array_equal(got2[o:o + w], L.loglike(P[o:o + w]), equal_nan=True), k
+                single = L.loglike(P[o:o + w])
+            if 1024 < len(tg[0]) < 1281:
+                d = np.abs(got2[o:o + w] - single) / np.maximum(1.0, np.abs(single))
+                assert np.array_equal(np.isnan(d), np.isnan(single)) and np.nanmax(d, initial=0) <= LOGL_RTOL, k
+            else:
+                assert np.array_equal(got2[o:o + w], single, equal_nan=True), k
         o += w
 
 
