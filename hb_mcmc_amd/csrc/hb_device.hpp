@@ -85,6 +85,27 @@ struct alignas(16) WalkerConst {
 };
 static_assert(sizeof(WalkerConst) == 48 * 8, "WalkerConst layout");
 
+// logL mode: a walker whose logL is decided without its light curve.
+//  * Roche overflow: chi^2 is replaced by 1e15 whatever the template is
+//    (likelihood3.c:866-869): logL = -5e14.
+//  * |e| > 1 (the sampler puts no upper wall on e, likelihood3.c:986-1121, so
+//    hot rungs propose it): sqrt(1 - e^2) is NaN, and with it every cadence's
+//    flux (traj, likelihood3.c:147-182), the median, chi^2 and the reference's
+//    logL -- a NaN (+qNaN, what the reference build returns for every such
+//    walker checked); a NaN logL is only ever rejected by the Hastings test.
+// Returns false when the light curve is needed.
+__device__ __forceinline__ bool logl_without_light_curve(const WalkerConst& w, double& ll) {
+  if (w.roche != 0.0) {
+    ll = -kBig / 2.0;
+    return true;
+  }
+  if (!(w.sq1me2 == w.sq1me2)) {
+    ll = __builtin_nan("");
+    return true;
+  }
+  return false;
+}
+
 // ------------------------------------------------------------------------
 // small helpers
 // ------------------------------------------------------------------------

@@ -413,6 +413,17 @@ struct ProposeShared {
   hbk::PrepShared<kPW> PL;
   int jl[kPW];
 };
+#ifdef HB_DS_CLOCKS
+// experiment builds only: per wave of the last ds_step launch: s_memtime and
+// s_memrealtime at entry, after the records barrier and at the end, the slot,
+// its temperature and e (read back by hb_debug_ds_clocks); per slot of the
+// last propose: the phase stamps DS_T(0..7) (s_memtime), s_memrealtime at
+// entry and after the stores, its temperature, proposal type (hb_debug_dp_clocks)
+constexpr int kDsClkWords = 9;
+__device__ unsigned long long ds_clk[kDsClkWords * 65536];
+constexpr int kDpClkWords = 12;
+__device__ unsigned long long dp_clk[kDpClkWords * 65536];
+#endif
 // the body of ds_propose: every wave of the workgroup calls it (it holds the
 // prep group's barriers); j_out: the wave's global slot, act_out: whether it
 // has one (the grid's last workgroup may hold fewer than kPW)
@@ -450,14 +461,19 @@ __device__ __forceinline__ void propose_group(const Dev& D, int W, int NPAST, lo
   j_out = j;
   act_out = act;
   const double pc_tab = PREP ? *D.tab_pc : 0.0;
-#ifdef HB_DS_TIMING  // experiment builds only: per-phase shader clocks of two slots at iteration 100
-  long long tclk[8], tw0 = wall_clock64();
-#define DS_T(k) tclk[k] = clock64()
-#define DS_PRINT()                                                                                              \
-  if (lane == 0 && iter == 100 && (j == 1 || j == 49 || j == 99))                                                \
-    printf("slot %d: init %lld u2 %lld gauss %lld - %lld walls %lld priors %lld alpha+store %lld total %lld wall %lld\n", \
-           j, tclk[1] - tclk[0], tclk[2] - tclk[1], tclk[3] - tclk[2], tclk[4] - tclk[3], tclk[5] - tclk[4],        \
-           tclk[6] - tclk[5], tclk[7] - tclk[6], tclk[7] - tclk[0], wall_clock64() - tw0);
+#ifdef HB_DS_CLOCKS  // experiment builds only: per-slot phase stamps (dp_clk, scripts/ds_clocks.py)
+  unsigned long long tclk[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const unsigned long long trt0 = __builtin_amdgcn_s_memrealtime();
+#define DS_T(k) tclk[k] = __builtin_amdgcn_s_memtime()
+#define DS_PRINT()                                                                      \
+  if (jl < 65536) {                                                                     \
+    unsigned long long* o_ = dp_clk + kDpClkWords * jl;                                 \
+    for (int q_ = 0; q_ < 8; ++q_) o_[q_] = tclk[q_];                                   \
+    o_[8] = trt0;                                                                       \
+    o_[9] = __builtin_amdgcn_s_memrealtime();                                           \
+    o_[10] = (unsigned long long)__double_as_longlong(temp);                            \
+    o_[11] = (unsigned long long)(jt | (jmp << 8));                                     \
+  }
 #else
 #define DS_T(k)
 #define DS_PRINT()
@@ -604,13 +620,6 @@ __global__ __launch_bounds__(64 * kPW) HB_DS_PROPOSE_ATTR void ds_propose(Dev D,
   propose_group<PREP>(D, W, NPAST, iter, sch_src, sch_dst, n8, S, j, act);
 }
 
-#ifdef HB_DS_CLOCKS
-// experiment builds only: per wave of the last ds_step launch: s_memtime and
-// s_memrealtime at entry, after the records barrier and at the end, the slot,
-// its temperature and e (read back by hb_debug_ds_clocks)
-constexpr int kDsClkWords = 9;
-__device__ unsigned long long ds_clk[kDsClkWords * 65536];
-#endif
 // The whole iteration up to the swaps in ONE launch (propose -> records ->
 // likelihood -> Hastings test), for a shard of at most one resident round
 // (nl <= 16 per CU) on the one-wave plan: each workgroup's four waves propose
@@ -1869,6 +1878,11 @@ extern "C" int hb_dsampler_gather(hb_dsampler* d, double* x_slots, double* logl_
 extern "C" int hb_debug_ds_clocks(unsigned long long* out, int nslots) {
   if (nslots > 65536) nslots = 65536;
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(ds_clk), kDsClkWords * sizeof(unsigned long long) * nslots) == hipSuccess
+             ? 0 : -1;
+}
+extern "C" int hb_debug_dp_clocks(unsigned long long* out, int nslots) {
+  if (nslots > 65536) nslots = 65536;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(dp_clk), kDpClkWords * sizeof(unsigned long long) * nslots) == hipSuccess
              ? 0 : -1;
 }
 #endif

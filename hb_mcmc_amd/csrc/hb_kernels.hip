@@ -443,10 +443,11 @@ __global__ __launch_bounds__(64 * NW) void hb_eval_kernel(
   double* vals = LDS ? reinterpret_cast<double*>(smem + sizeof(SelShared))
                      : scratch + (size_t)wv * (size_t)n;
   const WalkerConst& w = wcs[wv];
-  // Roche overflow replaces chi^2 by 1e15 whatever the template is
-  // (likelihood3.c:866-869): the logL needs no light curve (block-uniform exit)
-  if (mode == 0 && w.roche != 0.0) {
-    if (tid == 0) logl[wv] = -kBig / 2.0;
+  // Roche overflow, |e| > 1: the logL needs no light curve (block-uniform
+  // exit, logl_without_light_curve)
+  double ll0;
+  if (mode == 0 && logl_without_light_curve(w, ll0)) {
+    if (tid == 0) logl[wv] = ll0;
     return;
   }
 
@@ -780,8 +781,9 @@ __global__ __launch_bounds__(64 * NW) HB_WPE_ATTR void hb_eval_block_kernel(
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int wv = blockIdx.x;
   const WalkerConst& w = wcs[wv];
-  if (mode == 0 && w.roche != 0.0) {  // likelihood3.c:866-869, see hb_eval_kernel
-    if (tid == 0) logl[wv] = -kBig / 2.0;
+  double ll0;
+  if (mode == 0 && logl_without_light_curve(w, ll0)) {  // see hb_eval_kernel
+    if (tid == 0) logl[wv] = ll0;
     return;
   }
   const int nn = (int)n;

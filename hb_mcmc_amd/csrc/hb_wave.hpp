@@ -773,15 +773,16 @@ __device__ __forceinline__ void eval_wave_body(const double* __restrict__ t, con
   double* vals = reinterpret_cast<double*>(smem);
   uint32_t* hist = reinterpret_cast<uint32_t*>(smem);
   uint64_t* cand = reinterpret_cast<uint64_t*>(smem + cand_off);
-  const bool roche_exit = mode == 0 && w.roche != 0.0;
+  double ll0 = 0.0;
+  const bool early_exit = mode == 0 && logl_without_light_curve(w, ll0);
   Pacer pc{0, 0, 0};
   // the Hastings test's operands (uniform values and the 21-coordinate rows)
   // are loaded now, not after the likelihood
   hbds::AccPre apre{};
   if (ACC) apre = hbds::accept_prefetch(hst, wv, lane);
-  if (roche_exit) {  // likelihood3.c:866-869: chi^2 is replaced by 1e15 whatever the template is
-    if (row == 0) logl[wv] = -kBig / 2.0;
-    if (ACC) (void)hbds::accept_slot_wave_pre(hst, wv, -kBig / 2.0, lane, apre);
+  if (early_exit) {  // Roche overflow, |e| > 1: logl_without_light_curve (hb_device.hpp)
+    if (row == 0) logl[wv] = ll0;
+    if (ACC) (void)hbds::accept_slot_wave_pre(hst, wv, ll0, lane, apre);
     HB_CLK_END(wv);
     return;
   }

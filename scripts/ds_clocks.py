@@ -7,6 +7,11 @@ launch's length comes from: the hot slots' walls, the likelihood of hot
 (high-e) walkers, or the bulk.
 
     HB_DS_STEP=1 HBMI_LIB=.../libhbmi_dsclk.so python scripts/ds_clocks.py [--iters 120]
+
+--propose (the default two-launch iteration, HB_DS_STEP unset): the phases of
+every slot's wave in the last ds_propose launch instead (init, first draws,
+Gaussian / differential-evolution proposal, walls, priors, stores), by
+temperature decile and proposal type.
 """
 import argparse
 import ctypes as C
@@ -28,6 +33,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--walkers", type=int, default=4096)
 ap.add_argument("--ncad", type=int, default=1024)
 ap.add_argument("--iters", type=int, default=120)
+ap.add_argument("--propose", action="store_true")
 a = ap.parse_args()
 n, W = a.ncad, a.walkers
 t = synth.cadences(n)
@@ -44,6 +50,38 @@ with DeviceSampler(S, L) as D:
         D.step(it)
     D.sync()
 lib = _lib.lib()
+if a.propose:
+    NW = 12
+    buf = (C.c_ulonglong * (NW * W))()
+    assert lib.hb_debug_dp_clocks(buf, W) == 0
+    c = np.frombuffer(buf, dtype=np.uint64).reshape(W, NW)
+    ck = c[:, :8].astype(np.int64)
+    rt0, rt1 = c[:, 8].astype(np.int64), c[:, 9].astype(np.int64)
+    temp = c[:, 10].copy().view(np.float64)
+    jt = (c[:, 11] & 0xff).astype(int)
+    ph = np.diff(ck, axis=1)  # 0->1 init, 1->2 first draw, 2->3 proposal, 3->4 -, 4->5 walls, 5->6 priors, 6->7 stores
+    names = ["init", "first draw + jscale", "proposal", "-", "walls", "priors", "alpha + stores"]
+    k0 = rt0.min()
+    life = (rt1 - rt0) / 100.0
+    dec = np.minimum(9, (np.argsort(np.argsort(-temp)) * 10) // W)  # 0 = hottest decile
+    res = {"span_us": float((rt1.max() - k0) / 100.0),
+           "start_us_pct": [float(x) for x in np.percentile((rt0 - k0) / 100.0, [0, 50, 100])],
+           "end_us_pct": [float(x) for x in np.percentile((rt1 - k0) / 100.0, [5, 50, 90, 99, 100])],
+           "life_us_pct": [float(x) for x in np.percentile(life, [5, 50, 90, 99, 100])],
+           "phase_cycles_mean": dict(zip(names, [float(x) for x in ph.mean(axis=0)])),
+           "by_temperature_decile": [{"decile": int(d), "life_us_median": float(np.median(life[dec == d])),
+                                      "phase_cycles_median": dict(zip(names, [float(x) for x in np.median(ph[dec == d], axis=0)]))}
+                                     for d in range(10)],
+           "by_type": {str(t): {"slots": int((jt == t).sum()), "life_us_median": float(np.median(life[jt == t]))}
+                       for t in sorted(set(jt.tolist()))},
+           "last_64": {"temp_decile_median": float(np.median(dec[np.argsort(rt1)[-64:]])),
+                       "life_us_median": float(np.median(life[np.argsort(rt1)[-64:]])),
+                       "start_us_median": float(np.median((rt0[np.argsort(rt1)[-64:]] - k0) / 100.0))},
+           "shader_clock_ghz_median": float(np.median((ck[:, 7] - ck[:, 0]) / np.maximum(rt1 - rt0, 1)) * 0.1)}
+    print(json.dumps(res, indent=1))
+    S.close()
+    L.close()
+    sys.exit(0)
 NW = 9
 buf = (C.c_ulonglong * (NW * W))()
 assert lib.hb_debug_ds_clocks(buf, W) == 0

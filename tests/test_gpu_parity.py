@@ -546,6 +546,33 @@ def test_prior_spread_walkers_c2(hbmi, oracle, seed):
     assert ((P[:, 3] > 0.8) & ~roche).sum() >= 20  # cold-path walkers are exercised
 
 
+@pytest.mark.parametrize("n", [1024, 1500, 3000, 20000])
+def test_eccentricity_above_one_every_plan(hbmi, oracle, n):
+    """Walkers with |e| > 1 (the sampler's hot rungs propose them: e has no
+    upper wall, likelihood3.c:986-1121) take logl_without_light_curve's NaN;
+    e < -1 walkers in Roche overflow the sentinel.  One-wave, pair, rows and
+    block plans against the oracle: NaN pattern and sentinel exact, the
+    finite walkers beside them within 1e-10, and the batch reversed bit for
+    bit."""
+    from hb_mcmc_amd import synth
+    from hb_mcmc_amd.likelihood import HBLikelihood
+
+    t, f, s = synth.dataset(n, oracle.light_curve)
+    P = synth.prior_walkers(48, seed=5)
+    rng = np.random.default_rng(17)
+    P[:16, 3] = 1.0 + rng.random(16) * 4.0          # e in (1, 5]
+    P[16, 3] = np.nextafter(1.0, 2.0)               # the first e with 1 - e^2 < 0
+    P[17, 3] = 1.0                                  # sqrt(0): the light curve is computed
+    P[18:24, 3] = -1.0 - rng.random(6) * 2.0        # e < -1: Roche or NaN
+    with HBLikelihood(t, f, s) as L:
+        a = L.loglike(P)
+        rev = L.loglike(P[::-1].copy())[::-1]
+    assert np.array_equal(a, rev, equal_nan=True)
+    ref = oracle.loglike_batch(t, f, s, P, synth.MAG_DEFAULT, synth.MAGERR_DEFAULT, 8)
+    assert np.isnan(ref[:17]).all() and np.isnan(a[:17]).all()
+    close_logl(a, ref)
+
+
 # ------------------------------------------------- full-size (config C4)
 def test_full_size_c4_against_oracle_and_properties(hbmi, oracle):
     """W = 65 536, N = 1024 (BASELINE config C4's whole ensemble on one GPU):

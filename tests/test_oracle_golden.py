@@ -102,3 +102,33 @@ def test_write_lc_to_file_bytes(oracle, tmp_path):
         path = tmp_path / f"lc{k}.txt"
         oracle.write_lc_to_file(p, str(path))
         assert path.read_bytes() == g[f"file{k}"].tobytes()
+
+
+def test_eccentricity_above_one_gives_nan_logl(oracle):
+    """The premise of the eval kernels' |e| > 1 exit (hb_device.hpp
+    logl_without_light_curve): for every walker with 1 - e^2 < 0 that is not
+    in Roche overflow the reference's loglikelihood is NaN, whatever the other
+    parameters -- checked on the reference build itself (oracle/_ref, when
+    built here) and on the oracle, over 600 prior-box walkers with e in
+    (1, 50] and e < -1, on a synthetic and a real light curve."""
+    from oracle import Reference, reference_available
+
+    from hb_mcmc_amd import synth
+
+    rng = np.random.default_rng(23)
+    P = synth.prior_walkers(600, seed=21)
+    P[:300, 3] = 1.0 + rng.random(300) ** 3 * 49.0
+    P[300:400, 3] = np.nextafter(1.0, 2.0) + rng.random(100) * 1e-6
+    P[400:, 3] = -1.0 - rng.random(200) * 10.0
+    g = golden("lc_real231937440.npz")
+    sets = [synth.dataset(300, oracle.light_curve), (g["t"], g["f"], g["s"])]
+    impls = [oracle] + ([Reference()] if reference_available() else [])
+    for t, f, s in sets:
+        for impl in impls:
+            ll = impl.loglike_batch(t, f, s, P, synth.MAG_DEFAULT, synth.MAGERR_DEFAULT, 8)
+            pos = P[:, 3] > 1.0
+            assert np.isnan(ll[pos]).all()
+            # e < -1: the periastron a (1 - e) is positive, so Roche may fire and
+            # then wins (likelihood3.c:866-869); otherwise NaN
+            neg = ~pos
+            assert (np.isnan(ll[neg]) | (ll[neg] == -5e14)).all()
