@@ -547,8 +547,23 @@ __device__ __forceinline__ void propose_group(const Dev& D, int W, int NPAST, lo
     }
     DS_T(3);
     DS_T(4);
+#ifndef HB_DS_LOST
+#define HB_DS_LOST 1  // A/B knob: 0 = walls and priors of every proposal
+#endif
+    // A proposal with e > 1 that the walls leave as it is (e has no upper
+    // wall, set_limits :986-1121) gets a NaN logL whatever its other
+    // coordinates (hb_device.hpp logl_without_light_curve: 1 - e^2 < 0, Roche
+    // impossible with the periastron a (1 - e) < 0), so the Hastings test
+    // rejects it.  Its other coordinates' walls and its prior terms feed only
+    // that logL, the records and the test, and a rejected proposal is never
+    // stored: they are skipped (logPy = NaN).  No draw depends on them.
+    const double e_pre = rld(yn, 3);
+    const bool e_kept = (e_pre >= P->lim_lo[3] || (P->fl_lo[3] != 1 && P->fl_lo[3] != 2)) &&
+                        (e_pre <= P->lim_hi[3] || (P->fl_hi[3] != 1 && P->fl_hi[3] != 2));  // the walls leave e alone
+    const bool lost = HB_DS_LOST && e_pre > 1.0 && e_kept;
     // walls (:440-467), one coordinate per lane
-    if (lane < kNp) yn = hbwall::apply_wall(yn, P->lim_lo[lane], P->lim_hi[lane], P->fl_lo[lane], P->fl_hi[lane]);
+    if (lane < kNp && (!lost || lane == 3))
+      yn = hbwall::apply_wall(yn, P->lim_lo[lane], P->lim_hi[lane], P->fl_lo[lane], P->fl_hi[lane]);
     // "order the masses" (:470-475) as written: y[1] = y[0]; period fixed; T0 folded
     const double y0 = rld(yn, 0), y1 = rld(yn, 1);
     if (lane == 1 && y1 > y0) yn = y0;
@@ -557,7 +572,7 @@ __device__ __forceinline__ void propose_group(const Dev& D, int W, int NPAST, lo
     DS_T(5);
     // prior terms (:444, :477), summed per slot in the reference's order
     const bool prior = lane < kNp && P->gpflag[lane] == 1;
-    const double ty = prior ? prior_term(lane, yn, T) : 0.0;
+    const double ty = (prior && !lost) ? prior_term(lane, yn, T) : 0.0;
     const double tx = (needx && prior) ? prior_term(lane, xn, T) : 0.0;
     double lpy = 0., lpx = 0.;
     for (int i = 0; i < kNp; ++i) {
@@ -565,6 +580,7 @@ __device__ __forceinline__ void propose_group(const Dev& D, int W, int NPAST, lo
       lpy += rld(ty, i);
       if (needx) lpx += rld(tx, i);
     }
+    if (lost) lpy = __builtin_nan("");
     DS_T(6);
     // the alpha draw and the retirement of the consumed draws only feed the
     // stored state, so they follow the walls (off the hot slots' critical path)

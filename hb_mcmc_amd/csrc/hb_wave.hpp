@@ -776,10 +776,14 @@ __device__ __forceinline__ void eval_wave_body(const double* __restrict__ t, con
   double ll0 = 0.0;
   const bool early_exit = mode == 0 && logl_without_light_curve(w, ll0);
   Pacer pc{0, 0, 0};
-  // the Hastings test's operands (uniform values and the 21-coordinate rows)
-  // are loaded now, not after the likelihood
+#ifndef HB_ACC_LATE
+#define HB_ACC_LATE 1  // A/B knob: 0 = the Hastings operands loaded at the wave's start
+#endif
+  // the Hastings test's operands (uniform values and the 21-coordinate rows):
+  // loaded after the model pass (HB_ACC_LATE), in flight through the select,
+  // so they hold no registers across the model loop
   hbds::AccPre apre{};
-  if (ACC) apre = hbds::accept_prefetch(hst, wv, lane);
+  if (ACC && (!HB_ACC_LATE || early_exit)) apre = hbds::accept_prefetch(hst, wv, lane);
   if (early_exit) {  // Roche overflow, |e| > 1: logl_without_light_curve (hb_device.hpp)
     if (row == 0) logl[wv] = ll0;
     if (ACC) (void)hbds::accept_slot_wave_pre(hst, wv, ll0, lane, apre);
@@ -810,6 +814,7 @@ __device__ __forceinline__ void eval_wave_body(const double* __restrict__ t, con
   if (WPW > 1) __syncthreads();
   dq_apply(w, vals, dq, t, rw, (int)n, lane);
   if (WPW > 1) __syncthreads();
+  if (ACC && HB_ACC_LATE) apre = hbds::accept_prefetch(hst, wv, lane);
   HB_CLK_MARK(0);
   HB_WSYNC();
   // live key slots of this lane; a light curve of 64 VPT cadences fills every row
