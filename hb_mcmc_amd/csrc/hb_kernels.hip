@@ -733,6 +733,9 @@ __device__ __forceinline__ void block_select_pass(const uint64_t (&key)[VPT], ui
   hi = shift - 1;
 }
 
+// first digit of the block select: 10 bits like the one-wave kernels (C3 at
+// 9 / 11 / 12 bits: +0.8% / -0.2% / +0.5% per step, profiles/r05/r05q_c3_sel_bits_ab.txt)
+constexpr int kBlkSelBits = kSelBits;
 template <int NW, int VPT>
 __device__ double block_select2(const uint64_t (&key)[VPT], uint32_t kth, uint64_t kmin, uint64_t kmax,
                                 uint32_t* hist, uint64_t* cand, SelShared* sh) {
@@ -742,7 +745,7 @@ __device__ double block_select2(const uint64_t (&key)[VPT], uint32_t kth, uint64
   uint64_t mask = (hi == 63) ? 0ull : ~((2ull << hi) - 1ull);
   uint64_t prefix = kmin & mask;
   uint32_t kk = kth, cnt = 0;
-  block_select_pass<NW, VPT, kSelBits>(key, hist, sh, tid, hi, mask, prefix, kk, cnt);
+  block_select_pass<NW, VPT, kBlkSelBits>(key, hist, sh, tid, hi, mask, prefix, kk, cnt);
   while (cnt > (uint32_t)kCandMax && hi >= 0)
     block_select_pass<NW, VPT, kSelBits2>(key, hist, sh, tid, hi, mask, prefix, kk, cnt);
   if (hi < 0) return dval(prefix);
@@ -777,7 +780,7 @@ __global__ __launch_bounds__(64 * NW) HB_WPE_ATTR void hb_eval_block_kernel(
   SelShared* sh = reinterpret_cast<SelShared*>(smem);
   double* vals = reinterpret_cast<double*>(smem + sizeof(SelShared));
   uint32_t* hist = reinterpret_cast<uint32_t*>(vals);
-  uint64_t* cand = reinterpret_cast<uint64_t*>(smem + sizeof(SelShared) + (4u << kSelBits));
+  uint64_t* cand = reinterpret_cast<uint64_t*>(smem + sizeof(SelShared) + (4u << kBlkSelBits));
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int wv = blockIdx.x;
   const WalkerConst& w = wcs[wv];
@@ -1463,7 +1466,7 @@ EvalPlan make_block_plan(long n) {
     if (nw < 4) nw = 4;
     pl.nw = nw;
     const long per = (n + 64L * nw - 1) / (64L * nw);  // cadences per thread
-    if (per <= 32 && need >= sizeof(SelShared) + (4u << kSelBits) + 8 * kCandMax)
+    if (per <= 32 && need >= sizeof(SelShared) + (4u << kBlkSelBits) + 8 * kCandMax)
       // exact fit at 17..20 (C3: N = 20 000 over 16 waves is 19.5 per thread): 24
       // key slots there cost <16, 24> 14 VGPR spills (64 B of scratch per lane).
       // Whenever the slab fits LDS, per <= 20 (N <= 20 300 over 16 waves; fewer
