@@ -540,8 +540,8 @@ def run_c5(a, rank, world, local, dev):
                            "global_walkers": a.targets * a.walkers_per_target,
                            "parallelism": f"targets dealt over {world} GPU(s) by cadence count, no collective"},
                 "roofline": roofline("C5", call_ms, float(wtot), bytes_step,
-                                     {"kernel": "hb_catalog call (prep + hb_eval_wave_kernel<VPT,true> per size "
-                                                "class), rank 0", "kernel_ms": call_ms, "kernel_event_samples": ks,
+                                     {"kernel": "hb_catalog call (hb_prep_kernel + hb_eval_catalog_kernel, every "
+                                                "size class in one launch), rank 0", "kernel_ms": call_ms, "kernel_event_samples": ks,
                                       "kernel_timer": a.timer})}
         print(json.dumps(line), flush=True)
 

@@ -7,8 +7,8 @@ calling loglikelihood() per chain per step.  Here
 
 * `Catalog` holds every target's light curve on one GPU (concatenated in HBM
   with a per-target descriptor table, include/hbmi.h hb_catalog_*), and one
-  call evaluates all targets' walkers with one prep launch and one eval launch
-  per cadences-per-lane class, instead of one small launch per target;
+  call evaluates all targets' walkers with one prep launch and ONE eval launch
+  holding every cadences-per-lane class, instead of one small launch per target;
 * `run_catalog` runs one PT-MCMC per target (the mcmc_wrapper2.c loop, the
   same phase API as hb_mcmc_run) in lockstep: each iteration draws every
   target's proposals, evaluates all of them in ONE catalog call, then runs each

@@ -193,8 +193,8 @@ const char *hb_last_error(void);
  * data mag5[5k..5k+4] / magerr4[4k..4k+3] (NULL: the reference fallback
  * {1000,1,1,1,1} / 1e15).  All light curves are concatenated in HBM with a
  * per-target descriptor table; one call evaluates every target's walkers
- * with one prep launch and one eval launch per cadences-per-lane class
- * (instead of one small launch per target).  params: sum(walkers[k]) x 21
+ * with one prep launch and ONE eval launch holding every cadences-per-lane
+ * class (instead of one small launch per target).  params: sum(walkers[k]) x 21
  * rows, target 0's walkers first, then target 1's, ...; logl likewise. ---- */
 typedef struct hb_catalog hb_catalog;
 hb_catalog *hb_catalog_create(int ntargets, const double *const *t, const double *const *flux,

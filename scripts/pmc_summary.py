@@ -5,8 +5,8 @@
 Reads gpurun_out/pmc_TAG/*/run_counter_collection.csv (separate --pmc passes
 over `bench.py`, scripts/pmc.sh), keeps the dispatches of the timed workload
 (C2/C4: hb_eval_wave_kernel over 64 x WALKERS threads; C3: the eval kernel
-dispatch with the largest grid (the 16-wave rows kernel); C5: the catalog's hb_eval_wave_kernel<.., true, ..>
-classes, summed per call = per hb_prep_kernel over all walkers) and writes
+dispatch with the largest grid (the 16-wave rows kernel); C5: the catalog's one eval launch,
+hb_eval_catalog_kernel, per call = per hb_prep_kernel over all walkers) and writes
 
   profiles/TAG_pmc_CONFIG.json        per-call counters + derived figures
   profiles/pmc_counters.json          [build id][CONFIG] -> the same, read by bench.py
@@ -42,7 +42,7 @@ def is_eval(r):
         return "hb_eval_wave_kernel<" in k and int(r["Grid_Size"]) == 64 * walkers
     if config == "C3":  # the rows kernel (hb_eval_wave_kernel<.., WPW = 16>) or, HB_NO_ROWS=1, the block kernel
         return "hb_eval_block_kernel<" in k or "hb_eval_wave_kernel<" in k
-    return "hb_eval_wave_kernel<" in k and ", true," in k
+    return "hb_eval_catalog_kernel" in k
 
 
 # hb_prep_kernel: 32 / 16 walkers per 256-thread workgroup (hbk::launch_prep: the most that leave >= 256
