@@ -23,6 +23,10 @@ struct Counters {
   double xmap[kNp];
   int nev;
   int pad;
+  // differential-evolution trials of chain 0 drawn by iteration q's proposals
+  // (slot q & 1), folded into DEtrial_tot by q's bookkeeping (swap_tail): the
+  // next iteration's proposals may run beside it (deferred swaps)
+  long long de_trial_pend[2];
 };
 
 struct Event {  // LogSuspiciousJumps (:520-528) arguments
@@ -87,11 +91,14 @@ struct AccArgs {
   int pad;
   // eval wave -> local slot by descending e (null: wave w takes slot w):
   // ds_propose files slot j under bin b = e_bin_desc(e_j) at
-  // elist[b * ecap + ecnt[b]++]; ds_swap clears ecnt for the next iteration
+  // elist[b * ecap + ecnt[b]++].  The counters alternate between two buffers
+  // by iteration; this launch clears the next iteration's (ecnt_next, read by
+  // the previous launch, filed by the next ds_propose)
   const int* ecnt;     // [kOrdBins]
   const int* elist;    // [kOrdBins][ecap]
   int ecap, pad2;
   double* Lslot;       // [W] logL of the chain in slot j after its Hastings test (null: not kept)
+  int* ecnt_next;      // [kOrdBins] (null: none)
 };
 
 // Eval wave s of the device sampler takes the s-th slot of the bins in order

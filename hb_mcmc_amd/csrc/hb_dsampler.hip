@@ -130,6 +130,10 @@ struct Dev {
   int* idx_out;    // [W] the other buffer: ds_swap_seg writes the next iteration's index[] there
   int* order;      // [nl] propose wave -> (global) slot, hottest rungs first (dispatch order)
   int* ecnt;       // [kOrdBins] proposals per e bin (AccArgs::ecnt; null: eval waves in slot order)
+  int* ecnt_next;  // the other buffer (the next iteration's; cleared by this iteration's Hastings launch)
+  int par;         // the iteration's parity (Counters::de_trial_pend slot), counted by the host
+  long long* nsw;  // [nl] accepted swaps with b = slot counted by deferred replays, folded into
+                   // Counters::nswap by the next ds_swap_seg (no same-address atomics per wave)
   int* elist;      // [kOrdBins][nl] local slots by e bin
   double* wc;      // [nl] WalkerConst records (the context's workspace; set per launch)
   hbk::MagArgs ma; // Gaia term data of the context
@@ -421,17 +425,139 @@ struct ProposeShared {
 // entry and after the stores, its temperature, proposal type (hb_debug_dp_clocks)
 constexpr int kDsClkWords = 9;
 __device__ unsigned long long ds_clk[kDsClkWords * 65536];
-constexpr int kDpClkWords = 12;
+constexpr int kDpClkWords = 16;
 __device__ unsigned long long dp_clk[kDpClkWords * 65536];
 #endif
+// the per-iteration bookkeeping after the swaps (:551-572, :590, :622-629)
+// by thread 0 of one workgroup; c0 = the chain now in slot 0 (-1: not this
+// rank's slot).  nswap is added by every segment (atomics).
+__device__ __forceinline__ void swap_tail(const Dev& D, long long iter, int par, int c0) {
+  Counters* C = D.ctr;
+  C->DEtrial_tot += C->de_trial_pend[par];  // the iteration's proposals' DE trials (Counters)
+  C->de_trial_pend[par] = 0;
+  C->acc += C->acc_it;  // hb_sampler_accept's sums over the slots
+  C->cold_acc += C->acc_it;
+  C->DEacc += C->DEacc_tot;
+  C->DEtrial += C->DEtrial_tot;
+  C->acc_it = 0;
+  C->snap[0] = C->acc;
+  C->snap[1] = C->DEacc;
+  C->snap[2] = C->DEtrial;
+  C->snap[3] = C->atrial;
+  if (c0 >= 0 && D.logL[c0] > C->logLmap) {  // :565-572
+    for (int i = 0; i < kNp; ++i) C->xmap[i] = D.x[(size_t)c0 * kNp + i];
+    C->logLmap = D.logL[c0];
+  }
+  C->atrial++;  // :590 and the 100-step reset of :622-629
+  if (iter % 100 == 0) {
+    C->acc = C->atrial = 0;
+    C->DEacc_tot = C->DEtrial_tot = 0;
+  }
+}
+
+// The previous iteration's tempering swaps, deferred from their own launch
+// into this ds_propose (one-process samplers, hb_dsampler::pend): the wave of
+// slot j replays the cone of the one-slot segment [j, j + 1), i.e. the
+// attempts whose pair lies in [j - nlv, j + nlv + 1), taken from the attempt
+// lists of the ds_swap_seg segment holding j (whose cone contains it).  The
+// segment argument of ds_swap_seg holds for a one-slot segment: after the nlv
+// levels slot j's chain is exact, and so is every attempt with b = j, which
+// the wave counts (nswap).  So slot j's chain needs no other wave and no
+// launch boundary: it is written to this iteration's index[] (idx_out) and
+// the proposal reads its state.  The iteration's bookkeeping (swap_tail) is
+// run by slot 0's wave.
+struct SwapPrev {
+  const int* soff;        // the previous iteration's schedule (its device ring slot)
+  const SwapEnt* ent;
+  const double* betas;
+  const double* Ls;       // [W] logL by slot after the previous Hastings test (null: D.logL by chain)
+  int* idx_out;           // [W] this iteration's index[]
+  long long iter;         // the previous iteration
+  int nlv, G;
+  int cone, maxent;       // per-wave LDS sizing: cone slots (2 nlv + 1), attempts of one segment
+};
+__host__ __device__ inline size_t swap_prev_wave_bytes(int cone, int maxent) {
+  return (((size_t)cone * (2 * sizeof(double) + sizeof(int)) + 15) & ~(size_t)15) + sizeof(SwapEnt) * (size_t)maxent;
+}
+// returns the chain in slot j after the previous iteration's swaps; nacc: the
+// accepted attempts with b = j (wave-uniform)
+__device__ __forceinline__ int replay_prev_swaps(const Dev& D, const SwapPrev& SP, int W, int j, int lane,
+                                                 const hbglibc::Tabs& T, unsigned char* scr, int& nacc,
+                                                 unsigned long long* rp = nullptr) {
+  if (rp) rp[0] = __builtin_amdgcn_s_memtime();
+  const int nlv = SP.nlv;
+  const int g = seg_of(j - D.lo, D.nl, SP.G);
+  const int clo = max(0, j - nlv), chi = min(W, j + nlv + 1), Wc = chi - clo;
+  double* cL = reinterpret_cast<double*>(scr);
+  double* cH = cL + SP.cone;
+  int* cC = reinterpret_cast<int*>(cH + SP.cone);
+  SwapEnt* sE = reinterpret_cast<SwapEnt*>(scr + (((size_t)SP.cone * (2 * sizeof(double) + sizeof(int)) + 15) &
+                                                  ~(size_t)15));
+  // the segment's level offsets (nlv + 1 <= 65 of them: lane l holds level l's
+  // start, lane 64 the end read apart), then its attempts and the cone's slots
+  const int so = lane <= nlv ? SP.soff[g * nlv + lane] : 0;
+  const int eb = __builtin_amdgcn_readfirstlane(so);
+  const int eend = nlv < 64 ? __builtin_amdgcn_readlane(so, nlv) : SP.soff[g * nlv + nlv];
+  const int ne = eend - eb;
+  for (int q = lane; q < ne; q += 64) sE[q] = SP.ent[eb + q];
+  for (int i = lane; i < Wc; i += 64) {
+    const int c = D.idx[clo + i];
+    cC[i] = c;
+    cH[i] = D.hs[clo + i];
+    cL[i] = SP.Ls != nullptr ? SP.Ls[clo + i] : D.logL[c];
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  if (rp) {
+    rp[1] = __builtin_amdgcn_s_memtime();
+    rp[3] = (unsigned long long)(unsigned)ne | ((unsigned long long)(unsigned)nlv << 32);
+  }
+  int acc_j = 0;
+  for (int lv = 0; lv < nlv; ++lv) {  // ds_swap_seg's level loop on the cone's attempts
+    const int e0 = __builtin_amdgcn_readlane(so, lv) - eb;
+    const int e1 = (lv + 1 < 64 ? __builtin_amdgcn_readlane(so, lv + 1) : eend) - eb;
+    for (int q = e0 + lane; q < e1; q += 64) {
+      const int b = sE[q].b;
+      if (b < clo || b + 1 >= chi) continue;  // its pair is not in this slot's cone
+      const double lnb = sE[q].lnb;
+      const int bl = b - clo, al = bl + 1;
+      const double lb = cL[bl], la = cL[al];
+      const double x = (lb - la) * cH[bl];
+      bool acc;
+      const double dl = 1e-12 * (1.0 + fabs(lnb));
+      if (lnb > -HUGE_VAL && x >= lnb + dl) acc = true;
+      else if (lnb > -HUGE_VAL && x <= lnb - dl) acc = false;
+      else acc = hbglibc::exp(x, T) >= SP.betas[eb + q];
+      if (acc) {
+        const int ca = cC[al], cb = cC[bl];
+        cL[al] = lb;
+        cL[bl] = la;
+        cC[al] = cb;
+        cC[bl] = ca;
+        if (b == j) ++acc_j;  // a pair may be attempted at several levels
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+  if (rp) rp[2] = __builtin_amdgcn_s_memtime();
+  for (int off = 32; off >= 1; off >>= 1) acc_j += __shfl_xor(acc_j, off, 64);
+  nacc = __builtin_amdgcn_readfirstlane(acc_j);
+  return __builtin_amdgcn_readfirstlane(cC[j - clo]);
+}
+
 // the body of ds_propose: every wave of the workgroup calls it (it holds the
 // prep group's barriers); j_out: the wave's global slot, act_out: whether it
-// has one (the grid's last workgroup may hold fewer than kPW)
-template <bool PREP>
+// has one (the grid's last workgroup may hold fewer than kPW).  SWAP: the
+// previous iteration's swaps replayed first (SwapPrev; scr: the wave's LDS)
+template <bool PREP, bool SWAP = false>
 __device__ __forceinline__ void propose_group(const Dev& D, int W, int NPAST, long long iter,
                                               const unsigned long long* __restrict__ sch_src,
                                               unsigned long long* __restrict__ sch_dst, long long n8,
-                                              ProposeShared& Ls, int& j_out, bool& act_out) {
+                                              ProposeShared& Ls, int& j_out, bool& act_out,
+                                              const SwapPrev& SP = SwapPrev{}, unsigned char* scr = nullptr) {
   const long long sgt = (long long)(gridDim.x - 1 - blockIdx.x) * blockDim.x + threadIdx.x;
   const long long sgs = (long long)gridDim.x * blockDim.x;
   unsigned long long sv = 0;
@@ -463,6 +589,7 @@ __device__ __forceinline__ void propose_group(const Dev& D, int W, int NPAST, lo
   const double pc_tab = PREP ? *D.tab_pc : 0.0;
 #ifdef HB_DS_CLOCKS  // experiment builds only: per-slot phase stamps (dp_clk, scripts/ds_clocks.py)
   unsigned long long tclk[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long rp_[4] = {0, 0, 0, 0};  // deferred-swap replay: start, staged, levels done, (ne | nlv << 32)
   const unsigned long long trt0 = __builtin_amdgcn_s_memrealtime();
 #define DS_T(k) tclk[k] = __builtin_amdgcn_s_memtime()
 #define DS_PRINT()                                                                      \
@@ -473,15 +600,19 @@ __device__ __forceinline__ void propose_group(const Dev& D, int W, int NPAST, lo
     o_[9] = __builtin_amdgcn_s_memrealtime();                                           \
     o_[10] = (unsigned long long)__double_as_longlong(temp);                            \
     o_[11] = (unsigned long long)(jt | (jmp << 8));                                     \
+    o_[12] = rp_[0];                                                                    \
+    o_[13] = rp_[1];                                                                    \
+    o_[14] = rp_[2];                                                                    \
+    o_[15] = rp_[3];                                                                    \
   }
 #else
 #define DS_T(k)
 #define DS_PRINT()
 #endif
   DS_T(0);
-  const int chain = D.idx[j];
-  const bool needx = !D.logP_ok[chain];
-  const double xn = lane < kNp ? D.x[(size_t)chain * kNp + lane] : 0.0;
+  int chain = SWAP ? 0 : D.idx[j];
+  bool needx = SWAP ? false : !D.logP_ok[chain];
+  double xn = (!SWAP && lane < kNp) ? D.x[(size_t)chain * kNp + lane] : 0.0;
   const double temp = D.temp[j];
   int iset = D.iset[jl];
   double gset = D.gset[jl];
@@ -491,6 +622,26 @@ __device__ __forceinline__ void propose_group(const Dev& D, int W, int NPAST, lo
   if (sgt < n8) sch_dst[sgt] = sv;
   for (long long q = sgt + sgs; q < n8; q += sgs)
     sch_dst[q] = __hip_atomic_load(sch_src + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  if constexpr (SWAP) {
+    if (act) {  // the previous iteration's swaps for this slot, then its state
+      int nacc = 0;
+#ifdef HB_DS_CLOCKS
+      unsigned long long* rpp = rp_;
+#else
+      unsigned long long* rpp = nullptr;
+#endif
+      chain = replay_prev_swaps(D, SP, W, j, lane, T, scr + (size_t)wv * swap_prev_wave_bytes(SP.cone, SP.maxent),
+                                nacc, rpp);
+      if (lane == 0) {
+        SP.idx_out[j] = chain;
+        if (nacc) D.nsw[jl] += nacc;  // this slot's own counter: no contention
+        if (SP.iter % 100 == 0) D.DEacc_arr[jl] = D.DEtrial_arr[jl] = 0;  // ds_swap_seg's 100-step reset
+        if (j == 0) swap_tail(D, SP.iter, D.par ^ 1, chain);  // slot 0 (one-process samplers own every slot)
+      }
+      needx = !D.logP_ok[chain];
+      xn = lane < kNp ? D.x[(size_t)chain * kNp + lane] : 0.0;
+    }
+  }
   if (act) {  // wave-uniform; every wave reaches the prep group's barriers below
     DS_T(1);
     const double a = S.uniform();
@@ -512,7 +663,7 @@ __device__ __forceinline__ void propose_group(const Dev& D, int W, int NPAST, lo
     if (jmp == 1) {
       if (chain == 0 && lane == 0) {
         D.DEtrial_arr[jl]++;
-        atomicAdd((unsigned long long*)&D.ctr->DEtrial_tot, 1ull);
+        atomicAdd((unsigned long long*)&D.ctr->de_trial_pend[D.par], 1ull);
       }
       // differential_evolution_proposal_parallel (:1091-1140) as compiled (see
       // hb_sampler.cpp de_step: a == 0, the uninitialised c == 0).  The 0.9
@@ -626,14 +777,16 @@ __device__ __forceinline__ void propose_group(const Dev& D, int W, int NPAST, lo
     D.wc[(size_t)jl_s[w] * hbk::kWcDoubles + f] = PL.so[w * hbk::kSoStride + f];
   }
 }
-template <bool PREP>
+template <bool PREP, bool SWAP>
 __global__ __launch_bounds__(64 * kPW) HB_DS_PROPOSE_ATTR void ds_propose(Dev D, int W, int NPAST, long long iter,
                                                        const unsigned long long* __restrict__ sch_src,
-                                                       unsigned long long* __restrict__ sch_dst, long long n8) {
+                                                       unsigned long long* __restrict__ sch_dst, long long n8,
+                                                       SwapPrev SP) {
   __shared__ ProposeShared S;
+  extern __shared__ __attribute__((aligned(16))) unsigned char dyn[];  // SWAP: kPW waves' cone scratch
   int j;
   bool act;
-  propose_group<PREP>(D, W, NPAST, iter, sch_src, sch_dst, n8, S, j, act);
+  propose_group<PREP, SWAP>(D, W, NPAST, iter, sch_src, sch_dst, n8, S, j, act, SP, dyn);
 }
 
 // The whole iteration up to the swaps in ONE launch (propose -> records ->
@@ -699,6 +852,7 @@ constexpr int kAccThreads = 256;
 __global__ __launch_bounds__(kAccThreads) void ds_accept(Dev D, int W, int NPAST, long long iter) {
   __shared__ int chain_s[64], acc_s[64];
   const int tid = threadIdx.x, lane = tid;
+  if (blockIdx.x == 0 && D.ecnt_next != nullptr && tid < kOrdBins) D.ecnt_next[tid * kEbinStride] = 0;
   const int j0 = blockIdx.x * 64;  // local slots j0 .. j0 + nw - 1
   const int nw = min(64, D.nl - j0);
   const int k = (int)(iter - (iter / NPAST) * NPAST);
@@ -803,31 +957,6 @@ struct Gathered {
   int pad;
 };
 
-// the per-iteration bookkeeping after the swaps (:551-572, :590, :622-629)
-// by thread 0 of one workgroup; c0 = the chain now in slot 0 (-1: not this
-// rank's slot).  nswap is added by every segment (atomics).
-__device__ __forceinline__ void swap_tail(const Dev& D, long long iter, int c0) {
-  Counters* C = D.ctr;
-  C->acc += C->acc_it;  // hb_sampler_accept's sums over the slots
-  C->cold_acc += C->acc_it;
-  C->DEacc += C->DEacc_tot;
-  C->DEtrial += C->DEtrial_tot;
-  C->acc_it = 0;
-  C->snap[0] = C->acc;
-  C->snap[1] = C->DEacc;
-  C->snap[2] = C->DEtrial;
-  C->snap[3] = C->atrial;
-  if (c0 >= 0 && D.logL[c0] > C->logLmap) {  // :565-572
-    for (int i = 0; i < kNp; ++i) C->xmap[i] = D.x[(size_t)c0 * kNp + i];
-    C->logLmap = D.logL[c0];
-  }
-  C->atrial++;  // :590 and the 100-step reset of :622-629
-  if (iter % 100 == 0) {
-    C->acc = C->atrial = 0;
-    C->DEacc_tot = C->DEtrial_tot = 0;
-  }
-}
-
 // Tempering swaps (ptmcmc :768-817) and the iteration's bookkeeping, one
 // workgroup per segment [sl, sh) of the owned slots.  A level moves a slot's
 // content by one, so after the nlv levels the chains of [sl, sh) come from the
@@ -850,7 +979,7 @@ __global__ __launch_bounds__(kSegThreads) void ds_swap_seg(Dev D, int W, const i
                                                             const double* __restrict__ betas, int nlv, int G,
                                                             long long iter, Gathered X, const double* __restrict__ Ls) {
   extern __shared__ __align__(16) unsigned char smem[];
-  __shared__ int nacc_s;
+  __shared__ unsigned long long nacc_s;
   __shared__ uint64_t exp_s[256];  // exp table for the divergent lookups of the band case
   const int tid = threadIdx.x, g = blockIdx.x;
   const int lo = D.lo, hi = D.lo + D.nl;
@@ -913,13 +1042,20 @@ __global__ __launch_bounds__(kSegThreads) void ds_swap_seg(Dev D, int W, const i
       }
     }
   }
-  if (tid == 0) nacc_s = 0;
+  if (tid == 0) nacc_s = 0ull;
   __syncthreads();
   // the levels.  One attempt (:782-812): exp(x) >= beta decided by x against
   // ln(beta) outside a band of 1e-12 (1 + |ln beta|), far wider than the ulp
   // errors of the host log and of exp; inside the band (or beta = 0, NaN x)
   // the glibc-exact exp is compared with beta itself
-  int nacc = 0;
+  long long nacc = 0;
+  for (int s = sl + tid; s < sh; s += kSegThreads) {  // the deferred replays' counts of these slots
+    const long long v = D.nsw[s - lo];
+    if (v) {
+      nacc += v;
+      D.nsw[s - lo] = 0;
+    }
+  }
   for (int lv = 0; lv < nlv; ++lv) {
     const int e0 = soff[g * nlv + lv] - eb, e1 = soff[g * nlv + lv + 1] - eb;
     for (int q = e0 + tid; q < e1; q += kSegThreads) {
@@ -944,15 +1080,14 @@ __global__ __launch_bounds__(kSegThreads) void ds_swap_seg(Dev D, int W, const i
     }
     __syncthreads();
   }
-  if (nacc) atomicAdd(&nacc_s, nacc);
+  if (nacc) atomicAdd(&nacc_s, (unsigned long long)nacc);
   for (int s = sl + tid; s < sh; s += kSegThreads) D.idx_out[s] = cC[s - clo];
   if (iter % 100 == 0)
     for (int s = sl + tid; s < sh; s += kSegThreads) D.DEacc_arr[s - lo] = D.DEtrial_arr[s - lo] = 0;
-  if (g == 0 && D.ecnt != nullptr && tid < kOrdBins) D.ecnt[tid * kEbinStride] = 0;  // the eval launch read them
   __syncthreads();
   if (tid == 0) {
-    if (nacc_s) atomicAdd((unsigned long long*)&D.ctr->nswap, (unsigned long long)nacc_s);
-    if (g == 0) swap_tail(D, iter, lo == 0 ? cC[0 - clo] : -1);
+    if (nacc_s) atomicAdd((unsigned long long*)&D.ctr->nswap, nacc_s);
+    if (g == 0) swap_tail(D, iter, D.par, lo == 0 ? cC[0 - clo] : -1);
   }
 }
 
@@ -1060,6 +1195,24 @@ struct hb_dsampler {
   int step_prio = 0;  // the propose stage's s_setprio (HB_DS_STEP_PRIO, A/B knob)
   double* d_lslot = nullptr; // [W] logL by slot after the Hastings test (one-process samplers)
   bool lslot_now = false;    // this iteration's fused Hastings test wrote d_lslot
+  int* ecnt_buf[2] = {nullptr, nullptr};  // e-bin counters of even / odd iterations (Dev::ecnt)
+  long long n_iter = 0;      // iterations begun (their parity: Dev::par, ecnt_buf)
+  // Deferred swaps (one-process samplers on the ds_propose path): iteration
+  // pend_iter's tempering swaps are replayed by the next ds_propose
+  // (SwapPrev) instead of their own ds_swap_seg launch; ds_flush launches them
+  // before anything reads the state (gather, download, sync, event drains).
+  // HB_DS_DEFER=0 (A/B knob): never.
+  bool defer = false;
+  bool pend_on = false;
+  int pend_slot = -1;
+  long long pend_iter = -1;
+  bool pend_lslot = false;
+  int pend_par = 0;
+  // a schedule the current iteration's ds_propose consumed (deferred swaps):
+  // released in ds_end, after the likelihood launch, so the ring event (a
+  // cache-flushing barrier packet) does not sit between ds_propose and it
+  int rel_slot = -1;
+  long long rel_q = -1;
   // host timers [s]: producer work (all threads), waits for a schedule, issue
   double t_prod = 0.0, t_wait = 0.0, t_issue = 0.0;
   // the iteration between step_begin and step_end
@@ -1099,6 +1252,7 @@ struct hb_dsampler {
 };
 
 static int ds_upload(hb_dsampler* d, const int* chain_of_slot);
+static int ds_flush(hb_dsampler* d);
 
 // Puts the sampler into its sticky failed state (first message wins) and
 // wakes every waiter (producers and a ds_begin waiting for a schedule).
@@ -1353,16 +1507,20 @@ static hb_dsampler* ds_create(hb_sampler* s, hb_ctx* ctx, const int* chain_of_sl
       (e = d->alloc(&D.logPy, Nz)) || (e = d->alloc(&D.alpha2, Nz)) || (e = d->alloc(&D.logLy, Nz)) ||
       (e = d->alloc(&D.jump, Nz)) || (e = d->alloc(&D.jtype, Nz)) ||
       (e = d->alloc(&D.hist, Nz * (size_t)d->NPAST * kNp)) || (e = d->alloc(&D.DEacc_arr, Nz)) ||
-      (e = d->alloc(&D.DEtrial_arr, Nz)) || (e = d->alloc(&D.ctr, 1)) || (e = d->alloc(&D.ev, (size_t)kEvCap)) ||
+      (e = d->alloc(&D.DEtrial_arr, Nz)) || (e = d->alloc(&D.nsw, Nz)) || (e = d->alloc(&D.ctr, 1)) || (e = d->alloc(&D.ev, (size_t)kEvCap)) ||
       (e = d->alloc(&d->d_xs, Nz * kNp)) || (e = d->alloc(&d->d_ls, Nz)) || (e = d->alloc(&d->d_ps, Nz)) ||
       (e = d->alloc(&d->d_ok, Nz)) || (e = d->alloc(&D.hs, Wz)) || (e = d->alloc(&d->d_params, 1)))
     return fail("hipMalloc", e);
   D.P = d->d_params;
+  if ((e = hipMemsetAsync(D.nsw, 0, sizeof(long long) * Nz, d->st))) return fail("hipMemset", e);
   // eval order by e bins (AccArgs::ecnt) up to kEvalOrdMax owned slots
   if (Nz <= (size_t)kEvalOrdMax && !d->no_eord) {
-    if ((e = d->alloc(&D.ecnt, (size_t)kOrdBins * kEbinStride)) || (e = d->alloc(&D.elist, (size_t)kOrdBins * Nz)))
+    if ((e = d->alloc(&D.ecnt, 2 * (size_t)kOrdBins * kEbinStride)) || (e = d->alloc(&D.elist, (size_t)kOrdBins * Nz)))
       return fail("hipMalloc", e);
-    if ((e = hipMemsetAsync(D.ecnt, 0, sizeof(int) * kOrdBins * kEbinStride, d->st))) return fail("hipMemset", e);
+    if ((e = hipMemsetAsync(D.ecnt, 0, 2 * sizeof(int) * kOrdBins * kEbinStride, d->st))) return fail("hipMemset", e);
+    d->ecnt_buf[0] = D.ecnt;
+    d->ecnt_buf[1] = D.ecnt + (size_t)kOrdBins * kEbinStride;
+    D.ecnt_next = d->ecnt_buf[1];
   }
   // records in ds_propose's epilogue while the slots fit one resident round
   // of its waves at that occupancy (4 per SIMD, 16 per CU); HB_DS_FUSED_PREP=0/1 forces
@@ -1402,6 +1560,8 @@ static hb_dsampler* ds_create(hb_sampler* s, hb_ctx* ctx, const int* chain_of_sl
   {
     const bool one = !d->xchg && d->lo == 0 && d->nl == W;
     if (one && (e = d->alloc(&d->d_lslot, Wz))) return fail("hipMalloc", e);
+    const char* df = getenv("HB_DS_DEFER");
+    d->defer = one && !d->step && (df ? atoi(df) != 0 : true);
   }
   {
     const size_t G = (size_t)d->nseg, segmin = std::max<size_t>(1, (size_t)d->nl / G);
@@ -1546,6 +1706,7 @@ static int ds_drain_events(hb_dsampler* d);
 extern "C" int hb_dsampler_download(hb_dsampler* d) {
   if (!d) return hbx_set_error("hb_dsampler_download: null");
   if (const int rc = ds_check_failed(d, "hb_dsampler_download")) return rc;
+  if (const int rc = ds_flush(d)) return rc;
   const HbSamplerView& v = d->v;
   const int nl = d->nl;
   const size_t Nz = (size_t)nl;
@@ -1606,6 +1767,7 @@ extern "C" int hb_dsampler_download(hb_dsampler* d) {
 }
 
 static int ds_drain_events(hb_dsampler* d) {
+  if (const int rc = ds_flush(d)) return rc;
   DS_TRY(hipMemcpyAsync(d->h_ctr, d->D.ctr, sizeof(Counters), hipMemcpyDeviceToHost, d->st), "events");
   DS_TRY(hipStreamSynchronize(d->st), "events");
   const int n = std::min(d->h_ctr->nev, kEvCap);
@@ -1644,6 +1806,7 @@ __global__ __launch_bounds__(kBlk) void ds_scatter_logl(Dev D, const double* __r
 // tracker seeded with chain 0's state (:342; the rank owning chain 0)
 extern "C" int hb_dsampler_init_logl(hb_dsampler* d) {
   if (!d) return hbx_set_error("hb_dsampler_init_logl: null");
+  if (const int rc = ds_flush(d)) return rc;
   DS_TRY(hipSetDevice(d->device), "hipSetDevice");
   if (d->R == 1) {
     const int rc = hb_loglik_batch_dev(d->ctx, d->D.x, d->W, d->D.logL, (void*)d->st);
@@ -1686,6 +1849,62 @@ extern "C" int hb_dsampler_host_times(const hb_dsampler* d, double* out4) {
 // thread built it into the pinned ring), proposals, likelihood + Hastings
 // test of the owned slots; exchanging samplers also pack the rank's
 // all-gather contribution into send
+// Iteration q's schedule (ring slot `slot`) is consumed by a launch now on the
+// sampler's stream: its producer may reuse the slot once the next recorded
+// event has completed.
+static int ds_release(hb_dsampler* d, int slot, long long q) {
+  if ((q + 1) % d->ev_every == 0) DS_TRY(hipEventRecord(d->ev_used[slot], d->st), "schedule ring");
+  {
+    std::lock_guard<std::mutex> lk(d->smu);
+    d->slots[slot].released = true;
+    d->q_issued = q + 1;
+  }
+  d->scv.notify_all();
+  return 0;
+}
+// iteration `iter`'s tempering swaps and bookkeeping by ds_swap_seg (its
+// schedule in ring slot `slot`, `par` its parity); X: the all-gather of an
+// exchanging sampler (null: one process, logL by slot from d_lslot when lslot)
+static int ds_swap_launch(hb_dsampler* d, int slot, long long iter, bool lslot, int par, const Gathered* X) {
+  const hb_dsampler::Slot sl = d->slots[slot];  // written by its producer before the ready flag
+  const int G = d->nseg;
+  const unsigned char* base = d->d_sched[slot];
+  const int* d_soff = reinterpret_cast<const int*>(base);
+  const SwapEnt* d_ent = reinterpret_cast<const SwapEnt*>(base + sched_ent_off((size_t)G, (size_t)sl.nlv));
+  const double* d_beta =
+      reinterpret_cast<const double*>(base + sched_beta_off((size_t)G, (size_t)sl.nlv, (size_t)sl.nent));
+  // LDS: the widest cone's (logL, chain, pair factor) and the largest
+  // segment's attempts
+  const size_t wc_max = (size_t)(d->nl + G - 1) / G + 2 * (size_t)sl.nlv;
+  const size_t lds = sizeof(SwapEnt) * (size_t)sl.maxent + (2 * sizeof(double) + sizeof(int)) * wc_max;
+  Dev Dx = d->D;
+  Dx.par = par;
+  if (X) {
+    ds_swap_seg<true><<<G, kSegThreads, lds, d->st>>>(Dx, d->W, d_soff, d_ent, d_beta, sl.nlv, G, iter, *X, nullptr);
+  } else {
+    const Gathered none{nullptr, 0, 1, 0, 0, 0};
+    ds_swap_seg<false><<<G, kSegThreads, lds, d->st>>>(Dx, d->W, d_soff, d_ent, d_beta, sl.nlv, G, iter, none,
+                                                       lslot ? d->d_lslot : nullptr);
+  }
+  DS_TRY(hipGetLastError(), "ds_swap_seg");
+  return 0;
+}
+// the deferred swaps of the last iteration by their own launch (before
+// anything reads the sampler's state)
+static int ds_flush(hb_dsampler* d) {
+  if (!d->pend_on) return 0;
+  d->pend_on = false;
+  DsFailGuard guard{d};
+  DS_TRY(hipSetDevice(d->device), "hipSetDevice");
+  if (const int rc = ds_swap_launch(d, d->pend_slot, d->pend_iter, d->pend_lslot, d->pend_par, nullptr)) return rc;
+  std::swap(d->D.idx, d->D.idx_out);
+  if (const int rc = ds_release(d, d->pend_slot, d->pend_iter)) return rc;
+  guard.armed = false;
+  return 0;
+}
+// per-wave LDS of the deferred swaps' replay in ds_propose, at most
+constexpr size_t kSwapPrevLdsMax = 32768;
+
 static long ds_begin(hb_dsampler* d, long iter, double* send, long cap) {
   const int W = d->W;
   const Dev& D = d->D;
@@ -1712,6 +1931,43 @@ static long ds_begin(hb_dsampler* d, long iter, double* send, long cap) {
     return hbx_set_error("hb_dsampler: an iteration's swap schedule exceeds its buffer (more than 64 levels)");
   const size_t used_bytes = sched_bytes((size_t)d->nseg, (size_t)sl.nlv, (size_t)sl.nent);  // a multiple of 8
   const int NPAST = d->NPAST, nl = d->nl;
+  // the iteration's parity: its e-bin counters and DE-trial slot
+  {
+    const int par = (int)(d->n_iter & 1);
+    d->D.par = par;
+    if (d->ecnt_buf[0]) {
+      d->D.ecnt = d->ecnt_buf[par];
+      d->D.ecnt_next = d->ecnt_buf[par ^ 1];
+    }
+    d->n_iter++;
+  }
+  // the previous iteration's deferred swaps: replayed by this ds_propose when
+  // their per-wave scratch fits, else by their own launch first
+  SwapPrev SP{};
+  size_t sp_lds = 0;
+  bool fuse = false;
+  if (d->pend_on) {
+    const hb_dsampler::Slot& ps = d->slots[d->pend_slot];
+    const int cone = 2 * ps.nlv + 1;
+    sp_lds = (size_t)kPW * swap_prev_wave_bytes(cone, ps.maxent);
+    if (!d->step && sp_lds <= kSwapPrevLdsMax) {
+      const int G = d->nseg;
+      const unsigned char* base = d->d_sched[d->pend_slot];
+      SP.soff = reinterpret_cast<const int*>(base);
+      SP.ent = reinterpret_cast<const SwapEnt*>(base + sched_ent_off((size_t)G, (size_t)ps.nlv));
+      SP.betas = reinterpret_cast<const double*>(base + sched_beta_off((size_t)G, (size_t)ps.nlv, (size_t)ps.nent));
+      SP.Ls = d->pend_lslot ? d->d_lslot : nullptr;
+      SP.idx_out = D.idx_out;
+      SP.iter = d->pend_iter;
+      SP.nlv = ps.nlv;
+      SP.G = G;
+      SP.cone = cone;
+      SP.maxent = ps.maxent;
+      fuse = true;
+    } else if (const int rc = ds_flush(d)) {
+      return rc;
+    }
+  }
   // proposals, and in their epilogue the likelihood's walker records (the
   // context's workspace, looked up per launch: another caller may have grown it)
   Dev Dp = D;
@@ -1746,11 +2002,25 @@ static long ds_begin(hb_dsampler* d, long iter, double* send, long cap) {
     DS_TRY(hipGetLastError(), "ds_step");
     d->lslot_now = acc.Lslot != nullptr;
   } else {
-    if (d->fused_prep)
-      ds_propose<true><<<(nl + kPW - 1) / kPW, 64 * kPW, 0, s>>>(Dp, W, NPAST, (long long)iter, sch_src, sch_dst, n8);
-    else
-      ds_propose<false><<<(nl + kPW - 1) / kPW, 64 * kPW, 0, s>>>(Dp, W, NPAST, (long long)iter, sch_src, sch_dst, n8);
+    const unsigned pg = (unsigned)((nl + kPW - 1) / kPW);
+    if (fuse) {
+      Dp.idx = D.idx;  // the previous iteration's index[] (the replay's input)
+      if (d->fused_prep)
+        ds_propose<true, true><<<pg, 64 * kPW, sp_lds, s>>>(Dp, W, NPAST, (long long)iter, sch_src, sch_dst, n8, SP);
+      else
+        ds_propose<false, true><<<pg, 64 * kPW, sp_lds, s>>>(Dp, W, NPAST, (long long)iter, sch_src, sch_dst, n8, SP);
+    } else if (d->fused_prep) {
+      ds_propose<true, false><<<pg, 64 * kPW, 0, s>>>(Dp, W, NPAST, (long long)iter, sch_src, sch_dst, n8, SwapPrev{});
+    } else {
+      ds_propose<false, false><<<pg, 64 * kPW, 0, s>>>(Dp, W, NPAST, (long long)iter, sch_src, sch_dst, n8, SwapPrev{});
+    }
     DS_TRY(hipGetLastError(), "ds_propose");
+    if (fuse) {  // this iteration reads the index[] the replay wrote; the schedule is consumed
+      d->pend_on = false;
+      std::swap(d->D.idx, d->D.idx_out);
+      d->rel_slot = d->pend_slot;
+      d->rel_q = d->pend_iter;
+    }
     if (!d->fused_prep) {
       const int rc = hb_prepare_dev(d->ctx, D.y, nl, (void*)s);
       if (rc) return rc;
@@ -1759,7 +2029,7 @@ static long ds_begin(hb_dsampler* d, long iter, double* send, long cap) {
     // (hb_accept.hpp); ds_accept only where the plan has no one-wave kernel
     AccArgs acc{D.idx, D.logL, D.logP, D.logPy, D.temp, D.alpha2, D.jump, D.jtype, D.x, D.y, D.hist,
                 D.DEacc_arr, D.ctr, D.ev, d->P.log_on, NPAST, (long long)iter, d->lo, 0,
-                D.ecnt, D.elist, nl, 0, d->d_lslot};  // Lslot: null for exchanging samplers
+                D.ecnt, D.elist, nl, 0, d->d_lslot, D.ecnt_next};  // Lslot: null for exchanging samplers
     int rc = hbx_loglik_accept_dev(d->ctx, D.y, nl, D.logLy, &acc, (void*)s);
     d->lslot_now = rc == 0 && acc.Lslot != nullptr;
     if (rc == 1) {
@@ -1792,9 +2062,6 @@ static long ds_begin(hb_dsampler* d, long iter, double* send, long cap) {
 // second half: import the all-gather (exchanging samplers), tempering swaps,
 // bookkeeping
 static int ds_end(hb_dsampler* d, long iter, const double* recv, long n) {
-  const int W = d->W;
-  const Dev& D = d->D;
-  hipStream_t s = d->st;
   if (const int rc = ds_check_failed(d, "hb_dsampler_step_end")) return rc;
   if (d->cur_iter != iter) return hbx_set_error("hb_dsampler_step_end: no step_begin for this iteration");
   // a caller mistake is recoverable (step_end may be called again with the
@@ -1809,38 +2076,36 @@ static int ds_end(hb_dsampler* d, long iter, const double* recv, long n) {
   const hb_dsampler::Slot sl = d->slots[slot];  // written by its producer before the ready flag
   d->cur_iter = -1;
   DS_TRY(hipSetDevice(d->device), "hipSetDevice");
-  const int G = d->nseg;
-  const unsigned char* base = d->d_sched[slot];
-  const int* d_soff = reinterpret_cast<const int*>(base);
-  const SwapEnt* d_ent = reinterpret_cast<const SwapEnt*>(base + sched_ent_off((size_t)G, (size_t)sl.nlv));
-  const double* d_beta =
-      reinterpret_cast<const double*>(base + sched_beta_off((size_t)G, (size_t)sl.nlv, (size_t)sl.nent));
-  // LDS: the widest cone's (logL, chain, pair factor) and the largest
-  // segment's attempts
-  const size_t wc_max = (size_t)(d->nl + G - 1) / G + 2 * (size_t)sl.nlv;
-  const size_t lds = sizeof(SwapEnt) * (size_t)sl.maxent + (2 * sizeof(double) + sizeof(int)) * wc_max;
-  if (d->xchg) {
-    const Gathered X{recv, (long long)n, d->R, d->rank, d->m, 0};
-    ds_swap_seg<true><<<G, kSegThreads, lds, s>>>(D, W, d_soff, d_ent, d_beta, sl.nlv, G, (long long)iter, X, nullptr);
-    DS_TRY(hipGetLastError(), "ds_swap_seg");
+  if (d->rel_slot >= 0) {  // the previous iteration's schedule, consumed by this ds_propose
+    const int rs = d->rel_slot;
+    d->rel_slot = -1;
+    if (const int rc = ds_release(d, rs, d->rel_q)) return rc;
+  }
+  if (d->defer && !d->xchg) {
+    // the swaps wait for the next ds_propose (SwapPrev) or ds_flush
+    d->pend_on = true;
+    d->pend_slot = slot;
+    d->pend_iter = iter;
+    d->pend_lslot = d->lslot_now;
+    d->pend_par = d->D.par;
   } else {
-    const Gathered X{nullptr, 0, 1, 0, 0, 0};
-    ds_swap_seg<false><<<G, kSegThreads, lds, s>>>(D, W, d_soff, d_ent, d_beta, sl.nlv, G, (long long)iter, X,
-                                                   d->lslot_now ? d->d_lslot : nullptr);
-    DS_TRY(hipGetLastError(), "ds_swap_seg");
+    if (d->xchg) {
+      const Gathered X{recv, (long long)n, d->R, d->rank, d->m, 0};
+      if (const int rc = ds_swap_launch(d, slot, iter, false, d->D.par, &X)) return rc;
+    } else if (const int rc = ds_swap_launch(d, slot, iter, d->lslot_now, d->D.par, nullptr)) {
+      return rc;
+    }
+    std::swap(d->D.idx, d->D.idx_out);  // the next iteration reads what the swaps wrote
+    if (const int rc = ds_release(d, slot, sl.q)) return rc;
   }
-  std::swap(d->D.idx, d->D.idx_out);  // the next iteration reads what the swaps wrote
-  if ((sl.q + 1) % d->ev_every == 0) DS_TRY(hipEventRecord(d->ev_used[slot], s), "schedule ring");
-  {
-    std::lock_guard<std::mutex> lk(d->smu);
-    d->slots[slot].released = true;
-    d->q_issued = sl.q + 1;
-  }
-  d->q_cons = sl.q + 1;  // the iteration's swap draws are now on the stream
+  d->q_cons = sl.q + 1;  // the iteration's swap draws are on the stream, or deferred to the next ds_propose
   guard.armed = false;
   d->scv.notify_all();
   d->t_issue += now_s() - t0;
-  if (d->P.log_on && iter > 10000 && iter % 100 == 0) return ds_drain_events(d);
+  if (d->P.log_on && iter > 10000 && iter % 100 == 0) {
+    if (const int rc = ds_flush(d)) return rc;
+    return ds_drain_events(d);
+  }
   return 0;
 }
 
@@ -1872,6 +2137,7 @@ extern "C" int hb_dsampler_step(hb_dsampler* d, long iter) {
 extern "C" int hb_dsampler_gather(hb_dsampler* d, double* x_slots, double* logl_slots, double* xmap,
                                   double* logLmap, long* stats4) {
   if (!d) return hbx_set_error("hb_dsampler_gather: null");
+  if (const int rc = ds_flush(d)) return rc;
   const int nl = d->nl;
   hipStream_t s = d->st;
   DS_TRY(hipSetDevice(d->device), "hipSetDevice");
@@ -1904,6 +2170,7 @@ extern "C" int hb_debug_dp_clocks(unsigned long long* out, int nslots) {
 #endif
 extern "C" int hb_dsampler_sync(hb_dsampler* d) {
   if (!d) return hbx_set_error("hb_dsampler_sync: null");
+  if (const int rc = ds_flush(d)) return rc;
   DS_TRY(hipStreamSynchronize(d->st), "sync");
   return 0;
 }

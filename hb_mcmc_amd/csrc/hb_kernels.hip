@@ -615,6 +615,8 @@ __global__ __launch_bounds__(64 * WPB * WPW) HB_WPE_ATTR void hb_eval_wave_kerne
   }
   int wv = slot;
   if (ACC && hst.ecnt != nullptr && valid) wv = hbds::eval_slot_by_e(hst, slot, lane);  // device sampler
+  if (ACC && hst.ecnt_next != nullptr && slot == 0 && lane < hbds::kOrdBins)
+    hst.ecnt_next[lane * hbds::kEbinStride] = 0;  // the next iteration's e-bin counters
   if (!valid) return;
   // the select's survivors: past the slab, or (fused launch) inside it, past
   // the histogram (the slab is dead once the keys are in registers)

@@ -51,7 +51,7 @@ with DeviceSampler(S, L) as D:
     D.sync()
 lib = _lib.lib()
 if a.propose:
-    NW = 12
+    NW = 16
     buf = (C.c_ulonglong * (NW * W))()
     assert lib.hb_debug_dp_clocks(buf, W) == 0
     c = np.frombuffer(buf, dtype=np.uint64).reshape(W, NW)
@@ -78,6 +78,13 @@ if a.propose:
                        "life_us_median": float(np.median(life[np.argsort(rt1)[-64:]])),
                        "start_us_median": float(np.median((rt0[np.argsort(rt1)[-64:]] - k0) / 100.0))},
            "shader_clock_ghz_median": float(np.median((ck[:, 7] - ck[:, 0]) / np.maximum(rt1 - rt0, 1)) * 0.1)}
+    rp = c[:, 12:16].astype(np.int64)
+    if (rp[:, 0] > 0).any():  # the deferred-swap replay (defer builds): staging, levels, entries, levels
+        m = rp[:, 0] > 0
+        res["swap_replay"] = {"staging_cycles_pct": [float(x) for x in np.percentile((rp[m, 1] - rp[m, 0]), [5, 50, 95])],
+                              "levels_cycles_pct": [float(x) for x in np.percentile((rp[m, 2] - rp[m, 1]), [5, 50, 95])],
+                              "entries_pct": [float(x) for x in np.percentile(rp[m, 3] & 0xffffffff, [5, 50, 95, 100])],
+                              "nlv": [int(x) for x in np.unique(rp[m, 3] >> 32)]}
     print(json.dumps(res, indent=1))
     S.close()
     L.close()
