@@ -496,16 +496,16 @@ __device__ __forceinline__ int replay_prev_swaps(const Dev& D, const SwapPrev& S
   // the segment's level offsets (nlv + 1 <= 65 of them: lane l holds level l's
   // start, lane 64 the end read apart), then its attempts and the cone's slots
   const int so = lane <= nlv ? SP.soff[g * nlv + lane] : 0;
-  const int eb = __builtin_amdgcn_readfirstlane(so);
-  const int eend = nlv < 64 ? __builtin_amdgcn_readlane(so, nlv) : SP.soff[g * nlv + nlv];
-  const int ne = eend - eb;
-  for (int q = lane; q < ne; q += 64) sE[q] = SP.ent[eb + q];
-  for (int i = lane; i < Wc; i += 64) {
+  for (int i = lane; i < Wc; i += 64) {  // issued beside the offsets' load (independent of it)
     const int c = D.idx[clo + i];
     cC[i] = c;
     cH[i] = D.hs[clo + i];
     cL[i] = SP.Ls != nullptr ? SP.Ls[clo + i] : D.logL[c];
   }
+  const int eb = __builtin_amdgcn_readfirstlane(so);
+  const int eend = nlv < 64 ? __builtin_amdgcn_readlane(so, nlv) : SP.soff[g * nlv + nlv];
+  const int ne = eend - eb;
+  for (int q = lane; q < ne; q += 64) sE[q] = SP.ent[eb + q];
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
