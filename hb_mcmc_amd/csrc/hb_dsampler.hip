@@ -1571,7 +1571,15 @@ static hb_dsampler* ds_create(hb_sampler* s, hb_ctx* ctx, const int* chain_of_sl
   for (int r = 0; r < hb_dsampler::R_RING; ++r) {
     if ((e = d->alloc(&d->d_sched[r], d->sched_cap))) return fail("hipMalloc", e);
     if ((e = hipHostMalloc((void**)&d->pin[r], d->sched_cap, hipHostMallocDefault))) return fail("pinned", e);
-    if ((e = hipEventCreateWithFlags(&d->ev_used[r], hipEventDisableTiming))) return fail("event", e);
+    // the event only tells the producer that the GPU has finished reading the
+    // slot (ds_propose's pinned-source loads): no system-scope release is
+    // needed for that, and without it the barrier packet writes back and
+    // invalidates no caches before the next launch (HB_DS_EV_FENCE=1, A/B
+    // knob: with the fence)
+    static const bool ev_fence = getenv("HB_DS_EV_FENCE") != nullptr && atoi(getenv("HB_DS_EV_FENCE")) != 0;
+    if ((e = hipEventCreateWithFlags(&d->ev_used[r],
+                                     hipEventDisableTiming | (ev_fence ? 0u : (unsigned)hipEventDisableSystemFence))))
+      return fail("event", e);
   }
   if ((e = hipHostMalloc((void**)&d->h_ctr, sizeof(Counters), hipHostMallocDefault))) return fail("pinned", e);
   if ((e = hipHostMalloc((void**)&d->h_ev, sizeof(Event) * kEvCap, hipHostMallocDefault))) return fail("pinned", e);
