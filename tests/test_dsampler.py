@@ -197,3 +197,53 @@ def test_device_sampler_state_equals_host_sampler(W, niter, ladder, n):
     assert any(r.tobytes() not in init for r in hx), "no proposal accepted: the accept branch never ran"
     if n == 256:  # the sharper 2500-cadence posterior may reject every cold proposal in 30 iterations
         assert hs["cold_acc"] > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("W", [64, 4096])
+def test_deferred_swaps_equal_swap_launches(W, monkeypatch):
+    """The tempering swaps deferred into the next ds_propose (HB_DS_DEFER,
+    one-slot cone replays, per-slot swap counters, parity-split DE counts)
+    against their own ds_swap_seg launch per iteration (HB_DS_DEFER=0): states,
+    logL, chain ids and every counter bit for bit, with gathers after
+    iterations 0, 7 (odd: the parity-split counters) and 100 (the 100-step
+    resets) flushing the pending swaps mid-run, and past NPAST so that
+    differential-evolution proposals (chain 0's DE trials) occur."""
+    from hb_mcmc_amd import synth
+    from hb_mcmc_amd.dsampler import DeviceSampler
+    from hb_mcmc_amd.likelihood import HBLikelihood
+    from hb_mcmc_amd.sampler import SlotSampler
+
+    n, niter, npast = 256, 130, 20
+    t = synth.cadences(n)
+    with HBLikelihood(t, np.ones(n), np.ones(n)) as tmp:
+        truth = tmp.light_curve(synth.THETA_STAR[None, :])[0]
+    s = np.full(n, 1e-3)
+    f = truth + s * synth.noise(n)
+    runs = []
+    for defer in ("1", "0"):
+        monkeypatch.setenv("HB_DS_DEFER", defer)
+        with HBLikelihood(t, f, s) as L:
+            L.reserve(W)
+            S = SlotSampler(niter, W, synth.THETA_STAR[2], 0, W, run=3, npast=npast, ladder=1, nthreads=8)
+            seen = []
+            with DeviceSampler(S, L) as D:
+                D.init_logl()
+                for it in range(niter):
+                    D.step(it)
+                    if it in (0, 7, 100):
+                        seen.append(D.gather())
+                seen.append(D.gather())
+                D.download()
+            xs, ls, cid = S.get()
+            runs.append((seen, xs, ls, cid, S.stats()))
+            S.close()
+    (sa, xa, la, ca, sta), (sb, xb, lb, cb, stb) = runs
+    assert np.array_equal(xa, xb) and np.array_equal(la, lb) and np.array_equal(ca, cb)
+    assert sta == stb and sta["nswap"] > 0 and sta["DEtrial"] > 0
+    for ga, gb in zip(sa, sb):
+        for u, v in zip(ga, gb):
+            if isinstance(u, np.ndarray):
+                assert np.array_equal(u, v)
+            else:
+                assert u == v
