@@ -31,8 +31,8 @@ class HBMIError(RuntimeError):
 # sources that determine the likelihood kernels' machine code: the PMC counter
 # file (profiles/pmc_counters.json) is keyed by this id, so bench.py only
 # quotes counters that were measured on the kernels it runs
-KERNEL_SOURCES = ("hb_kernels.hip", "hb_device.hpp", "hb_math.hpp", "hb_internal.hpp", "hb_accept.hpp",
-                  "hb_prep.hpp", "hb_glibc_math.hpp", "hb_glibc_tables.inc", "Makefile")
+KERNEL_SOURCES = ("hb_kernels.hip", "hb_wave.hpp", "hb_device.hpp", "hb_math.hpp", "hb_internal.hpp",
+                  "hb_accept.hpp", "hb_prep.hpp", "hb_glibc_math.hpp", "hb_glibc_tables.inc", "Makefile")
 
 
 def kernel_build_id() -> str:
