@@ -1,9 +1,11 @@
 """Pin the oracle (oracle/hb_oracle.c) against vectors the REFERENCE produced
 (tests/golden/make_golden.py): bit-exact, same box / same glibc libm."""
+import os
+
 import numpy as np
 import pytest
 
-from conftest import golden
+from conftest import ROOT, golden
 
 
 def same(a, b):
@@ -104,14 +106,19 @@ def test_write_lc_to_file_bytes(oracle, tmp_path):
         assert path.read_bytes() == g[f"file{k}"].tobytes()
 
 
-def test_eccentricity_above_one_gives_nan_logl(oracle):
+def test_eccentricity_above_one_gives_nan_logl(oracle, tmp_path):
     """The premise of the eval kernels' |e| > 1 exit (hb_device.hpp
     logl_without_light_curve): for every walker with 1 - e^2 < 0 that is not
     in Roche overflow the reference's loglikelihood is NaN, whatever the other
     parameters -- checked on the reference build itself (oracle/_ref, when
-    built here) and on the oracle, over 600 prior-box walkers with e in
-    (1, 50] and e < -1, on a synthetic and a real light curve."""
-    from oracle import Reference, reference_available
+    built here; in a child process, since an in-process load would bind its
+    loglikelihood() to an already loaded libhbmi.so's global symbol) and on
+    the oracle, over 600 prior-box walkers with e in (1, 50] and e < -1, on a
+    synthetic and a real light curve."""
+    import subprocess
+    import sys
+
+    from oracle import reference_available
 
     from hb_mcmc_amd import synth
 
@@ -122,13 +129,22 @@ def test_eccentricity_above_one_gives_nan_logl(oracle):
     P[400:, 3] = -1.0 - rng.random(200) * 10.0
     g = golden("lc_real231937440.npz")
     sets = [synth.dataset(300, oracle.light_curve), (g["t"], g["f"], g["s"])]
-    impls = [oracle] + ([Reference()] if reference_available() else [])
-    for t, f, s in sets:
-        for impl in impls:
-            ll = impl.loglike_batch(t, f, s, P, synth.MAG_DEFAULT, synth.MAGERR_DEFAULT, 8)
-            pos = P[:, 3] > 1.0
-            assert np.isnan(ll[pos]).all()
-            # e < -1: the periastron a (1 - e) is positive, so Roche may fire and
-            # then wins (likelihood3.c:866-869); otherwise NaN
-            neg = ~pos
-            assert (np.isnan(ll[neg]) | (ll[neg] == -5e14)).all()
+    pos, neg = P[:, 3] > 1.0, P[:, 3] < -1.0
+
+    def check(ll):
+        assert np.isnan(ll[pos]).all()
+        # e < -1: the periastron a (1 - e) is positive, so Roche may fire and
+        # then wins (likelihood3.c:866-869); otherwise NaN
+        assert (np.isnan(ll[neg]) | (ll[neg] == -5e14)).all()
+
+    for k, (t, f, s) in enumerate(sets):
+        check(oracle.loglike_batch(t, f, s, P, synth.MAG_DEFAULT, synth.MAGERR_DEFAULT, 8))
+        if reference_available():
+            np.savez(tmp_path / f"in{k}.npz", t=t, f=f, s=s, P=P, m=synth.MAG_DEFAULT, e=synth.MAGERR_DEFAULT)
+            code = ("import sys, numpy as np; sys.path.insert(0, sys.argv[3]); from oracle import Reference; "
+                    "d = np.load(sys.argv[1]); "
+                    "np.save(sys.argv[2], Reference().loglike_batch(d['t'], d['f'], d['s'], d['P'], d['m'], d['e'], 8))")
+            r = subprocess.run([sys.executable, "-c", code, str(tmp_path / f"in{k}.npz"), str(tmp_path / f"out{k}.npy"),
+                                os.path.join(ROOT, "oracle")], capture_output=True, text=True, timeout=300)
+            assert r.returncode == 0, r.stderr[-2000:]
+            check(np.load(tmp_path / f"out{k}.npy"))
