@@ -51,14 +51,15 @@ if a.fused and L.fused_wpb(w) > 0:  # the fused prologue's marks, wave 0 of ever
     pb = (C.c_ulonglong * (16 * nwg))()
     assert lib.hb_debug_prologue_clocks(pb, nwg) == 0
     pc = np.frombuffer(pb, dtype=np.uint64).reshape(nwg, 16).astype(np.int64)
-    d = pc[:, 1:14] - pc[:, 0:1]
+    # marks 1..12 (13, the records-combined mark, went with the round-5 prologue);
+    # s_memtime is per XCD, so only differences within a workgroup are kept
+    d = pc[:, 1:13] - pc[:, 0:1]
     prologue = {"workgroups": int(nwg), "marks": ["params in LDS", "records in LDS", "after last barrier",
                                                   "table waves done"] +
                                                  [f"role {r} phase 1 done" for r in range(4)] +
-                                                 [f"role {r} phase 2 done" for r in range(4)] + ["records combined"],
+                                                 [f"role {r} phase 2 done" for r in range(4)],
                 "mean_cycles_from_entry": [float(x) for x in d.mean(axis=0)],
-                "max_cycles_from_entry": [float(x) for x in d.max(axis=0)],
-                "entry_spread_cycles": float(pc[:, 0].max() - pc[:, 0].min())}
+                "max_cycles_from_entry": [float(x) for x in d.max(axis=0)]}
 NW = 10  # words per wave (hb_kernels.hip kClkWords)
 buf = (C.c_ulonglong * (NW * w))()
 assert lib.hb_debug_wave_clocks(buf, w) == 0
@@ -124,7 +125,6 @@ if prologue is not None:  # per workgroup: entry (prologue mark 0) to its last w
     prologue["wg_entry_to_first_eval_start_mean"] = float((starts_wg - ent).mean())
     prologue["wg_entry_to_last_end_mean"] = float((ends_wg - ent).mean())
     prologue["wg_entry_to_last_end_max"] = float((ends_wg - ent).max())
-    prologue["kernel_span_cycles"] = float(ends_wg.max() - ent.min())
 res["prologue"] = prologue
 print(json.dumps(res, indent=1))
 L.close()

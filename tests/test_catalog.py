@@ -150,6 +150,46 @@ def test_catalog_equals_per_target_contexts_and_oracle(hbmi, oracle):
 
 
 @pytest.mark.gpu
+def test_catalog_full_deferred_queue_every_class(hbmi, oracle):
+    """Times shifted by 2.5e5 days send every cadence to the reference-order
+    slow path, so every wave's deferred queue fills to capacity -- in a
+    catalog whose targets span the pair class (N = 1500 and 2048, the last
+    region of the queue buffer, sized by each segment's launch geometry in
+    hb_capi.hip catalog_layout) and the one-wave classes.  logL against the
+    oracle and the same targets in per-target contexts."""
+    from hb_mcmc_amd import synth
+    from hb_mcmc_amd.catalog import Catalog
+    from hb_mcmc_amd.likelihood import HBLikelihood
+
+    targets = []
+    for i, n in enumerate((40, 300, 1024, 1100, 1500, 2048)):
+        t, f, s = synth_target(n, 50 + i, oracle)
+        t = t + 2.5e5
+        assert (2 * np.pi * t / 10.0 ** synth.THETA_STAR[2] >= 2.0 ** 19).all()
+        targets.append((t, f, s))
+    walkers = np.array([9, 16, 24, 8, 40, 33], dtype=np.int32)
+    P = synth.walkers(int(walkers.sum()), seed=77, roche_frac=0.1)
+    with Catalog(targets) as cat:
+        got = cat.loglike(P, walkers)
+    o = 0
+    for k, (t, f, s) in enumerate(targets):
+        w = int(walkers[k])
+        ref = oracle.loglike_batch(t, f, s, P[o:o + w], synth.MAG_DEFAULT, synth.MAGERR_DEFAULT, 8)
+        ok = ~np.isnan(ref)
+        assert np.array_equal(np.isnan(got[o:o + w]), ~ok), k
+        rel = np.abs(got[o:o + w][ok] - ref[ok]) / np.maximum(1.0, np.abs(ref[ok]))
+        assert rel.max(initial=0) <= LOGL_RTOL, (k, rel.max())
+        with HBLikelihood(t, f, s, latency_plan=False) as L:
+            single = L.loglike(P[o:o + w])
+        if 1024 < len(t) < 1281:
+            d = np.abs(got[o:o + w] - single) / np.maximum(1.0, np.abs(single))
+            assert np.nanmax(d, initial=0) <= LOGL_RTOL, k
+        else:
+            assert np.array_equal(got[o:o + w], single, equal_nan=True), k
+        o += w
+
+
+@pytest.mark.gpu
 def test_catalog_rejects_long_light_curves(hbmi, oracle):
     from hb_mcmc_amd import HBMIError
     from hb_mcmc_amd.catalog import Catalog
