@@ -378,39 +378,8 @@ extern "C" int hbx_loglik_accept_dev(hb_ctx* c, const double* d_params, int w, d
   // (the epilogue's registers would spill there, hbk::launch_eval)
   if (c->plan.vpt == 0 || c->plan.wpw != 1 || c->plan.vpt > 16) return 1;
   if (w > c->cap) return set_err_msg("hbx_loglik_accept_dev: W exceeds the prepared workspace");
-  static const bool split = getenv("HB_DS_SPLIT_ACCEPT") != nullptr;  // experiment knob: separate ds_accept
-  if (split) return 1;
   return run_batch(c, d_params, w, d_logl, nullptr, (hipStream_t)stream,
                    static_cast<const hbds::AccArgs*>(acc), false);
-}
-
-// internal (device sampler): LDS bytes each wave of the one-wave likelihood
-// kernel owns (slab, survivors); 0 when the plan has no one-wave path
-extern "C" long hbx_ctx_wave_lds(const hb_ctx* c) {
-  if (!c || c->plan.vpt == 0) return 0;
-  return (long)hbk::wave_lds_bytes(c->plan.slab_bytes, c->plan.vpt, c->plan.wpw);
-}
-
-// internal (device sampler): the one-wave likelihood's inputs (hbk::
-// WaveEvalArgs; valid until the next hb_reserve that grows the workspace)
-extern "C" int hbx_ctx_wave_eval_args(hb_ctx* c, void* out) {
-  if (!c || !out) return set_err_msg("null argument");
-  hbk::WaveEvalArgs e{};
-  e.t = c->d_t;
-  e.ph = c->d_ph;
-  e.f = c->d_f;
-  e.isg = c->d_s;
-  e.rows = c->d_rows;
-  e.n = c->plan.n;
-  e.kth = c->plan.kth;
-  e.gap = c->plan.gap;
-  e.dq = c->d_dq;
-  e.vpt = c->plan.vpt;
-  e.wpw = c->plan.wpw;
-  e.slab_bytes = (int)c->plan.slab_bytes;
-  e.lds_per = c->plan.vpt > 0 ? (int)hbk::wave_lds_bytes(c->plan.slab_bytes, c->plan.vpt, c->plan.wpw) : 0;
-  memcpy(out, &e, sizeof e);
-  return 0;
 }
 
 // internal (device sampler): where its propose epilogue writes the walker

@@ -61,8 +61,6 @@ extern "C" int hbx_ctx_device(const hb_ctx* c);
 extern "C" int hbx_ctx_prep_args(hb_ctx* c, void** wc, void* mags, double** tab_pc);
 extern "C" int hbx_loglik_accept_dev(hb_ctx* c, const double* d_params, int w, double* d_logl, const void* acc,
                                      void* stream);
-extern "C" long hbx_ctx_wave_lds(const hb_ctx* c);
-extern "C" int hbx_ctx_wave_eval_args(hb_ctx* c, void* out);
 
 namespace hbds {
 
@@ -408,9 +406,7 @@ static_assert(kPW == hbk::kPrepRoles, "the propose workgroup is one prep group")
 #else
 #define HB_DS_PROPOSE_ATTR
 #endif
-constexpr bool kDsStepDefault = false;  // ds_step until measured on the GPU (HB_DS_STEP=1 turns it on)
-// LDS of a propose workgroup (ds_propose; ds_step's slabs alias it once the
-// records are written)
+// LDS of a propose workgroup (ds_propose)
 struct ProposeShared {
   uint64_t tab[hbglibc::kTabWords];  // exp / log / pow tables (divergent lookups)
   double gs[kPW][32];
@@ -418,13 +414,8 @@ struct ProposeShared {
   int jl[kPW];
 };
 #ifdef HB_DS_CLOCKS
-// experiment builds only: per wave of the last ds_step launch: s_memtime and
-// s_memrealtime at entry, after the records barrier and at the end, the slot,
-// its temperature and e (read back by hb_debug_ds_clocks); per slot of the
-// last propose: the phase stamps DS_T(0..7) (s_memtime), s_memrealtime at
+// experiment builds only: per slot of the last propose: the phase stamps DS_T(0..7) (s_memtime), s_memrealtime at
 // entry and after the stores, its temperature, proposal type (hb_debug_dp_clocks)
-constexpr int kDsClkWords = 9;
-__device__ unsigned long long ds_clk[kDsClkWords * 65536];
 constexpr int kDpClkWords = 16;
 __device__ unsigned long long dp_clk[kDpClkWords * 65536];
 #endif
@@ -698,9 +689,6 @@ __device__ __forceinline__ void propose_group(const Dev& D, int W, int NPAST, lo
     }
     DS_T(3);
     DS_T(4);
-#ifndef HB_DS_LOST
-#define HB_DS_LOST 1  // A/B knob: 0 = walls and priors of every proposal
-#endif
     // A proposal with e > 1 that the walls leave as it is (e has no upper
     // wall, set_limits :986-1121) gets a NaN logL whatever its other
     // coordinates (hb_device.hpp logl_without_light_curve: 1 - e^2 < 0, Roche
@@ -711,7 +699,7 @@ __device__ __forceinline__ void propose_group(const Dev& D, int W, int NPAST, lo
     const double e_pre = rld(yn, 3);
     const bool e_kept = (e_pre >= P->lim_lo[3] || (P->fl_lo[3] != 1 && P->fl_lo[3] != 2)) &&
                         (e_pre <= P->lim_hi[3] || (P->fl_hi[3] != 1 && P->fl_hi[3] != 2));  // the walls leave e alone
-    const bool lost = HB_DS_LOST && e_pre > 1.0 && e_kept;
+    const bool lost = e_pre > 1.0 && e_kept;  // profiles/r05/r05p_ds_lost_acc_ab.txt
     // walls (:440-467), one coordinate per lane
     if (lane < kNp && (!lost || lane == 3))
       yn = hbwall::apply_wall(yn, P->lim_lo[lane], P->lim_hi[lane], P->fl_lo[lane], P->fl_hi[lane]);
@@ -787,63 +775,6 @@ __global__ __launch_bounds__(64 * kPW) HB_DS_PROPOSE_ATTR void ds_propose(Dev D,
   int j;
   bool act;
   propose_group<PREP, SWAP>(D, W, NPAST, iter, sch_src, sch_dst, n8, S, j, act, SP, dyn);
-}
-
-// The whole iteration up to the swaps in ONE launch (propose -> records ->
-// likelihood -> Hastings test), for a shard of at most one resident round
-// (nl <= 16 per CU) on the one-wave plan: each workgroup's four waves propose
-// their slots (hot rungs first, order[]), turn into the prep group for their
-// records, then each evaluates its own slot's proposal and tests it.  A hot
-// slot's long wall run no longer holds the whole likelihood launch back at a
-// kernel boundary: the SIMD it shares with colder slots' waves runs their
-// likelihoods meanwhile.  The likelihood and the test are those of the
-// separate launch (hb_wave.hpp eval_wave_body, hb_accept.hpp), on the same
-// records, so every result is bit-identical.  LDS: the propose stage's tables
-// and prep scratch, then (after the barrier that publishes the records) the
-// four waves' slabs over the same bytes.  prio: the propose stage's wave
-// priority (s_setprio; the likelihood starts at 3, lowered by the pacer).
-template <int VPT>
-__global__ __launch_bounds__(64 * kPW) __attribute__((amdgpu_waves_per_eu(4))) void ds_step(
-    Dev D, int W, int NPAST, long long iter, const unsigned long long* __restrict__ sch_src,
-    unsigned long long* __restrict__ sch_dst, long long n8, hbk::WaveEvalArgs E, AccArgs A, int prio) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem_all[];
-  ProposeShared& S = *reinterpret_cast<ProposeShared*>(smem_all);
-#ifdef HB_DS_CLOCKS
-  const unsigned long long c0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
-#endif
-  if (prio == 3) __builtin_amdgcn_s_setprio(3);
-  else if (prio == 2) __builtin_amdgcn_s_setprio(2);
-  else if (prio == 1) __builtin_amdgcn_s_setprio(1);
-  int j;
-  bool act;
-  propose_group<true>(D, W, NPAST, iter, sch_src, sch_dst, n8, S, j, act);
-  __builtin_amdgcn_s_waitcnt(0);  // the group's records acknowledged (L2) before any wave's scalar loads
-  __syncthreads();                // and the propose / prep LDS is dead: the slabs take it
-  if (!act) return;
-  const int jl = __builtin_amdgcn_readfirstlane(j - D.lo);
-  const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-#ifdef HB_DS_CLOCKS
-  const unsigned long long c1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
-#endif
-  // the records just written: scalar loads (constant address space), issued
-  // only after the barrier (the pointer passes through asm)
-  typedef const __attribute__((address_space(4))) hbdev::WalkerConst cwc_t;
-  uint64_t a = (uint64_t)D.wc;
-  __asm__ volatile("" : "+s"(a));
-  const hbdev::WalkerConst* wcs = (const hbdev::WalkerConst*)(cwc_t*)a;
-  hbk::eval_wave_body<VPT, true, 1>(E.t, E.ph, E.f, E.isg, E.rows, E.n, E.kth, wcs[jl], jl, jl, D.logLy, nullptr, 0,
-                                    E.slab_bytes, E.slab_bytes, E.gap, A, smem_all + (size_t)wv * (size_t)E.lds_per,
-                                    E.dq);
-#ifdef HB_DS_CLOCKS
-  const unsigned long long c2 = __builtin_amdgcn_s_memtime(), r2 = __builtin_amdgcn_s_memrealtime();
-  if ((threadIdx.x & 63) == 0 && jl < 65536) {
-    unsigned long long* o = ds_clk + kDsClkWords * jl;
-    o[0] = c0; o[1] = c1; o[2] = c2; o[3] = r0; o[4] = r1; o[5] = r2;
-    o[6] = (unsigned long long)j;
-    o[7] = __double_as_longlong(D.temp[j]);
-    o[8] = __double_as_longlong(D.y[(size_t)jl * kNp + 3]);
-  }
-#endif
 }
 
 // Hastings test and history (:492-546); 64 slots per block (one lane each),
@@ -1144,7 +1075,6 @@ struct hb_dsampler {
   // one-rank one made by hb_dsampler_create_shard (the exchange path on a
   // single GPU: RCCL world size 1 in tests)
   bool xchg = false;
-  bool no_eord = getenv("HB_DS_NO_EORD") != nullptr;  // experiment knob: eval waves in slot order
   std::vector<void*> allocs;
   std::vector<int> order;  // owned slots in descending temperature (ds_propose's wave order)
   // Swap schedules (SwapEnt | off | beta, compact), drawn ahead by producer
@@ -1161,7 +1091,7 @@ struct hb_dsampler {
   // an event after every swap launch costs a cache-flushing barrier packet
   // (~5 us of idle GPU before the next ds_propose, rocprof timeline); every
   // fourth iteration suffices for the producers' slot reuse
-  int ev_every = 4;
+  static constexpr int ev_every = 4;  // divides R_RING: the events land on fixed ring slots
   long long q_issued = 0;  // iterations whose swaps are enqueued
   struct Slot {
     long long q = -1;       // iteration it holds (-1: never used)
@@ -1187,12 +1117,6 @@ struct hb_dsampler {
   int nthreads = 0;
   int nseg = 1;  // swap segments (ds_swap_seg workgroups) over the owned slots
   bool fused_prep = true;  // walker records in ds_propose's epilogue (else an hb_prep_kernel launch)
-  // propose, records, likelihood and Hastings test in ONE launch (ds_step):
-  // one resident round of slots on the one-wave plan at 4, 8 or 16 cadences
-  // per lane whose four slabs fit a quarter of the CU's LDS; HB_DS_STEP=1 / 0
-  // (A/B knob): on / off
-  bool step = false;
-  int step_prio = 0;  // the propose stage's s_setprio (HB_DS_STEP_PRIO, A/B knob)
   double* d_lslot = nullptr; // [W] logL by slot after the Hastings test (one-process samplers)
   bool lslot_now = false;    // this iteration's fused Hastings test wrote d_lslot
   int* ecnt_buf[2] = {nullptr, nullptr};  // e-bin counters of even / odd iterations (Dev::ecnt)
@@ -1514,7 +1438,7 @@ static hb_dsampler* ds_create(hb_sampler* s, hb_ctx* ctx, const int* chain_of_sl
   D.P = d->d_params;
   if ((e = hipMemsetAsync(D.nsw, 0, sizeof(long long) * Nz, d->st))) return fail("hipMemset", e);
   // eval order by e bins (AccArgs::ecnt) up to kEvalOrdMax owned slots
-  if (Nz <= (size_t)kEvalOrdMax && !d->no_eord) {
+  if (Nz <= (size_t)kEvalOrdMax) {
     if ((e = d->alloc(&D.ecnt, 2 * (size_t)kOrdBins * kEbinStride)) || (e = d->alloc(&D.elist, (size_t)kOrdBins * Nz)))
       return fail("hipMalloc", e);
     if ((e = hipMemsetAsync(D.ecnt, 0, 2 * sizeof(int) * kOrdBins * kEbinStride, d->st))) return fail("hipMemset", e);
@@ -1523,36 +1447,12 @@ static hb_dsampler* ds_create(hb_sampler* s, hb_ctx* ctx, const int* chain_of_sl
     D.ecnt_next = d->ecnt_buf[1];
   }
   // records in ds_propose's epilogue while the slots fit one resident round
-  // of its waves at that occupancy (4 per SIMD, 16 per CU); HB_DS_FUSED_PREP=0/1 forces
+  // of its waves at that occupancy (4 per SIMD, 16 per CU)
   {
     int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, d->device) != hipSuccess || cus <= 0)
       cus = 256;
-    const char* fp = getenv("HB_DS_FUSED_PREP");
-    d->fused_prep = fp ? atoi(fp) != 0 : d->nl <= 16 * cus;
-    hbk::WaveEvalArgs E{};
-    const char* st = getenv("HB_DS_STEP");
-    const char* sp = getenv("HB_DS_STEP_PRIO");
-    d->step_prio = sp ? std::max(0, std::min(3, atoi(sp))) : 0;
-    const bool step_on = st ? atoi(st) != 0 : kDsStepDefault;
-    if (d->fused_prep && step_on && hbx_ctx_wave_eval_args(ctx, &E) == 0 && E.wpw == 1 &&
-        (E.vpt == 4 || E.vpt == 8 || E.vpt == 16)) {
-      const size_t lds = std::max((size_t)kPW * (size_t)E.lds_per, sizeof(ProposeShared));
-      d->step = lds <= 163840 / 4;
-    }
-  }
-  if (const char* ee = getenv("HB_DS_EV_EVERY")) {  // experiment knob
-    // a producer reuses ring slot q % R_RING once the event after iteration
-    // ceil((q+1)/ev_every) ev_every - 1 completed: that iteration must not need
-    // the slot being reused (ev_every <= R_RING), and the events must land on
-    // fixed slots (R_RING % ev_every == 0)
-    const int ev = atoi(ee);
-    if (ev < 1 || ev > hb_dsampler::R_RING || hb_dsampler::R_RING % ev != 0) {
-      hbx_set_error("hb_dsampler_create: HB_DS_EV_EVERY must divide the schedule ring size (8)");
-      delete d;
-      return nullptr;
-    }
-    d->ev_every = ev;
+    d->fused_prep = d->nl <= 16 * cus;
   }
   // swap segments of <= kSegSlots owned slots; an attempt is listed for at
   // most min(G, 3 + 2 kMaxLevels / (smallest segment)) segments
@@ -1561,7 +1461,7 @@ static hb_dsampler* ds_create(hb_sampler* s, hb_ctx* ctx, const int* chain_of_sl
     const bool one = !d->xchg && d->lo == 0 && d->nl == W;
     if (one && (e = d->alloc(&d->d_lslot, Wz))) return fail("hipMalloc", e);
     const char* df = getenv("HB_DS_DEFER");
-    d->defer = one && !d->step && (df ? atoi(df) != 0 : true);
+    d->defer = one && (df ? atoi(df) != 0 : true);
   }
   {
     const size_t G = (size_t)d->nseg, segmin = std::max<size_t>(1, (size_t)d->nl / G);
@@ -1574,11 +1474,9 @@ static hb_dsampler* ds_create(hb_sampler* s, hb_ctx* ctx, const int* chain_of_sl
     // the event only tells the producer that the GPU has finished reading the
     // slot (ds_propose's pinned-source loads): no system-scope release is
     // needed for that, and without it the barrier packet writes back and
-    // invalidates no caches before the next launch (HB_DS_EV_FENCE=1, A/B
-    // knob: with the fence)
-    static const bool ev_fence = getenv("HB_DS_EV_FENCE") != nullptr && atoi(getenv("HB_DS_EV_FENCE")) != 0;
-    if ((e = hipEventCreateWithFlags(&d->ev_used[r],
-                                     hipEventDisableTiming | (ev_fence ? 0u : (unsigned)hipEventDisableSystemFence))))
+    // invalidates no caches before the next launch (with the fence: within
+    // noise, profiles/r05/r05v_ds_event_fence_ab.txt)
+    if ((e = hipEventCreateWithFlags(&d->ev_used[r], hipEventDisableTiming | hipEventDisableSystemFence)))
       return fail("event", e);
   }
   if ((e = hipHostMalloc((void**)&d->h_ctr, sizeof(Counters), hipHostMallocDefault))) return fail("pinned", e);
@@ -1958,7 +1856,7 @@ static long ds_begin(hb_dsampler* d, long iter, double* send, long cap) {
     const hb_dsampler::Slot& ps = d->slots[d->pend_slot];
     const int cone = 2 * ps.nlv + 1;
     sp_lds = (size_t)kPW * swap_prev_wave_bytes(cone, ps.maxent);
-    if (!d->step && sp_lds <= kSwapPrevLdsMax) {
+    if (sp_lds <= kSwapPrevLdsMax) {
       const int G = d->nseg;
       const unsigned char* base = d->d_sched[d->pend_slot];
       SP.soff = reinterpret_cast<const int*>(base);
@@ -1990,26 +1888,7 @@ static long ds_begin(hb_dsampler* d, long iter, double* send, long cap) {
   auto* sch_src = reinterpret_cast<const unsigned long long*>(d->pin[slot]);
   auto* sch_dst = reinterpret_cast<unsigned long long*>(d->d_sched[slot]);
   const long long n8 = (long long)(used_bytes / 8);
-  if (d->step) {
-    // propose -> records -> likelihood -> Hastings test, one launch
-    hbk::WaveEvalArgs E{};
-    if (const int rc = hbx_ctx_wave_eval_args(d->ctx, &E)) return rc;
-    Dev Ds = Dp;
-    Ds.ecnt = nullptr;  // the waves evaluate their own slots: no e-order lists
-    const AccArgs acc{D.idx, D.logL, D.logP, D.logPy, D.temp, D.alpha2, D.jump, D.jtype, D.x, D.y, D.hist,
-                      D.DEacc_arr, D.ctr, D.ev, d->P.log_on, NPAST, (long long)iter, d->lo, 0,
-                      nullptr, nullptr, nl, 0, d->d_lslot};  // Lslot: null for exchanging samplers
-    const size_t lds = std::max((size_t)kPW * (size_t)E.lds_per, sizeof(ProposeShared));
-    const dim3 grid((nl + kPW - 1) / kPW), blk(64 * kPW);
-    if (E.vpt == 16)
-      ds_step<16><<<grid, blk, lds, s>>>(Ds, W, NPAST, (long long)iter, sch_src, sch_dst, n8, E, acc, d->step_prio);
-    else if (E.vpt == 8)
-      ds_step<8><<<grid, blk, lds, s>>>(Ds, W, NPAST, (long long)iter, sch_src, sch_dst, n8, E, acc, d->step_prio);
-    else
-      ds_step<4><<<grid, blk, lds, s>>>(Ds, W, NPAST, (long long)iter, sch_src, sch_dst, n8, E, acc, d->step_prio);
-    DS_TRY(hipGetLastError(), "ds_step");
-    d->lslot_now = acc.Lslot != nullptr;
-  } else {
+  {
     const unsigned pg = (unsigned)((nl + kPW - 1) / kPW);
     if (fuse) {
       Dp.idx = D.idx;  // the previous iteration's index[] (the replay's input)
@@ -2165,11 +2044,6 @@ extern "C" int hb_dsampler_gather(hb_dsampler* d, double* x_slots, double* logl_
 }
 
 #ifdef HB_DS_CLOCKS
-extern "C" int hb_debug_ds_clocks(unsigned long long* out, int nslots) {
-  if (nslots > 65536) nslots = 65536;
-  return hipMemcpyFromSymbol(out, HIP_SYMBOL(ds_clk), kDsClkWords * sizeof(unsigned long long) * nslots) == hipSuccess
-             ? 0 : -1;
-}
 extern "C" int hb_debug_dp_clocks(unsigned long long* out, int nslots) {
   if (nslots > 65536) nslots = 65536;
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(dp_clk), kDpClkWords * sizeof(unsigned long long) * nslots) == hipSuccess

@@ -129,21 +129,6 @@ struct PreArgs {
   double2* ph;              // the global phase table (each workgroup writes a slice)
   double* tab_pc;           // its period [s]
 };
-// A context's inputs of the one-wave likelihood (hb_wave.hpp eval_wave_body):
-// the device sampler's fused step kernel (hb_dsampler.hip ds_step) runs it
-// on the records its propose stage writes (hbx_ctx_wave_eval_args)
-struct WaveEvalArgs {
-  const double* t;     // times, cadence order
-  const double2* ph;   // shared-period phase table
-  const double* f;
-  const double* isg;   // 1 / max(sigma, 1e-5)
-  const double* rows;  // t, f, 1/sigma in lane-row order
-  long n, kth;
-  double gap;          // the warm-chain gate's cadence gap
-  double* dq;          // deferred queues (cap walkers)
-  int vpt, wpw;        // plan (vpt 0: no one-wave path)
-  int slab_bytes, lds_per;
-};
 // walkers per workgroup of the fused launch for w walkers on `cus` CUs (0: the
 // two-launch path: prep + eval)
 int fused_wpb(const EvalPlan& pl, int w, int cus);

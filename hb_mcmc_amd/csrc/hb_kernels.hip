@@ -1438,8 +1438,7 @@ EvalPlan make_plan(long n) {
   EvalPlan pl;
   pl.n = n;
   pl.kth = (n % 2 == 0) ? n / 2 : n / 2 + 1;  // likelihood3.c:97-99
-  static const long wave_max = getenv("HB_WAVE_NMAX") ? atol(getenv("HB_WAVE_NMAX")) : 64 * 32;  // A/B knob
-  if ((n <= wave_max || n > 64 * 32) && wave_nr_for(n) > 0) {  // one wave (or 2..16) per walker, keys in registers
+  if (wave_nr_for(n) > 0) {  // one wave (or 2..16) per walker, keys in registers
     pl.vpt = wave_vpt_for(n);
     pl.wpw = wave_nr_for(n) / 64;
     pl.nw = pl.wpw;  // waves per walker (hb_ctx_waves_per_walker)

@@ -29,10 +29,6 @@
 #define HBW_FN static inline
 #endif
 
-#ifndef HB_WALL_PRED
-#define HB_WALL_PRED 0  // 1: predicated 4-fold groups for the short runs (measured 0.8 us per iteration slower)
-#endif
-
 namespace hbwall {
 
 constexpr int kGuard = 100000000;  // fold bound of the host loop (hb_sampler.cpp, before hb_walls)
@@ -178,31 +174,8 @@ HBW_FN double apply_wall(double v, double lo, double hi, double fl, double fh) {
                           : mode == kFfBinade ? bottom * (1.0 - 0x1p-53)  // |v| >= bottom
                                               : edge - lim2 - edge * 0x1p-48;
       const int smax = mode >= kFfBinade ? kGuard : 16;
-      if (HB_WALL_PRED && smax == 16) {
-        // the common case (after a fast-forward, or at a binade top): at most
-        // 16 folds, predicated and unrolled -- a GPU lane pays no branch per
-        // fold, only a wave-wide "any lane still folding" test per 4 folds
-        bool run = true;
-        for (int s0 = 0; s0 < 16; s0 += 4) {
-#if defined(__HIPCC__)
-#pragma unroll
-#endif
-          for (int u = 0; u < 4; ++u) {
-            const int s = s0 + u;
-            run = run & (guard < kGuard) & ((v < lo) | (v > hi)) & ((s < 4) | (fabs(v) > stop));
-            const double vf = (v < lo ? lo2 : hi2) - v;
-            v = run ? vf : v;
-            guard += run ? 1 : 0;
-          }
-#if defined(__HIP_DEVICE_COMPILE__)
-          if (!__any(run)) break;
-#else
-          if (!run) break;
-#endif
-        }
-        continue;
-      }
-      // the plain loop's folds, two per trip: the second is taken under the
+      // the plain loop's folds, two per trip (predicated 4-fold groups for the
+      // short runs measured 0.8 us per iteration slower): the second is taken under the
       // same test, so the sequence and the count are unchanged, and a GPU
       // lane pays one exec-mask branch per two dependent folds
       for (int s = 0;;) {

@@ -4,9 +4,8 @@
 // queue, exact median by register-key radix select, chi^2 and the Gaia /
 // Roche terms (likelihood3.c:530-686, 86-105, 809-873), and the fused
 // Hastings test (hb_accept.hpp).  Shared by the batched eval kernels
-// (hb_kernels.hip hb_eval_wave_kernel) and the device sampler's fused step
-// kernel (hb_dsampler.hip ds_step), which call eval_wave_body() once the
-// walker's record (WalkerConst) is in memory.
+// (hb_kernels.hip hb_eval_wave_kernel, hb_eval_catalog_kernel), which call
+// eval_wave_body() once the walker's record (WalkerConst) is in memory.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -776,14 +775,11 @@ __device__ __forceinline__ void eval_wave_body(const double* __restrict__ t, con
   double ll0 = 0.0;
   const bool early_exit = mode == 0 && logl_without_light_curve(w, ll0);
   Pacer pc{0, 0, 0};
-#ifndef HB_ACC_LATE
-#define HB_ACC_LATE 1  // A/B knob: 0 = the Hastings operands loaded at the wave's start
-#endif
   // the Hastings test's operands (uniform values and the 21-coordinate rows):
-  // loaded after the model pass (HB_ACC_LATE), in flight through the select,
-  // so they hold no registers across the model loop
+  // loaded after the model pass, in flight through the select, so they hold
+  // no registers across the model loop (profiles/r05/r05p_ds_lost_acc_ab.txt)
   hbds::AccPre apre{};
-  if (ACC && (!HB_ACC_LATE || early_exit)) apre = hbds::accept_prefetch(hst, wv, lane);
+  if (ACC && early_exit) apre = hbds::accept_prefetch(hst, wv, lane);
   if (early_exit) {  // Roche overflow, |e| > 1: logl_without_light_curve (hb_device.hpp)
     if (row == 0) logl[wv] = ll0;
     if (ACC) (void)hbds::accept_slot_wave_pre(hst, wv, ll0, lane, apre);
@@ -814,7 +810,7 @@ __device__ __forceinline__ void eval_wave_body(const double* __restrict__ t, con
   if (WPW > 1) __syncthreads();
   dq_apply(w, vals, dq, t, rw, (int)n, lane);
   if (WPW > 1) __syncthreads();
-  if (ACC && HB_ACC_LATE) apre = hbds::accept_prefetch(hst, wv, lane);
+  if (ACC) apre = hbds::accept_prefetch(hst, wv, lane);
   HB_CLK_MARK(0);
   HB_WSYNC();
   // live key slots of this lane; a light curve of 64 VPT cadences fills every row
