@@ -157,7 +157,10 @@ __device__ __forceinline__ void dq_apply(const WalkerConst& w, double* vals, con
 // cadence spacing, host-side), at most kWarmD1: the fast path then holds for
 // nearly every cadence.  Otherwise (high e, sparse or shuffled cadences) the
 // cold path with four interleaved cadences per lane is faster.
-constexpr double kWarmD1 = 0x1p-10;
+#ifndef HB_WARM_D1
+#define HB_WARM_D1 0x1p-6  // A/B knob (2^-10 until round 5: profiles/r05/r05za_warm_gate_ab.txt)
+#endif
+constexpr double kWarmD1 = HB_WARM_D1;
 // cadences per lane of the chain path (4: catalog classes of 129-256 cadences
 // on warm chains measured within noise, profiles/r05/r05c_c5_ab.txt)
 constexpr int kChainVptMin = 8, kChainVptMax = 32;
