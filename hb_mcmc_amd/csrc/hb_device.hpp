@@ -897,7 +897,7 @@ __device__ __forceinline__ void hb_cadence_flux_k(const double (&t)[K], const do
 // reversion below): one Newton step instead of the reference start's three
 // or four.  The root is the one the reference's five steps reach whenever
 // those converge -- which holds for every M when e <= 0.85
-// (scripts/kepler_warm.py) -- so the warm start is taken only for e <= 0.8
+// (scripts/kepler_warm.py) -- so the warm start is taken only for e <= 0.84
 // (chain_eligible), and a lane outside the fast path continues with the
 // general Newton loop, failing that from the reference's start
 // (wave-uniform decisions throughout).
@@ -909,7 +909,10 @@ __device__ __forceinline__ void hb_cadence_flux_k(const double (&t)[K], const do
 // independent fp64 chains per lane: the drain, where one or two waves are left
 // on a SIMD, is latency-bound).
 // ------------------------------------------------------------------------
-constexpr double kWarmEmax = 0.8;
+#ifndef HB_WARM_EMAX
+#define HB_WARM_EMAX 0.84  // A/B knob (at most 0.85, see above; 0.8 until round 5: profiles/r05/r05za_warm_gate_ab.txt)
+#endif
+constexpr double kWarmEmax = HB_WARM_EMAX;
 // The chain carries the previous cadence's solved E, (sin, cos)(E), its mean
 // anomaly m and 1 / (1 - e cos E) (the polynomial's beta, which is also the
 // warm start's 1 / f'(E_p)); the polynomial's reciprocal is seeded with the

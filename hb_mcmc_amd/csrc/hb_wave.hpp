@@ -154,11 +154,13 @@ __device__ __forceinline__ void dq_apply(const WalkerConst& w, double* vals, con
 // reference's five steps converge, so the root is the same) and the first
 // Newton correction after the first-order start, |d1| <= e dM^2 / (2 (1-e)^3)
 // for the light curve's typical phase step dM (gap = 90th percentile of the
-// cadence spacing, host-side), at most kWarmD1: the fast path then holds for
-// nearly every cadence.  Otherwise (high e, sparse or shuffled cadences) the
-// cold path with four interleaved cadences per lane is faster.
+// cadence spacing, host-side), at most kWarmD1.  Steps that miss the one-step
+// fast path continue with the Newton loop from the warm iterate, which still
+// takes fewer steps than the reference's start; past the gate (sparse or
+// shuffled cadences) the cold path with four interleaved cadences per lane is
+// faster.
 #ifndef HB_WARM_D1
-#define HB_WARM_D1 0x1p-6  // A/B knob (2^-10 until round 5: profiles/r05/r05za_warm_gate_ab.txt)
+#define HB_WARM_D1 0x1p-4  // A/B knob (2^-10 until round 5: profiles/r05/r05za_warm_gate_ab.txt)
 #endif
 constexpr double kWarmD1 = HB_WARM_D1;
 // cadences per lane of the chain path (4: catalog classes of 129-256 cadences
