@@ -703,13 +703,49 @@ __device__ __forceinline__ void mean_anomaly_k(const double (&t)[K], const Walke
 // 155-157) and (sin, cos)(E0): rotations of the shared-period table entry
 // (tab), else the branch-free sincos.  Lanes flagged `exact` recompute M by
 // fmod_twopi_fast first (wave-uniform branch).
+//
+// Series start (tab and |e| <= kSeriesEmax): E0 = M + the fifth-order Lagrange
+// series of Kepler's equation in e, written in s = sin M, c = cos M, x = s^2:
+//   E - M = s [c ((e^2 + e^4) - 8/3 e^4 x)
+//              + (e + e^3 + e^5) + x (-(3/2 e^3 + 17/3 e^5) + 125/24 e^5 x)] + O(e^6)
+// (e sin M + e^2/2 sin 2M + e^3/8 (3 sin 3M - sin M) + e^4/6 (2 sin 4M - sin 2M)
+// + e^5/384 (125 sin 5M - 81 sin 3M + 2 sin M)), and (sin, cos)(E0) by the
+// Taylor rotation of the table entry through E0 - M (|E0 - M| <= e + O(e^6)
+// <= kRotMaxK).  The start is within 8e-5 of the root at e = 0.226 (1.5e-4 at
+// 0.25), so Newton converges in two steps where the reference's start takes
+// three (scripts/kepler_series.py); for e <= 0.85 every start Newton
+// converges from reaches the reference's root to rounding
+// (scripts/kepler_warm.py), so only the path there changes.
+#ifndef HB_SERIES_EMAX
+#define HB_SERIES_EMAX 0.25  // A/B knob (0: the reference's start everywhere)
+#endif
+constexpr double kSeriesEmax = HB_SERIES_EMAX;
+static_assert(kSeriesEmax <= kRotMaxK, "the series start's rotation needs |E0 - M| <= kRotMaxK");
 template <int K>
 __device__ __forceinline__ void cold_start_k(const double (&t)[K], const double2 (&ph)[K], bool tab, bool exact,
                                              const WalkerConst& w, double (&m)[K], const bool (&plus)[K],
                                              double (&E)[K], double (&s)[K], double (&c)[K], bool& ok) {
+  const bool ser = tab && fabs(w.e) <= kSeriesEmax;  // walker-uniform
+  if (ser) {
+    const double e = w.e, e2 = e * e, e3 = e2 * e, e4 = e2 * e2, e5 = e4 * e;
+    const double a0 = e2 + e4, a1 = (-8.0 / 3.0) * e4;
+    const double b0 = (e + e3) + e5, b1 = -(1.5 * e3 + (17.0 / 3.0) * e5), b2 = (125.0 / 24.0) * e5;
 #pragma unroll
-  for (int k = 0; k < K; ++k) E[k] = m[k] + (plus[k] ? w.e085 : -w.e085);
-  if (tab) {  // walker-uniform: E0 = M + sg del by rotations of the table entry
+    for (int k = 0; k < K; ++k) {
+      const double sx = fma(ph[k].x, w.cpsi, -(ph[k].y * w.spsi));  // sin M
+      const double cx = fma(ph[k].y, w.cpsi, ph[k].x * w.spsi);     // cos M
+      const double x = sx * sx;
+      const double dl = sx * fma(cx, fma(x, a1, a0), fma(x, fma(x, b2, b1), b0));
+      E[k] = m[k] + dl;
+      s[k] = sx;
+      c[k] = cx;
+      rotate_back_wide(-dl, dl * dl, s[k], c[k]);  // (sin, cos)(M + dl)
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < K; ++k) E[k] = m[k] + (plus[k] ? w.e085 : -w.e085);
+  }
+  if (tab && !ser) {  // walker-uniform: E0 = M + sg del by rotations of the table entry
 #pragma unroll
     for (int k = 0; k < K; ++k) {
       const double sx = fma(ph[k].x, w.cpsi, -(ph[k].y * w.spsi));  // sin(phi - psi)

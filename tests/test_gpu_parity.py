@@ -194,15 +194,26 @@ def mean_anomaly_cond(oracle, t, P):
 
 
 def ulp_sensitivity(oracle, t, P, ref):
-    """Per cadence, how far the reference's own template moves when every
-    cadence time moves by one ulp (up or down): its discrete ill-conditioning,
-    which the derivative above misses -- e.g. an eclipse near the regime
-    boundary of eclipse_area (likelihood3.c:353-389), where asin is evaluated
-    next to 1 (at N = 4096, e = 0.85 the reference's values at two cadences of
-    the same phase, one period apart, differ by 3.2e-12)."""
-    up = oracle.light_curve_batch(np.nextafter(t, np.inf), P, 8)
-    dn = oracle.light_curve_batch(np.nextafter(t, -np.inf), P, 8)
-    return np.maximum(np.abs(up - ref), np.abs(dn - ref))
+    """Per cadence, how far the reference's own template moves when the
+    cadence's mean anomaly moves by one ulp (up or down): its discrete
+    ill-conditioning, which the derivative above misses -- e.g. an eclipse
+    near the regime boundary of eclipse_area (likelihood3.c:353-389), where
+    asin is evaluated next to 1 (at N = 4096, e = 0.85 the reference's values
+    at two cadences of the same phase, one period apart, differ by 3.2e-12).
+    The shift is dt = max(ulp(t), ulp(M) P / 2 pi): one ulp of the time, or
+    of M where that is coarser (early cadences, |t| << |M| P / 2 pi: at N =
+    6001, t = 0.068 d, M = -4.4, one ulp of M moves the reference's template
+    by 6.3e-12 and one ulp of t by 2.2e-16) -- any solver's E carries M's
+    rounding, whatever its Newton path."""
+    Pd = 10.0 ** P[:, 2]
+    M = 2.0 * np.pi * (t[None, :] - P[:, 6:7]) / Pd[:, None]
+    dt = np.maximum(np.spacing(np.abs(t))[None, :], np.spacing(np.abs(M)) * Pd[:, None] / (2.0 * np.pi))
+    out = np.empty_like(ref)
+    for w in range(len(P)):
+        up = oracle.light_curve(t + dt[w], P[w])
+        dn = oracle.light_curve(t - dt[w], P[w])
+        out[w] = np.maximum(np.abs(up - ref[w]), np.abs(dn - ref[w]))
+    return out
 
 
 # The cold Kepler path at e >= 0.85 (scripts/cold_err_probe.py, GPU, N = 2048
