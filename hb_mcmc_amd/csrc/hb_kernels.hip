@@ -246,11 +246,14 @@ __device__ __forceinline__ double wave_sum(double v) {
 // Model flux for cadences tid, tid+NT, ... : kK interleaved cadences per lane
 // per iteration (ILP for the fp64 Kepler chains), next iteration's times
 // prefetched; values go to vals[], min/max order keys returned per lane.
+#ifndef HB_BLK_K
+#define HB_BLK_K kK  // A/B knob: cadences interleaved per thread in the block kernels' model pass
+#endif
 template <int NT>
 __device__ __forceinline__ void model_pass(const double* __restrict__ t, const double2* __restrict__ ph, int n,
                                            const WalkerConst& w, double* vals, int tid, uint64_t& kmn_out,
                                            uint64_t& kmx_out) {
-  constexpr int K = kK;
+  constexpr int K = HB_BLK_K;
   const bool tab = (ph != nullptr) && (w.tab != 0.0);  // walker-uniform
   // running min/max as doubles (v_min/v_max_f64); NaN lanes are tracked and
   // the order keys recomputed from vals[] in that (never observed) case
