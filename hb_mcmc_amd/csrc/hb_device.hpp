@@ -780,6 +780,7 @@ __device__ __forceinline__ void cold_start_k(const double (&t)[K], const double2
 template <int K>
 __device__ __forceinline__ bool newton_k(double e, const double (&m)[K], double (&E)[K], double (&s)[K],
                                          double (&c)[K], double (&yk)[K], bool& ok) {
+  const double ae = fabs(e);
 #pragma unroll
   for (int it = 0; it < 5; ++it) {
     bool small = true, mid = true, tiny = true, conv = true;
@@ -797,7 +798,7 @@ __device__ __forceinline__ bool newton_k(double e, const double (&m)[K], double 
       small &= ad <= kRotMaxK;
       mid &= ad <= 0x1p-9;
       tiny &= ad <= 0x1p-22;
-      conv &= e * z[k] <= 0x1p-51 * den;
+      conv &= ae * z[k] <= 0x1p-51 * den;  // |e|: e < 0 is Kepler's equation at M + pi
     }
     // rotation degree by the wave's largest step (wave-uniform branches)
     if (wave_all(tiny)) {
@@ -964,7 +965,7 @@ struct ChainState {
 struct WarmK {
   double he, e6, ke;  // 0.5 e, e / 6, 2^-51 / e (the convergence test z <= ke den)
 };
-__device__ __forceinline__ WarmK warm_k(double e) { return WarmK{0.5 * e, e * (1.0 / 6.0), 0x1p-51 / e}; }
+__device__ __forceinline__ WarmK warm_k(double e) { return WarmK{0.5 * e, e * (1.0 / 6.0), 0x1p-51 / fabs(e)}; }
 
 // Warm half: the mean anomaly up to a multiple of 2pi (no exactness flags:
 // D is reduced by rint), the third-order start -- series reversion of Kepler's

@@ -167,7 +167,7 @@ constexpr double kWarmD1 = HB_WARM_D1;
 // on warm chains measured within noise, profiles/r05/r05c_c5_ab.txt)
 constexpr int kChainVptMin = 8, kChainVptMax = 32;
 __device__ __forceinline__ bool chain_eligible(const WalkerConst& w, double gap) {
-  const double e = w.e;
+  const double e = fabs(w.e);  // e < 0 is Kepler's equation at M + pi, E + pi
   const double dm = gap * kDay * fabs(w.mA);
   const double ome = 1.0 - e;
   return (e <= kWarmEmax) && (e * dm * dm <= 2.0 * kWarmD1 * ome * ome * ome);

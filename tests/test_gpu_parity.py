@@ -358,6 +358,44 @@ def test_block_kernel_cold_roche_shuffled(hbmi, oracle, n, order):
     assert worst <= 1.0, f"template error {worst:.2f} x the bound"
 
 
+@pytest.mark.parametrize("n,order", [(6001, "sorted"), (1024, "shuffled"), (200, "sorted"), (1024, "sorted")],
+                         ids=["block-kernel", "one-wave-cold", "one-wave-vpt4", "one-wave-warm"])
+def test_series_kepler_start_boundary(hbmi, oracle, n, order):
+    """The cold path's series Kepler start (hb_device.hpp cold_start_k, |e| <=
+    kSeriesEmax = 0.25 on the phase table) and the reference's start on either
+    side of its bound, e = 0 and negative e included: the block kernel (N =
+    6001), the one-wave cold pass (shuffled cadences leave the warm-chain gate)
+    and a 4-cadence-per-lane light curve, and the warm chains (sorted N =
+    1024); templates under the conditioning bound and logL against the
+    oracle, batch reversal bit-identical.  Negative e is Kepler's equation at
+    M + pi: the Newton stopping rule and the warm-chain gate take |e| (with e
+    itself the rule stopped after one step for every e < 0: logL off by up to
+    3e-3 before round 5's fix)."""
+    from hb_mcmc_amd import synth
+    from hb_mcmc_amd.likelihood import HBLikelihood
+
+    t, f, s = synth.dataset(n, oracle.light_curve)
+    if order == "shuffled":
+        p = np.random.default_rng(n + 7).permutation(n)
+        t, f, s = t[p], f[p], s[p]
+    es = [0.0, 1e-9, 0.05, 0.1, 0.226, 0.24, 0.2499, 0.25, np.nextafter(0.25, 1.0), 0.2501, 0.3, 0.6,
+          -0.1, -0.25, -0.2501, 0.85]
+    P = synth.walkers(len(es), seed=n + 5, roche_frac=0.0)
+    P[:, 3] = es
+    with HBLikelihood(t, f, s) as L:
+        ll = L.loglike(P)
+        rev = L.loglike(P[::-1].copy())[::-1]
+        tm = L.light_curve(P)
+    assert np.array_equal(ll, rev, equal_nan=True)
+    close_logl(ll, oracle.loglike_batch(t, f, s, P, synth.MAG_DEFAULT, synth.MAGERR_DEFAULT, 8))
+    ref = oracle.light_curve_batch(t, P, 8)
+    ok = ~np.isnan(ref).any(1)
+    assert ok.sum() >= len(es) - 2
+    tol = cold_tol(oracle, t, P, ref)
+    worst = np.nanmax(np.where(ok[:, None], np.abs(tm - ref) / tol, 0.0))
+    assert worst <= 1.0, f"template error {worst:.2f} x the bound"
+
+
 @pytest.mark.parametrize("latency", [True, False], ids=["small-batch-plan", "one-wave-plan"])
 @pytest.mark.parametrize("n", [1024, 6001])
 def test_phase_table_and_direct_paths(hbmi, oracle, n, latency):
