@@ -358,8 +358,9 @@ def test_block_kernel_cold_roche_shuffled(hbmi, oracle, n, order):
     assert worst <= 1.0, f"template error {worst:.2f} x the bound"
 
 
-@pytest.mark.parametrize("n,order", [(6001, "sorted"), (1024, "shuffled"), (200, "sorted"), (1024, "sorted")],
-                         ids=["block-kernel", "one-wave-cold", "one-wave-vpt4", "one-wave-warm"])
+@pytest.mark.parametrize("n,order", [(6001, "sorted"), (1024, "shuffled"), (200, "sorted"), (1024, "sorted"),
+                                     (1500, "sorted"), (3000, "sorted")],
+                         ids=["block-kernel", "one-wave-cold", "one-wave-vpt4", "one-wave-warm", "pair", "rows"])
 def test_series_kepler_start_boundary(hbmi, oracle, n, order):
     """The cold path's series Kepler start (hb_device.hpp cold_start_k, |e| <=
     kSeriesEmax = 0.25 on the phase table) and the reference's start on either
