@@ -94,6 +94,16 @@ static_assert(sizeof(WalkerConst) == 48 * 8, "WalkerConst layout");
 //    logL -- a NaN (+qNaN, what the reference build returns for every such
 //    walker checked); a NaN logL is only ever rejected by the Hastings test.
 // Returns false when the light curve is needed.
+// sqrt(1 - e^2) of the record, NaN at |e| = 1 as well as above: there the
+// reference divides by 1 - e^2 = 0 (beta = (1 + e cos nu) / (1 - e^2) = 0 / 0,
+// likelihood3.c:266, 326; the beaming factor's / sqrt(1 - e^2), :230) and its
+// template is NaN, while the kernels' identity beta = 1 / (1 - e cos E) stays
+// finite.  (e = 1 is also Roche overflow, periastron a (1 - e) = 0.)
+__device__ __forceinline__ double sqrt_1me2(double e) {
+  const double d = 1.0 - e * e;
+  return d == 0.0 ? __builtin_nan("") : sqrt(d);
+}
+
 __device__ __forceinline__ bool logl_without_light_curve(const WalkerConst& w, double& ll) {
   if (w.roche != 0.0) {
     ll = -kBig / 2.0;
@@ -407,7 +417,7 @@ __device__ inline void hb_prepare_walker(const double* __restrict__ p, const dou
   w.T0c = p[6] * kDay;
   w.e = e;
   w.e085 = 0.85 * e;
-  w.sq1me2 = sqrt(1.0 - e * e);
+  w.sq1me2 = sqrt_1me2(e);
   w.inv1me2 = 1.0 / (1.0 - e * e);
   sincos(om, &w.sw, &w.cw);
   double si, ci;

@@ -222,7 +222,7 @@ __device__ __forceinline__ void prep_records(PrepShared<NW>& L, int nb, const Ma
       const double mtot_cgs = m1 * kMsun + m2 * kMsun;
       const double Pc = pd * kDay;
       const double a_cgs = cbrt(kG * mtot_cgs * (Pc * Pc) / (kTwoPi * kTwoPi));
-      const double sq1me2 = sqrt(1.0 - e * e);
+      const double sq1me2 = sqrt_1me2(e);  // NaN at |e| >= 1 (hb_device.hpp)
       double sa, ca;  // (sin, cos) of i (half 0) or omega (half 1)
       sincos(h1 ? p[5] : p[4], &sa, &ca);
       // phase-table rotations: psi = T0 2pi/P (half 0, walkers on the table

@@ -599,7 +599,8 @@ def test_prior_spread_walkers_c2(hbmi, oracle, seed):
 @pytest.mark.parametrize("n", [1024, 1500, 3000, 20000])
 def test_eccentricity_above_one_every_plan(hbmi, oracle, n):
     """Walkers with |e| > 1 (the sampler's hot rungs propose them: e has no
-    upper wall, likelihood3.c:986-1121) take logl_without_light_curve's NaN;
+    upper wall, likelihood3.c:986-1121), and e = -1 exactly (1 - e^2 = 0), take
+    logl_without_light_curve's NaN;
     e < -1 walkers in Roche overflow the sentinel.  One-wave, pair, rows and
     block plans against the oracle: NaN pattern and sentinel exact, the
     finite walkers beside them within 1e-10, and the batch reversed bit for
@@ -614,13 +615,18 @@ def test_eccentricity_above_one_every_plan(hbmi, oracle, n):
     P[16, 3] = np.nextafter(1.0, 2.0)               # the first e with 1 - e^2 < 0
     P[17, 3] = 1.0                                  # sqrt(0): the light curve is computed
     P[18:24, 3] = -1.0 - rng.random(6) * 2.0        # e < -1: Roche or NaN
+    P[24, 3] = -1.0                                 # 1 - e^2 = 0: the reference's beta is 0 / 0
     with HBLikelihood(t, f, s) as L:
         a = L.loglike(P)
         rev = L.loglike(P[::-1].copy())[::-1]
+        tm = L.light_curve(P[[16, 17, 24]])
     assert np.array_equal(a, rev, equal_nan=True)
     ref = oracle.loglike_batch(t, f, s, P, synth.MAG_DEFAULT, synth.MAGERR_DEFAULT, 8)
     assert np.isnan(ref[:17]).all() and np.isnan(a[:17]).all()
     close_logl(a, ref)
+    # templates at |e| >= 1: NaN wherever the reference's are (e = 1 too, though its logL is the Roche sentinel)
+    rt = oracle.light_curve_batch(t, P[[16, 17, 24]], 8)
+    assert np.array_equal(np.isnan(tm), np.isnan(rt))
 
 
 # ------------------------------------------------- full-size (config C4)

@@ -113,7 +113,7 @@ def test_eccentricity_above_one_gives_nan_logl(oracle, tmp_path):
     parameters -- checked on the reference build itself (oracle/_ref, when
     built here; in a child process, since an in-process load would bind its
     loglikelihood() to an already loaded libhbmi.so's global symbol) and on
-    the oracle, over 600 prior-box walkers with e in (1, 50] and e < -1, on a
+    the oracle, over 600 prior-box walkers with e in (1, 50], e < -1 and e = -1, on a
     synthetic and a real light curve."""
     import subprocess
     import sys
@@ -127,9 +127,10 @@ def test_eccentricity_above_one_gives_nan_logl(oracle, tmp_path):
     P[:300, 3] = 1.0 + rng.random(300) ** 3 * 49.0
     P[300:400, 3] = np.nextafter(1.0, 2.0) + rng.random(100) * 1e-6
     P[400:, 3] = -1.0 - rng.random(200) * 10.0
+    P[590:, 3] = -1.0  # 1 - e^2 = 0: beta = (1 + e cos nu) / (1 - e^2) = 0 / 0 (likelihood3.c:266, 326)
     g = golden("lc_real231937440.npz")
     sets = [synth.dataset(300, oracle.light_curve), (g["t"], g["f"], g["s"])]
-    pos, neg = P[:, 3] > 1.0, P[:, 3] < -1.0
+    pos, neg = P[:, 3] > 1.0, P[:, 3] <= -1.0
 
     def check(ll):
         assert np.isnan(ll[pos]).all()
