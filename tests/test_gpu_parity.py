@@ -629,6 +629,34 @@ def test_eccentricity_above_one_every_plan(hbmi, oracle, n):
     assert np.array_equal(np.isnan(tm), np.isnan(rt))
 
 
+@pytest.mark.parametrize("n", [300, 1024, 6001])
+def test_non_finite_parameter_in_each_slot(hbmi, oracle, n):
+    """A NaN, +inf or -inf in any one of the 21 parameters (the C-ABI takes
+    whatever the caller passes): logL against the reference's restatement --
+    NaN where it is NaN, the Roche sentinel and +-inf exactly, finite values
+    within 1e-10 -- on the one-wave (N = 300, 1024) and block (6001) plans."""
+    from hb_mcmc_amd import synth
+    from hb_mcmc_amd.likelihood import HBLikelihood
+
+    t, f, s = synth.dataset(n, oracle.light_curve)
+    # not -inf in the radius-spread slots 7 / 8: a star of radius 0, whose
+    # eclipse factor Norm / (pi R^2) is 0 / 0 -- the reference multiplies it
+    # into every cadence where that star is behind (NaN), the kernels only into
+    # overlapping ones (DESIGN.md section 5)
+    cases = [(v, i) for v in (np.nan, np.inf, -np.inf) for i in range(21) if not (v == -np.inf and i in (7, 8))]
+    P = np.repeat(synth.THETA_STAR[None, :], len(cases) + 1, 0)
+    for r, (v, i) in enumerate(cases):
+        P[r, i] = v
+    with HBLikelihood(t, f, s) as L:
+        ll = L.loglike(P)
+    ref = oracle.loglike_batch(t, f, s, P, synth.MAG_DEFAULT, synth.MAGERR_DEFAULT, 8)
+    assert np.array_equal(np.isnan(ll), np.isnan(ref)), np.flatnonzero(np.isnan(ll) != np.isnan(ref))
+    inf = np.isinf(ref)
+    assert np.array_equal(ll[inf], ref[inf]) and not np.isinf(ll[~inf]).any()
+    fin = np.isfinite(ref)
+    close_logl(ll[fin], ref[fin])
+
+
 # ------------------------------------------------- full-size (config C4)
 def test_full_size_c4_against_oracle_and_properties(hbmi, oracle):
     """W = 65 536, N = 1024 (BASELINE config C4's whole ensemble on one GPU):
