@@ -128,6 +128,30 @@ def plumbing_check(a, rank, world):
                           "plumbing": True, "ranks_seen": got, "config": {"workload": a.config}}), flush=True)
 
 
+def process_group_info(a, rank, world, local, dev):
+    """What the process group saw, all-gathered over it: every rank's id, its
+    LOCAL_RANK, the HIP device ordinal it runs on and that device's PCI
+    location, so an N > 1 line shows N ranks on N distinct devices (or, in a
+    gloo rehearsal, N ranks sharing one).  Collective: every rank calls it."""
+    p = torch.cuda.get_device_properties(dev)
+    mine = torch.tensor([rank, local, dev.index, p.pci_domain_id, p.pci_bus_id, p.pci_device_id],
+                        dtype=torch.int64)
+    if world > 1:
+        on = dev if a.backend == "nccl" else torch.device("cpu")
+        out = torch.empty(world * mine.numel(), dtype=torch.int64, device=on)
+        dist.all_gather_into_tensor(out, mine.to(on))
+        rows = out.cpu().view(world, -1).tolist()
+    else:
+        rows = [mine.tolist()]
+    ranks = [{"rank": r[0], "local_rank": r[1], "device": r[2],
+              "pci": f"{r[3]:04x}:{r[4]:02x}:{r[5]:02x}"} for r in rows]
+    return {"world_size": dist.get_world_size() if world > 1 else 1,
+            "backend": dist.get_backend() if world > 1 else None,
+            "ranks_seen": [r["rank"] for r in ranks],
+            "distinct_devices": len({r["pci"] for r in ranks}),
+            "ranks": ranks, "device_name": p.name, "devices_visible": torch.cuda.device_count()}
+
+
 def cpu_threads() -> int:
     try:
         n = len(os.sched_getaffinity(0))
@@ -340,7 +364,13 @@ def prior_spread(L, n, w, steps, stream, dev, timer, ks=50):
                             "log P fixed, T0 folded"}
 
 
-def dropin_rate(niter):
+DROPIN_LEGS = (("dropin", "hb_mcmc_ref_hbmi", {}),
+               ("dropin_memo_off", "hb_mcmc_ref_hbmi", {"HBMI_DROPIN_MEMO": "0"}),
+               ("dropin_profile", "hb_mcmc_ref_hbmi", {"HBMI_DROPIN_PROFILE": "1"}),
+               ("reference_cpu", "hb_mcmc_ref", {}))
+
+
+def dropin_rate(niter, legs=DROPIN_LEGS):
     """The literal north_star drop-in: the reference's OWN sampler
     (src/mcmc_wrapper2.c, unmodified, 25 OpenMP threads) relinked against
     libhbmi.so (`make -C oracle dropin` -> oracle/_ref/hb_mcmc_ref_hbmi), so
@@ -360,7 +390,7 @@ def dropin_rate(niter):
     g = np.load(os.path.join(ROOT, "tests", "golden", "sampler_127079833.npz"))
     out = {"niter": niter, "chains": 50, "light_curve": f"TIC 127079833 folded, N = {len(g['lc_t'])}",
            "unit": "sampler iterations/s (100 scalar loglikelihood() calls each)"}
-    for key, name in (("dropin", "hb_mcmc_ref_hbmi"), ("reference_cpu", "hb_mcmc_ref")):
+    for key, name, extra in legs:
         path = os.path.join(ROOT, "oracle", "_ref", name)
         if not os.path.exists(path):
             continue
@@ -371,14 +401,33 @@ def dropin_rate(niter):
             for sub in ("subpars", "pars", "chains", "logL", "log", "lightcurves/mcmc_lightcurves"):
                 os.makedirs(os.path.join(tmp, "data", sub), exist_ok=True)
             os.makedirs(os.path.join(tmp, "debug"))
+            stats_path = os.path.join(tmp, "dropin_stats.json")
+            env = dict(os.environ, HBREF_ROOT=tmp, **extra)
+            if name == "hb_mcmc_ref_hbmi":
+                env["HBMI_DROPIN_STATS"] = stats_path  # libhbmi writes its drop-in counters at exit
             t0 = time.perf_counter()
             r = subprocess.run([path, str(niter), "127079833", "0.5021", "0"], cwd=tmp, capture_output=True,
-                               text=True, timeout=600, env=dict(os.environ, HBREF_ROOT=tmp))
+                               text=True, timeout=600, env=env)
             dt = time.perf_counter() - t0
+            st = None
+            if os.path.exists(stats_path):
+                with open(stats_path) as fp:
+                    st = json.load(fp)
         if r.returncode != 0:
             out[key] = {"error": r.stderr[-300:]}
             continue
         out[key] = {"iters_per_s": niter / dt, "loglik_calls_per_s": 100.0 * niter / dt, "wall_s": dt}
+        if extra:
+            out[key]["env"] = extra
+        if st:  # per-iteration breakdown of the drop-in's GPU round trips (hb_dropin.hpp Stats)
+            b = max(1, st["batches"])
+            st["batches_per_iter"] = st["batches"] / niter
+            st["mean_batch"] = st["walkers"] / b
+            st["memo_hit_frac"] = st["memo_hits"] / max(1, st["calls"])
+            st["us_per_batch"] = {k[2:]: st[k] / b * 1e6 for k in ("s_combine", "s_upload", "s_launch",
+                                                                   "s_download_sync")}
+            st["us_wake_per_waiter"] = st["s_wake"] / max(1, st["walkers"] - st["batches"]) * 1e6
+            out[key]["stats"] = st
     if "iters_per_s" in out.get("dropin", {}) and "iters_per_s" in out.get("reference_cpu", {}):
         out["speedup_vs_reference_cpu"] = out["dropin"]["iters_per_s"] / out["reference_cpu"]["iters_per_s"]
     return out
@@ -456,7 +505,7 @@ def make_event(kind):
     return _HipEvent() if kind == "hip" else torch.cuda.Event(enable_timing=True)
 
 
-def run_c5(a, rank, world, local, dev):
+def run_c5(a, rank, world, local, dev, pg):
     """Catalog sweep (BASELINE config C5): every step evaluates all local
     targets' walkers with one hb_catalog call (one prep launch + one eval
     launch per size class).  Targets are dealt over ranks by cadence count;
@@ -543,6 +592,8 @@ def run_c5(a, rank, world, local, dev):
                                      {"kernel": "hb_catalog call (hb_prep_kernel + hb_eval_catalog_kernel, every "
                                                 "size class in one launch), rank 0", "kernel_ms": call_ms, "kernel_event_samples": ks,
                                       "kernel_timer": a.timer})}
+        if world > 1:
+            line["process_group"] = pg
         print(json.dumps(line), flush=True)
 
 
@@ -569,11 +620,13 @@ def main():
         if world > 1:
             dist.destroy_process_group()
         return
+    local_rank = local
     local = local % max(1, torch.cuda.device_count())  # rehearsal: several ranks may share one GPU (gloo)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    pg = process_group_info(a, rank, world, local_rank, dev)
     if a.config == "C5":
-        run_c5(a, rank, world, local, dev)
+        run_c5(a, rank, world, local, dev, pg)
         if world > 1:
             dist.destroy_process_group()
         return
@@ -668,8 +721,13 @@ def main():
         wall, eval_ms, prep_ms = (float(x) for x in tt.tolist())
     # sanity: the reference's model itself yields NaN for a rare walker (eclipse_area's asin
     # outside its domain, likelihood3.c:353-389) -- reproduced, counted, never more than a trace
+    gather_ok = None
     if world > 1:  # the last all-gather holds every rank's logL of that batch, this rank's at its offset
         assert np.array_equal(gl[rank * w:(rank + 1) * w], lv, equal_nan=True), "all-gather mismatch"
+        # ... and every other rank's: each rank checks its own slice, rank 0 reports the AND
+        ok = torch.tensor([1.0], dtype=torch.float64, device=dev if a.backend == "nccl" else "cpu")
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        gather_ok = bool(ok.item() == 1.0)
     nonfinite = int((~np.isfinite(lv)).sum())
     assert nonfinite <= max(1, w // 100), f"{nonfinite} non-finite logL of {w}"
 
@@ -712,6 +770,10 @@ def main():
             "kernel_only_evals_per_s": w / ((eval_ms + prep_ms) * 1e-3),
             "nonfinite_logl_last_batch": nonfinite,
         }
+        if world > 1:
+            line["process_group"] = pg
+            line["allgather_check"] = {"ok": gather_ok, "doubles_per_step": world * w,
+                                       "what": "last timed step's gathered logL equals each rank's own, on every rank"}
         if world == 1 and a.prior_steps > 0 and n <= 2048:
             line["c2_prior_spread"] = prior_spread(L, n, w, a.prior_steps, stream, dev, a.timer)
         if world == 1 and a.sampler_iters > 0:

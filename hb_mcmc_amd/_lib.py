@@ -105,6 +105,11 @@ def _declare(lib):
     lib.partition.argtypes = [_PD, _I, _I]
     lib.set_limits.argtypes = [_VP, _VP, _VP, _D]
     lib.initialize_proposals.argtypes = [_PD, _VP]
+    # internal: drop-in bookkeeping (hb_dropin.hpp) -- stats, memo switch, hash test hook
+    lib.hbx_dropin_stats.restype = _I
+    lib.hbx_dropin_stats.argtypes = [_PD, _I]
+    lib.hbx_dropin_set_memo.argtypes = [_I]
+    lib.hbx_dropin_test_hash.argtypes = [_I]
     return lib
 
 

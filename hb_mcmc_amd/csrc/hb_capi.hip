@@ -7,12 +7,14 @@
 // Part 2: the batched context API (hb_create / hb_loglik_batch...).
 #include <hip/hip_runtime.h>
 
+#include <limits.h>
 #include <math.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
+#include <atomic>
 #include <memory>
 #include <condition_variable>
 #include <mutex>
@@ -22,6 +24,7 @@
 
 #include "hb_accept.hpp"
 #include "hb_device.hpp"
+#include "hb_dropin.hpp"
 #include "hb_internal.hpp"
 
 
@@ -564,6 +567,10 @@ extern "C" hb_catalog* hb_catalog_create(int ntargets, const double* const* t, c
     c->cls[k] = catalog_class_of(n[k]);
     total += n[k];
   }
+  if (total > (long)INT_MAX) {  // the prep kernel indexes the concatenated cadences with 32-bit ints
+    set_err_msg("hb_catalog_create: more than INT_MAX cadences over all targets");
+    return nullptr;
+  }
   c->ncad = total;
   std::vector<double> ht((size_t)total), hf((size_t)total), hs((size_t)total);
   for (int k = 0; k < ntargets; ++k) {
@@ -798,128 +805,230 @@ void require_device() {
   }
 }
 
-uint64_t mix64(uint64_t h, uint64_t v) {
-  h ^= v + 0x9e3779b97f4a7c15ull + (h << 6) + (h >> 2);
-  h *= 0xbf58476d1ce4e5b9ull;
-  return h ^ (h >> 31);
-}
-// four independent lanes (the multiply chains overlap), folded at the end
-uint64_t hash_doubles(uint64_t h, const double* a, long n) {
-  uint64_t l[4] = {h, h ^ 0x1111, h ^ 0x2222, h ^ 0x3333};
-  long i = 0;
-  for (; i + 4 <= n; i += 4)
-    for (int k = 0; k < 4; ++k) {
-      uint64_t v;
-      memcpy(&v, a + i + k, 8);
-      l[k] = mix64(l[k], v);
-    }
-  for (; i < n; ++i) {
-    uint64_t v;
-    memcpy(&v, a + i, 8);
-    l[0] = mix64(l[0], v);
-  }
-  return mix64(mix64(mix64(mix64(l[0], l[1]), l[2]), l[3]), (uint64_t)n);
+// Resident light curves of the likelihood3.h drop-in (hb_dropin.hpp: exact
+// cache, logL memo, call combiner), shared by every caller thread: the
+// reference sampler calls loglikelihood() with the same arrays from its 25
+// OpenMP threads (mcmc_wrapper2.c:383-489).  A context here is the batched
+// hb_ctx plus the drop-in's own stream and pinned staging, so a combined batch
+// is one H2D DMA of its rows, the launch and one D2H DMA of its logL values on
+// a stream that waits for nothing else.
+double env_num(const char* name, double dflt) {
+  const char* e = getenv(name);
+  return e && *e ? atof(e) : dflt;
 }
 
-// Resident light curves of the likelihood3.h drop-in, shared by every caller
-// thread: the reference sampler calls loglikelihood() with the same arrays
-// from its 25 OpenMP threads (mcmc_wrapper2.c:383-489).
-//
-// Call combiner: concurrent loglikelihood() calls on one light curve are
-// evaluated together.  A caller queues its parameter vector; if no launch is
-// in flight it becomes the leader, takes every queued request and evaluates
-// them as one batch (one H2D copy, one prep + eval launch pair, one D2H copy);
-// the others sleep until their result is written.  Requests that arrive while
-// a batch runs form the next batch.  Each walker's logL does not depend on the
-// batch it rides in (the kernels evaluate walkers independently).
-struct DropReq {
-  const double* p;
-  double out;
-  bool done;
+// Drop-in policy knobs, read once (A/B runs; defaults measured in
+// profiles/r06*_dropin_ab.txt): HBMI_DROPIN_SPIN_US, HBMI_DROPIN_WINDOW_US
+// (hb_dropin.hpp Entry), HBMI_DROPIN_ZC=1 (the batch's rows read and its logL
+// written by the kernels in pinned host memory, no DMA copies),
+// HBMI_DROPIN_POLL=1 (the leader polls the stream instead of
+// hipStreamSynchronize), HBMI_DROPIN_LAT=1 (the multi-wave latency plan).
+struct DropPolicy {
+  double spin_s, window_s;
+  bool zc, poll, lat;
 };
-struct DropinCtx {
-  uint64_t key = 0;
-  hb_ctx* ctx = nullptr;
-  std::mutex mu;
-  std::condition_variable cv;
-  std::vector<DropReq*> pending;
-  bool busy = false;
-  std::vector<double> params, out;  // the leader's staging
-  uint64_t last_use = 0;
+const DropPolicy& drop_policy() {
+  static const DropPolicy p{env_num("HBMI_DROPIN_SPIN_US", 0) * 1e-6, env_num("HBMI_DROPIN_WINDOW_US", 0) * 1e-6,
+                            env_num("HBMI_DROPIN_ZC", 0) != 0, env_num("HBMI_DROPIN_POLL", 0) != 0,
+                            env_num("HBMI_DROPIN_LAT", 0) != 0};
+  return p;
+}
+
+struct DropCtx {
+  hb_ctx* c = nullptr;
+  hipStream_t s = nullptr;
+  double* h_params = nullptr;  // pinned, hcap x 21
+  double* h_out = nullptr;     // pinned, hcap
+  double* dv_params = nullptr;  // their device addresses (zero-copy mode)
+  double* dv_out = nullptr;
+  int hcap = 0;
 };
-struct DropinCache {
-  std::mutex mu;
-  std::vector<std::shared_ptr<DropinCtx>> ents;
-  uint64_t tick = 0;
-};
+
+void dropctx_destroy(DropCtx* d) {
+  if (!d) return;
+  if (d->c) (void)hipSetDevice(d->c->device);
+  if (d->h_params) (void)hipHostFree(d->h_params);
+  if (d->h_out) (void)hipHostFree(d->h_out);
+  if (d->s) (void)hipStreamDestroy(d->s);
+  hb_destroy(d->c);
+  delete d;
+}
+
+DropCtx* dropctx_create(const double* t, const double* f, const double* s, long n, const double* mag,
+                        const double* err) {
+  std::unique_ptr<DropCtx> d(new DropCtx);
+  d->c = hb_create(t, f, s, n, mag, err, 0);
+  if (!d->c) return nullptr;
+  if (drop_policy().lat) (void)hb_ctx_set_latency_plan(d->c, 1);
+  if (hipStreamCreateWithFlags(&d->s, hipStreamNonBlocking) != hipSuccess) {
+    set_err_msg("drop-in: hipStreamCreateWithFlags failed");
+    dropctx_destroy(d.release());
+    return nullptr;
+  }
+  return d.release();
+}
+
+// pinned staging for w rows (the combiner writes the batch's rows here)
+double* dropctx_stage(DropCtx* d, int w) {
+  if (w > d->hcap) {
+    const int cap = std::max(w, 2 * d->hcap);
+    if (d->h_params) (void)hipHostFree(d->h_params);
+    if (d->h_out) (void)hipHostFree(d->h_out);
+    d->h_params = d->h_out = nullptr;
+    d->hcap = 0;
+    // coherent (fine-grained): in zero-copy mode the kernels read the rows and
+    // write the logL values here directly, nothing may sit in a GPU cache
+    const unsigned fl = hipHostMallocMapped | hipHostMallocCoherent;
+    if (hipHostMalloc((void**)&d->h_params, sizeof(double) * 21 * (size_t)cap, fl) != hipSuccess ||
+        hipHostMalloc((void**)&d->h_out, sizeof(double) * (size_t)cap, fl) != hipSuccess ||
+        hipHostGetDevicePointer((void**)&d->dv_params, d->h_params, 0) != hipSuccess ||
+        hipHostGetDevicePointer((void**)&d->dv_out, d->h_out, 0) != hipSuccess)
+      hb_fatal("drop-in: hipHostMalloc failed");
+    d->hcap = cap;
+  }
+  return d->h_params;
+}
+
+// Profile mode (HBMI_DROPIN_PROFILE=1): synchronise after the upload and after
+// the launch, so the stats split the device time between the three steps
+// (each wait adds a round trip: for the breakdown only).
+bool dropin_profile() {
+  static const bool on = [] {
+    const char* e = getenv("HBMI_DROPIN_PROFILE");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
+
+int dropctx_eval(DropCtx* d, const double* rows, int w, double* out, hbdrop::Times* tm) {
+  hb_ctx* c = d->c;
+  const DropPolicy& pol = drop_policy();
+  const bool prof = dropin_profile();
+  std::lock_guard<std::mutex> lk(c->mu);  // the context's workspace and staging (calc_light_curve shares them)
+  HB_TRY(hipSetDevice(c->device), "hipSetDevice");
+  if (w > c->cap) {
+    int rc = hb_reserve(c, w);
+    if (rc) return rc;
+  }
+  int rc = ctx_host_staging(c, w, false);
+  if (rc) return rc;
+  if (rows != d->h_params) dropctx_stage(d, w), memcpy(d->h_params, rows, sizeof(double) * 21 * (size_t)w);
+  auto wait = [&]() -> hipError_t {
+    if (!pol.poll) return hipStreamSynchronize(d->s);
+    hipError_t e;
+    while ((e = hipStreamQuery(d->s)) == hipErrorNotReady) hbdrop::Entry<DropCtx>::relax();
+    return e;
+  };
+  const double t0 = hbdrop::now_s();
+  const double* dp = pol.zc ? d->dv_params : c->d_params;
+  double* dout = pol.zc ? d->dv_out : c->d_out;
+  if (!pol.zc)
+    HB_TRY(hipMemcpyAsync(c->d_params, d->h_params, sizeof(double) * 21 * (size_t)w, hipMemcpyHostToDevice, d->s),
+           "drop-in upload");
+  if (prof) HB_TRY(wait(), "hipStreamSynchronize");
+  const double t1 = hbdrop::now_s();
+  rc = run_batch(c, dp, w, dout, nullptr, d->s);
+  if (rc) return rc;
+  if (prof) HB_TRY(wait(), "hipStreamSynchronize");
+  const double t2 = hbdrop::now_s();
+  if (!pol.zc)
+    HB_TRY(hipMemcpyAsync(d->h_out, c->d_out, sizeof(double) * (size_t)w, hipMemcpyDeviceToHost, d->s),
+           "drop-in download");
+  HB_TRY(wait(), "hipStreamSynchronize");
+  const double t3 = hbdrop::now_s();
+  memcpy(out, d->h_out, sizeof(double) * (size_t)w);
+  tm->upload = t1 - t0;
+  tm->launch = t2 - t1;
+  tm->download = t3 - t2;
+  return 0;
+}
+
+void dropin_write_stats();
+
 // never destroyed: contexts outlive static destruction (the HIP runtime may
-// already be gone then); at most kDropinMax light curves stay resident
-DropinCache& dropin_cache() {
-  static DropinCache* c = new DropinCache;
+// already be gone then); at most hbdrop::kCacheMax light curves stay resident
+hbdrop::Cache<DropCtx>& dropin_cache() {
+  static hbdrop::Cache<DropCtx>* c = [] {
+    if (getenv("HBMI_DROPIN_STATS")) atexit(dropin_write_stats);
+    return new hbdrop::Cache<DropCtx>(dropctx_create, dropctx_destroy, hbdrop::kCacheMax,
+                                      [](hbdrop::Entry<DropCtx>& e) {
+                                        e.spin_s = drop_policy().spin_s;
+                                        e.window_s = drop_policy().window_s;
+                                      });
+  }();
   return *c;
 }
-constexpr size_t kDropinMax = 8;
 
-std::shared_ptr<DropinCtx> dropin_ctx(const double* t, const double* f, const double* s, long n,
-                                      const double* mag, const double* err) {
-  uint64_t key = hash_doubles(0x5eed, t, n);
-  key = hash_doubles(key, f, n);
-  key = hash_doubles(key, s, n);
-  key = hash_doubles(key, mag, 5);
-  key = hash_doubles(key, err, 4);
-  DropinCache& dc = dropin_cache();
-  std::lock_guard<std::mutex> lk(dc.mu);
-  for (auto& e : dc.ents)
-    if (e->key == key) {
-      e->last_use = ++dc.tick;
-      return e;
-    }
-  if (dc.ents.size() >= kDropinMax) {  // evict the least recently used idle entry
-    size_t victim = dc.ents.size();
-    for (size_t i = 0; i < dc.ents.size(); ++i)
-      if (dc.ents[i].use_count() == 1 && (victim == dc.ents.size() || dc.ents[i]->last_use < dc.ents[victim]->last_use))
-        victim = i;
-    if (victim < dc.ents.size()) {
-      hb_destroy(dc.ents[victim]->ctx);
-      dc.ents.erase(dc.ents.begin() + (long)victim);
-    }
+// HBMI_DROPIN_MEMO=0 turns the logL memo off (A/B runs); default on;
+// hbx_dropin_set_memo switches it at run time (tests)
+std::atomic<int> g_dropin_memo{-1};
+bool dropin_memo_on() {
+  int v = g_dropin_memo.load(std::memory_order_relaxed);
+  if (v < 0) {
+    const char* e = getenv("HBMI_DROPIN_MEMO");
+    v = (e && e[0] == '0') ? 0 : 1;
+    g_dropin_memo.store(v, std::memory_order_relaxed);
   }
-  auto e = std::make_shared<DropinCtx>();
-  e->key = key;
-  e->ctx = hb_create(t, f, s, n, mag, err, 0);
-  if (!e->ctx) hb_fatal("hb_create failed");
-  e->last_use = ++dc.tick;
-  dc.ents.push_back(e);
+  return v != 0;
+}
+
+std::shared_ptr<hbdrop::Entry<DropCtx>> dropin_ctx(const double* t, const double* f, const double* s, long n,
+                                                   const double* mag, const double* err) {
+  auto e = dropin_cache().get(t, f, s, n, mag, err);
+  if (!e) hb_fatal("hb_create failed");
+  e->use_memo = dropin_memo_on();
   return e;
 }
 
-double dropin_loglik(DropinCtx& d, const double* params) {
-  DropReq r{params, 0.0, false};
-  std::unique_lock<std::mutex> lk(d.mu);
-  d.pending.push_back(&r);
-  for (;;) {
-    if (r.done) return r.out;
-    if (!d.busy) {  // lead: evaluate every queued request (this one included)
-      d.busy = true;
-      std::vector<DropReq*> batch;
-      batch.swap(d.pending);
-      lk.unlock();
-      const int w = (int)batch.size();
-      d.params.resize((size_t)w * 21);
-      d.out.resize((size_t)w);
-      for (int i = 0; i < w; ++i) memcpy(&d.params[(size_t)i * 21], batch[(size_t)i]->p, 21 * sizeof(double));
-      if (hb_loglik_batch(d.ctx, d.params.data(), w, d.out.data(), nullptr) != 0) hb_fatal("hb_loglik_batch failed");
-      lk.lock();
-      for (int i = 0; i < w; ++i) {
-        batch[(size_t)i]->out = d.out[(size_t)i];
-        batch[(size_t)i]->done = true;
-      }
-      d.busy = false;
-      d.cv.notify_all();
-      continue;
-    }
-    d.cv.wait(lk);
+void stats_sum(hbdrop::Stats& a, const hbdrop::Stats& b) {
+  a.calls += b.calls;
+  a.memo_hits += b.memo_hits;
+  a.batches += b.batches;
+  a.walkers += b.walkers;
+  a.max_batch = std::max(a.max_batch, b.max_batch);
+  a.s_combine += b.s_combine;
+  a.s_upload += b.s_upload;
+  a.s_launch += b.s_launch;
+  a.s_download += b.s_download;
+  a.s_wake += b.s_wake;
+}
+
+hbdrop::Stats dropin_totals(uint64_t* contexts) {
+  hbdrop::Stats tot;
+  auto ents = dropin_cache().entries();
+  for (auto& e : ents) {
+    std::lock_guard<std::mutex> lk(e->mu);
+    hbdrop::Stats x = e->st;
+    x.s_wake = 1e-9 * (double)e->wake_ns.load();
+    stats_sum(tot, x);
   }
+  if (contexts) *contexts = dropin_cache().created();
+  return tot;
+}
+
+void dropin_write_stats() {
+  const char* path = getenv("HBMI_DROPIN_STATS");
+  if (!path) return;
+  uint64_t created = 0;
+  const hbdrop::Stats s = dropin_totals(&created);
+  FILE* fp = fopen(path, "w");
+  if (!fp) return;
+  fprintf(fp,
+          "{\"calls\": %llu, \"memo_hits\": %llu, \"batches\": %llu, \"walkers\": %llu, \"max_batch\": %llu, "
+          "\"contexts_created\": %llu, \"profile_mode\": %s, \"s_combine\": %.9g, \"s_upload\": %.9g, "
+          "\"s_launch\": %.9g, \"s_download_sync\": %.9g, \"s_wake\": %.9g}\n",
+          (unsigned long long)s.calls, (unsigned long long)s.memo_hits, (unsigned long long)s.batches,
+          (unsigned long long)s.walkers, (unsigned long long)s.max_batch, (unsigned long long)created,
+          dropin_profile() ? "true" : "false", s.s_combine, s.s_upload, s.s_launch, s.s_download, s.s_wake);
+  fclose(fp);
+}
+
+double dropin_loglik(hbdrop::Entry<DropCtx>& d, const double* params) {
+  static const hbdrop::Eval<DropCtx> eval = dropctx_eval;
+  static const std::function<double*(DropCtx*, int)> stage = dropctx_stage;
+  double v = 0.0;
+  if (d.call(params, &v, eval, stage) != 0) hb_fatal("hb_loglik_batch failed");
+  return v;
 }
 
 struct DevBuf {
@@ -954,9 +1063,9 @@ double probe(int op, const double* in, int nin, double* out, int nout) {
 }
 
 hb_ctx* cached_ctx(const double* t, const double* f, const double* s, long n, const double* mag,
-                   const double* err, std::shared_ptr<DropinCtx>& hold) {
+                   const double* err, std::shared_ptr<hbdrop::Entry<DropCtx>>& hold) {
   hold = dropin_ctx(t, f, s, n, mag, err);
-  return hold->ctx;
+  return hold->ctx->c;
 }
 
 }  // namespace
@@ -967,15 +1076,46 @@ extern "C" double loglikelihood(double time[], double lightcurve[], double noise
   // caller-visible side effect of the reference (likelihood3.c:824-827)
   for (long i = 0; i < N; ++i)
     if (noise[i] < 1.e-5) noise[i] = 1.e-5;
-  std::shared_ptr<DropinCtx> d = dropin_ctx(time, lightcurve, noise, N, mag_data, magerr);
+  auto d = dropin_ctx(time, lightcurve, noise, N, mag_data, magerr);
   return dropin_loglik(*d, params);
+}
+
+// internal (tests, bench): the drop-in's running totals over every resident
+// context -- {calls, memo_hits, batches, walkers, max_batch, contexts created,
+// s_combine, s_upload, s_launch, s_download_sync, s_wake}; returns the count
+// written (at most n)
+extern "C" int hbx_dropin_stats(double* out, int n) {
+  uint64_t created = 0;
+  const hbdrop::Stats s = dropin_totals(&created);
+  const double v[11] = {(double)s.calls, (double)s.memo_hits, (double)s.batches, (double)s.walkers,
+                        (double)s.max_batch, (double)created, s.s_combine, s.s_upload, s.s_launch,
+                        s.s_download, s.s_wake};
+  const int k = std::min(n, 11);
+  for (int i = 0; i < k; ++i) out[i] = v[i];
+  return k;
+}
+
+// internal (tests, A/B): the logL memo on (1) or off (0) for later calls
+extern "C" int hbx_dropin_set_memo(int on) {
+  g_dropin_memo.store(on ? 1 : 0, std::memory_order_relaxed);
+  return 0;
+}
+
+// internal (tests): mode 1 gives every light curve the same cache key, so
+// distinct light curves meet on one hash and must still get their own
+// contexts; mode 0 restores the hash
+extern "C" int hbx_dropin_test_hash(int mode) {
+  dropin_cache().set_hash(mode == 1 ? [](const double*, const double*, const double*, long, const double*,
+                                         const double*) -> uint64_t { return 42; }
+                                    : nullptr);
+  return 0;
 }
 
 extern "C" void calc_light_curve(double* times, long Nt, double* pars, double* tmpl) {
   require_device();
   std::vector<double> zeros((size_t)Nt, 0.0), ones((size_t)Nt, 1.0);
   const double mag[5] = {1000., 1., 1., 1., 1.}, err[4] = {1e15, 1e15, 1e15, 1e15};
-  std::shared_ptr<DropinCtx> hold;
+  std::shared_ptr<hbdrop::Entry<DropCtx>> hold;
   hb_ctx* c = cached_ctx(times, zeros.data(), ones.data(), Nt, mag, err, hold);
   if (hb_light_curve_batch(c, pars, 1, tmpl, nullptr) != 0) hb_fatal("hb_light_curve_batch failed");
 }

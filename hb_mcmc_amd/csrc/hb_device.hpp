@@ -85,15 +85,6 @@ struct alignas(16) WalkerConst {
 };
 static_assert(sizeof(WalkerConst) == 48 * 8, "WalkerConst layout");
 
-// logL mode: a walker whose logL is decided without its light curve.
-//  * Roche overflow: chi^2 is replaced by 1e15 whatever the template is
-//    (likelihood3.c:866-869): logL = -5e14.
-//  * |e| > 1 (the sampler puts no upper wall on e, likelihood3.c:986-1121, so
-//    hot rungs propose it): sqrt(1 - e^2) is NaN, and with it every cadence's
-//    flux (traj, likelihood3.c:147-182), the median, chi^2 and the reference's
-//    logL -- a NaN (+qNaN, what the reference build returns for every such
-//    walker checked); a NaN logL is only ever rejected by the Hastings test.
-// Returns false when the light curve is needed.
 // sqrt(1 - e^2) of the record, NaN at |e| = 1 as well as above: there the
 // reference divides by 1 - e^2 = 0 (beta = (1 + e cos nu) / (1 - e^2) = 0 / 0,
 // likelihood3.c:266, 326; the beaming factor's / sqrt(1 - e^2), :230) and its
@@ -103,6 +94,17 @@ __device__ __forceinline__ double sqrt_1me2(double e) {
   const double d = 1.0 - e * e;
   return d == 0.0 ? __builtin_nan("") : sqrt(d);
 }
+
+// logL mode: a walker whose logL is decided without its light curve.
+//  * Roche overflow: chi^2 is replaced by 1e15 whatever the template is
+//    (likelihood3.c:866-869): logL = -5e14.
+//  * |e| >= 1 (the sampler puts no upper wall on e, likelihood3.c:986-1121, so
+//    hot rungs propose it): sqrt(1 - e^2) is NaN (sqrt_1me2, |e| = 1
+//    included), and with it every cadence's flux (traj, likelihood3.c:147-182),
+//    the median, chi^2 and the reference's logL -- a NaN (+qNaN, what the
+//    reference build returns for every such walker checked); a NaN logL is only
+//    ever rejected by the Hastings test.
+// Returns false when the light curve is needed.
 
 __device__ __forceinline__ bool logl_without_light_curve(const WalkerConst& w, double& ll) {
   if (w.roche != 0.0) {

@@ -1518,6 +1518,10 @@ extern "C" hb_dsampler* hb_dsampler_create_shard(hb_sampler* s, hb_ctx* ctx, con
   return ds_create(s, ctx, chain_of_slot, nranks, rank);
 }
 
+// A deferred tempering swap still pending here (pend_on) is dropped on
+// purpose: the device state goes with the sampler.  Every entry point that
+// READS the state (download, gather, sync, init_logl, the event drain) calls
+// ds_flush first; a new reader must do the same.
 extern "C" void hb_dsampler_destroy(hb_dsampler* d) { delete d; }
 
 // host sampler (owned slots, by slot) -> device (by chain); chain_of_slot

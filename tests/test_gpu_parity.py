@@ -481,6 +481,9 @@ def test_dropin_concurrent_calls_are_combined_exactly(hbmi):
     solo = [hbmi.loglikelihood(p(t), p(f), p(s), len(t), p(P[i].copy()), p(mag), p(err)) for i in range(24)]
     solo2 = [hbmi.loglikelihood(p(t2), p(f2), p(s2), len(t2), p(P[i].copy()), p(mag), p(err)) for i in range(24)]
     res, res2, errs = {}, {}, []
+    # with the logL memo on, every threaded call below would be answered from
+    # the table; off, they are combined into launches
+    hbmi.hbx_dropin_set_memo(0)
 
     def worker(k):
         try:
@@ -495,10 +498,13 @@ def test_dropin_concurrent_calls_are_combined_exactly(hbmi):
             errs.append(e)
 
     th = [threading.Thread(target=worker, args=(k,)) for k in range(16)]
-    for x in th:
-        x.start()
-    for x in th:
-        x.join()
+    try:
+        for x in th:
+            x.start()
+        for x in th:
+            x.join()
+    finally:
+        hbmi.hbx_dropin_set_memo(1)
     assert not errs
     assert len(res) + len(res2) == 16 * 24
     for i, v in res.values():
@@ -506,6 +512,77 @@ def test_dropin_concurrent_calls_are_combined_exactly(hbmi):
     for i, v in res2.values():
         assert v == solo2[i] or (np.isnan(v) and np.isnan(solo2[i]))
     close_logl(solo, g["logl"][:24])
+
+
+def _dropin_stats(hbmi):
+    out = np.zeros(11)
+    assert hbmi.hbx_dropin_stats(p(out), 11) == 11
+    return dict(zip(("calls", "memo_hits", "batches", "walkers", "max_batch", "created"), out[:6]))
+
+
+def test_dropin_memo_hit_and_bit_flip(hbmi):
+    """mcmc_wrapper2.c:488 re-asks for logL of x[chain_id], a state the library
+    has evaluated already: the drop-in answers it from the context's memo
+    (exact parameter bytes) without a launch.  One flipped mantissa bit is a
+    fresh evaluation, and every value equals the batched API's for the same
+    vector bit for bit.  A second light curve one ulp away gets its own
+    context and memo."""
+    from hb_mcmc_amd.likelihood import HBLikelihood
+
+    g = golden("lc_synth1024.npz")
+    t, s = g["t"].copy(), g["s"].copy()
+    f = g["f"].copy()
+    f[5] = np.nextafter(f[5], 2.0)  # a light curve no earlier test used: a fresh context
+    mag, err = g["mag"].copy(), g["magerr"].copy()
+    P = np.ascontiguousarray(g["params"][:3]).copy()
+    q = P[1].copy()
+    q.view(np.uint64)[4] ^= np.uint64(1)  # lowest mantissa bit of the inclination
+    with HBLikelihood(t, f, np.maximum(s, 1e-5), g["mag"], g["magerr"]) as L:
+        want = L.loglike(np.vstack([P, q[None, :]]))
+    s0 = _dropin_stats(hbmi)
+    v0 = hbmi.loglikelihood(p(t), p(f), p(s), len(t), p(P[1].copy()), p(mag), p(err))
+    s1 = _dropin_stats(hbmi)
+    assert s1["created"] == s0["created"] + 1 and s1["batches"] == s0["batches"] + 1
+    v1 = hbmi.loglikelihood(p(t), p(f), p(s), len(t), p(P[1].copy()), p(mag), p(err))
+    s2 = _dropin_stats(hbmi)
+    assert s2["memo_hits"] == s1["memo_hits"] + 1 and s2["batches"] == s1["batches"]
+    vq = hbmi.loglikelihood(p(t), p(f), p(s), len(t), p(q), p(mag), p(err))
+    s3 = _dropin_stats(hbmi)
+    assert s3["batches"] == s2["batches"] + 1 and s3["memo_hits"] == s2["memo_hits"]
+    assert v0 == want[1] and v1 == want[1] and vq == want[3]
+    # the other light curve (f one ulp apart at cadence 5) is its own context
+    f0 = g["f"].copy()
+    u = hbmi.loglikelihood(p(t), p(f0), p(s), len(t), p(P[1].copy()), p(mag), p(err))
+    with HBLikelihood(t, f0, np.maximum(s, 1e-5), g["mag"], g["magerr"]) as L0:
+        assert u == L0.loglike(P[1:2])[0]
+
+
+def test_dropin_light_curves_on_one_hash_key_stay_apart(hbmi):
+    """Every light curve forced onto one cache key (hbx_dropin_test_hash): two
+    light curves that differ in one flux value still get two contexts, and
+    each call evaluates its own arrays (the full compare behind a hash hit)."""
+    from hb_mcmc_amd.likelihood import HBLikelihood
+
+    g = golden("lc_synth1024.npz")
+    t, s = g["t"].copy(), g["s"].copy()
+    fa, fb = g["f"].copy(), g["f"].copy()
+    fa[9] += 1e-3
+    fb[9] -= 1e-3
+    mag, err = g["mag"].copy(), g["magerr"].copy()
+    pv = g["params"][2].copy()
+    hbmi.hbx_dropin_test_hash(1)
+    try:
+        c0 = _dropin_stats(hbmi)["created"]
+        va = hbmi.loglikelihood(p(t), p(fa), p(s), len(t), p(pv), p(mag), p(err))
+        vb = hbmi.loglikelihood(p(t), p(fb), p(s), len(t), p(pv), p(mag), p(err))
+        va2 = hbmi.loglikelihood(p(t), p(fa.copy()), p(s), len(t), p(pv), p(mag), p(err))
+        assert _dropin_stats(hbmi)["created"] == c0 + 2
+    finally:
+        hbmi.hbx_dropin_test_hash(0)
+    for fx, v in ((fa, va), (fb, vb), (fa, va2)):
+        with HBLikelihood(t, fx, np.maximum(s, 1e-5), g["mag"], g["magerr"]) as L:
+            assert v == L.loglike(pv[None, :])[0]
+    assert va != vb
 
 
 # ------------------------------------------------- fused launch
@@ -613,7 +690,7 @@ def test_eccentricity_above_one_every_plan(hbmi, oracle, n):
     rng = np.random.default_rng(17)
     P[:16, 3] = 1.0 + rng.random(16) * 4.0          # e in (1, 5]
     P[16, 3] = np.nextafter(1.0, 2.0)               # the first e with 1 - e^2 < 0
-    P[17, 3] = 1.0                                  # sqrt(0): the light curve is computed
+    P[17, 3] = 1.0                                  # 1 - e^2 = 0: NaN like the reference's 0/0 beta
     P[18:24, 3] = -1.0 - rng.random(6) * 2.0        # e < -1: Roche or NaN
     P[24, 3] = -1.0                                 # 1 - e^2 = 0: the reference's beta is 0 / 0
     with HBLikelihood(t, f, s) as L:
