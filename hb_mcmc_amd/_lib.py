@@ -105,11 +105,13 @@ def _declare(lib):
     lib.partition.argtypes = [_PD, _I, _I]
     lib.set_limits.argtypes = [_VP, _VP, _VP, _D]
     lib.initialize_proposals.argtypes = [_PD, _VP]
-    # internal: drop-in bookkeeping (hb_dropin.hpp) -- stats, memo switch, hash test hook
-    lib.hbx_dropin_stats.restype = _I
-    lib.hbx_dropin_stats.argtypes = [_PD, _I]
-    lib.hbx_dropin_set_memo.argtypes = [_I]
-    lib.hbx_dropin_test_hash.argtypes = [_I]
+    # internal (tests, bench): drop-in bookkeeping (hb_dropin.hpp) and the
+    # Kepler probe; absent from older builds loaded as A/B variants (HBMI_LIB)
+    for name, res, args in (("hbx_dropin_stats", _I, [_PD, _I]), ("hbx_dropin_set_memo", _I, [_I]),
+                            ("hbx_dropin_test_hash", _I, [_I]), ("hbx_kepler_probe", _I, [_PD, _L, _D, _I, _PD])):
+        if hasattr(lib, name):
+            f = getattr(lib, name)
+            f.restype, f.argtypes = res, args
     return lib
 
 

@@ -505,6 +505,8 @@ struct hb_catalog {
   int* d_wt = nullptr;           // target of each walker
   int* d_list = nullptr;         // walkers grouped by size class
   hbk::CatSegs segs{};                   // the eval launch's grid segments (catalog_layout)
+  hbk::CatJob* d_jobs = nullptr;         // the eval launch's per-wave jobs (2 per workgroup)
+  size_t jobs_cap = 0;
   WalkerConst* d_wc = nullptr;
   double* d_params = nullptr;    // host-API staging
   double* d_out = nullptr;
@@ -519,7 +521,7 @@ extern "C" void hb_catalog_destroy(hb_catalog* c) {
   (void)hipSetDevice(c->device);
   for (void* p : {(void*)c->d_t, (void*)c->d_f, (void*)c->d_s, (void*)c->d_ph, (void*)c->d_rows, (void*)c->d_cw0,
                   (void*)c->d_tab,
-                  (void*)c->d_wt, (void*)c->d_wf, (void*)c->d_list,
+                  (void*)c->d_wt, (void*)c->d_wf, (void*)c->d_list, (void*)c->d_jobs,
                   (void*)c->d_wc, (void*)c->d_params, (void*)c->d_out, (void*)c->d_dq})
     if (p) (void)hipFree(p);
   delete c;
@@ -702,6 +704,28 @@ static int catalog_layout(hb_catalog* c, const int* walkers, hipStream_t s) {
     ++q;
   }
   c->segs = sg;
+  // per-wave jobs: wave h of workgroup b -> job 2 b + h (a pair: both waves the same walker)
+  std::vector<hbk::CatJob> jobs(2 * (size_t)blocks);
+  for (hbk::CatJob& j : jobs) j = hbk::CatJob{-1, 0, 0, 0, 0, 0, 0};
+  for (int q = 0; q < sg.nseg; ++q)
+    for (int p = 0; p < sg.cnt[q]; ++p) {
+      const int wv = list[(size_t)sg.off[q] + (size_t)p];
+      const hbk::CatJob j{wv, wt[(size_t)wv], p, sg.slab[q], sg.dq[q], sg.lds_per[q], sg.vpt[q] | sg.wpw[q] << 8};
+      if (sg.wpw[q] == 2) {
+        jobs[2 * (size_t)(sg.first[q] + p)] = j;
+        jobs[2 * (size_t)(sg.first[q] + p) + 1] = j;
+      } else {
+        jobs[2 * (size_t)sg.first[q] + (size_t)p] = j;
+      }
+    }
+  if (jobs.size() > c->jobs_cap) {
+    if (c->d_jobs) (void)hipFree(c->d_jobs);
+    c->d_jobs = nullptr;
+    c->jobs_cap = 0;
+    if (hipMalloc(&c->d_jobs, sizeof(hbk::CatJob) * jobs.size()) != hipSuccess)
+      return set_err_msg("hb_catalog: hipMalloc(jobs) failed");
+    c->jobs_cap = jobs.size();
+  }
   if (qb > c->dq_bytes) {
     if (c->d_dq) (void)hipFree(c->d_dq);
     c->d_dq = nullptr;
@@ -734,6 +758,8 @@ static int catalog_layout(hb_catalog* c, const int* walkers, hipStream_t s) {
     HB_TRY(hipMemcpyAsync(c->d_wt, wt.data(), sizeof(int) * (size_t)total, hipMemcpyHostToDevice, s), "upload map");
     HB_TRY(hipMemcpyAsync(c->d_list, list.data(), sizeof(int) * (size_t)total, hipMemcpyHostToDevice, s),
            "upload lists");
+    HB_TRY(hipMemcpyAsync(c->d_jobs, jobs.data(), sizeof(hbk::CatJob) * jobs.size(), hipMemcpyHostToDevice, s),
+           "upload jobs");
     HB_TRY(hipStreamSynchronize(s), "hipStreamSynchronize");  // host vectors go out of scope
   }
   c->layout.assign(walkers, walkers + c->ntargets);
@@ -751,8 +777,8 @@ static int catalog_run(hb_catalog* c, const double* d_params, double* d_logl, hi
   HB_TRY(hbk::launch_prep(d_params, c->total, unused, c->d_wc, s, c->d_tab, c->d_wt, c->d_t, c->ncad, c->d_ph,
                           c->d_cw0, c->d_wf),
          "prep launch");
-  HB_TRY(hbk::launch_eval_catalog(c->segs, c->d_t, c->d_ph, c->d_f, c->d_s, c->d_rows, c->d_tab, c->d_wt, c->d_list,
-                                  c->d_wc, d_logl, c->d_dq, s),
+  HB_TRY(hbk::launch_eval_catalog(c->segs, c->d_jobs, c->d_t, c->d_ph, c->d_f, c->d_s, c->d_rows, c->d_tab, c->d_wc,
+                                  d_logl, c->d_dq, s),
          "eval launch");
   return 0;
 }
@@ -822,71 +848,96 @@ double env_num(const char* name, double dflt) {
 // (hb_dropin.hpp Entry), HBMI_DROPIN_ZC=1 (the batch's rows read and its logL
 // written by the kernels in pinned host memory, no DMA copies),
 // HBMI_DROPIN_POLL=1 (the leader polls the stream instead of
-// hipStreamSynchronize), HBMI_DROPIN_LAT=1 (the multi-wave latency plan).
+// hipStreamSynchronize), HBMI_DROPIN_LAT=1 (the multi-wave latency plan),
+// HBMI_DROPIN_LANES (batches in flight at once, hb_dropin.hpp).
 struct DropPolicy {
   double spin_s, window_s;
   bool zc, poll, lat;
+  int lanes;
 };
 const DropPolicy& drop_policy() {
   static const DropPolicy p{env_num("HBMI_DROPIN_SPIN_US", 0) * 1e-6, env_num("HBMI_DROPIN_WINDOW_US", 0) * 1e-6,
                             env_num("HBMI_DROPIN_ZC", 0) != 0, env_num("HBMI_DROPIN_POLL", 0) != 0,
-                            env_num("HBMI_DROPIN_LAT", 0) != 0};
+                            env_num("HBMI_DROPIN_LAT", 0) != 0, (int)env_num("HBMI_DROPIN_LANES", 1)};
   return p;
 }
 
-struct DropCtx {
+struct DropLane {
   hb_ctx* c = nullptr;
   hipStream_t s = nullptr;
-  double* h_params = nullptr;  // pinned, hcap x 21
-  double* h_out = nullptr;     // pinned, hcap
+  double* h_params = nullptr;   // pinned, hcap x 21
+  double* h_out = nullptr;      // pinned, hcap
   double* dv_params = nullptr;  // their device addresses (zero-copy mode)
   double* dv_out = nullptr;
   int hcap = 0;
 };
+// One drop-in light curve: `nlanes` identical contexts, each with its own
+// stream and pinned staging, so that several combined batches can be in
+// flight at once (hb_dropin.hpp Entry::lanes).  Every lane holds the same
+// arrays and runs the same kernels: a walker's logL does not depend on the
+// lane (or batch) that evaluates it.
+struct DropCtx {
+  DropLane lane[hbdrop::kMaxLanes];
+  int nlanes = 0;
+  hb_ctx* c = nullptr;  // lane 0's context (calc_light_curve, write_lc_to_file)
+};
 
 void dropctx_destroy(DropCtx* d) {
   if (!d) return;
-  if (d->c) (void)hipSetDevice(d->c->device);
-  if (d->h_params) (void)hipHostFree(d->h_params);
-  if (d->h_out) (void)hipHostFree(d->h_out);
-  if (d->s) (void)hipStreamDestroy(d->s);
-  hb_destroy(d->c);
+  for (int k = 0; k < d->nlanes; ++k) {
+    DropLane& l = d->lane[k];
+    if (l.c) (void)hipSetDevice(l.c->device);
+    if (l.h_params) (void)hipHostFree(l.h_params);
+    if (l.h_out) (void)hipHostFree(l.h_out);
+    if (l.s) (void)hipStreamDestroy(l.s);
+    hb_destroy(l.c);
+  }
   delete d;
 }
 
 DropCtx* dropctx_create(const double* t, const double* f, const double* s, long n, const double* mag,
                         const double* err) {
   std::unique_ptr<DropCtx> d(new DropCtx);
-  d->c = hb_create(t, f, s, n, mag, err, 0);
-  if (!d->c) return nullptr;
-  if (drop_policy().lat) (void)hb_ctx_set_latency_plan(d->c, 1);
-  if (hipStreamCreateWithFlags(&d->s, hipStreamNonBlocking) != hipSuccess) {
-    set_err_msg("drop-in: hipStreamCreateWithFlags failed");
-    dropctx_destroy(d.release());
-    return nullptr;
+  const int nl = std::max(1, std::min(hbdrop::kMaxLanes, drop_policy().lanes));
+  for (int k = 0; k < nl; ++k) {
+    DropLane& l = d->lane[k];
+    l.c = hb_create(t, f, s, n, mag, err, 0);
+    d->nlanes = k + 1;
+    if (!l.c) {
+      dropctx_destroy(d.release());
+      return nullptr;
+    }
+    if (drop_policy().lat) (void)hb_ctx_set_latency_plan(l.c, 1);
+    if (hipStreamCreateWithFlags(&l.s, hipStreamNonBlocking) != hipSuccess) {
+      set_err_msg("drop-in: hipStreamCreateWithFlags failed");
+      dropctx_destroy(d.release());
+      return nullptr;
+    }
   }
+  d->c = d->lane[0].c;
   return d.release();
 }
 
-// pinned staging for w rows (the combiner writes the batch's rows here)
-double* dropctx_stage(DropCtx* d, int w) {
-  if (w > d->hcap) {
-    const int cap = std::max(w, 2 * d->hcap);
-    if (d->h_params) (void)hipHostFree(d->h_params);
-    if (d->h_out) (void)hipHostFree(d->h_out);
-    d->h_params = d->h_out = nullptr;
-    d->hcap = 0;
+// pinned staging for w rows of lane k (the combiner writes the batch's rows here)
+double* dropctx_stage(DropCtx* d, int k, int w) {
+  DropLane& l = d->lane[k];
+  if (w > l.hcap) {
+    const int cap = std::max(w, 2 * l.hcap);
+    if (l.h_params) (void)hipHostFree(l.h_params);
+    if (l.h_out) (void)hipHostFree(l.h_out);
+    l.h_params = l.h_out = nullptr;
+    l.hcap = 0;
     // coherent (fine-grained): in zero-copy mode the kernels read the rows and
     // write the logL values here directly, nothing may sit in a GPU cache
     const unsigned fl = hipHostMallocMapped | hipHostMallocCoherent;
-    if (hipHostMalloc((void**)&d->h_params, sizeof(double) * 21 * (size_t)cap, fl) != hipSuccess ||
-        hipHostMalloc((void**)&d->h_out, sizeof(double) * (size_t)cap, fl) != hipSuccess ||
-        hipHostGetDevicePointer((void**)&d->dv_params, d->h_params, 0) != hipSuccess ||
-        hipHostGetDevicePointer((void**)&d->dv_out, d->h_out, 0) != hipSuccess)
+    if (hipHostMalloc((void**)&l.h_params, sizeof(double) * 21 * (size_t)cap, fl) != hipSuccess ||
+        hipHostMalloc((void**)&l.h_out, sizeof(double) * (size_t)cap, fl) != hipSuccess ||
+        hipHostGetDevicePointer((void**)&l.dv_params, l.h_params, 0) != hipSuccess ||
+        hipHostGetDevicePointer((void**)&l.dv_out, l.h_out, 0) != hipSuccess)
       hb_fatal("drop-in: hipHostMalloc failed");
-    d->hcap = cap;
+    l.hcap = cap;
   }
-  return d->h_params;
+  return l.h_params;
 }
 
 // Profile mode (HBMI_DROPIN_PROFILE=1): synchronise after the upload and after
@@ -900,11 +951,12 @@ bool dropin_profile() {
   return on;
 }
 
-int dropctx_eval(DropCtx* d, const double* rows, int w, double* out, hbdrop::Times* tm) {
-  hb_ctx* c = d->c;
+int dropctx_eval(DropCtx* d, int k, const double* rows, int w, double* out, hbdrop::Times* tm) {
+  DropLane& l = d->lane[k];
+  hb_ctx* c = l.c;
   const DropPolicy& pol = drop_policy();
   const bool prof = dropin_profile();
-  std::lock_guard<std::mutex> lk(c->mu);  // the context's workspace and staging (calc_light_curve shares them)
+  std::lock_guard<std::mutex> lk(c->mu);  // the context's workspace and staging (calc_light_curve shares lane 0's)
   HB_TRY(hipSetDevice(c->device), "hipSetDevice");
   if (w > c->cap) {
     int rc = hb_reserve(c, w);
@@ -912,31 +964,31 @@ int dropctx_eval(DropCtx* d, const double* rows, int w, double* out, hbdrop::Tim
   }
   int rc = ctx_host_staging(c, w, false);
   if (rc) return rc;
-  if (rows != d->h_params) dropctx_stage(d, w), memcpy(d->h_params, rows, sizeof(double) * 21 * (size_t)w);
+  if (rows != l.h_params) dropctx_stage(d, k, w), memcpy(l.h_params, rows, sizeof(double) * 21 * (size_t)w);
   auto wait = [&]() -> hipError_t {
-    if (!pol.poll) return hipStreamSynchronize(d->s);
+    if (!pol.poll) return hipStreamSynchronize(l.s);
     hipError_t e;
-    while ((e = hipStreamQuery(d->s)) == hipErrorNotReady) hbdrop::Entry<DropCtx>::relax();
+    while ((e = hipStreamQuery(l.s)) == hipErrorNotReady) hbdrop::Entry<DropCtx>::relax();
     return e;
   };
   const double t0 = hbdrop::now_s();
-  const double* dp = pol.zc ? d->dv_params : c->d_params;
-  double* dout = pol.zc ? d->dv_out : c->d_out;
+  const double* dp = pol.zc ? l.dv_params : c->d_params;
+  double* dout = pol.zc ? l.dv_out : c->d_out;
   if (!pol.zc)
-    HB_TRY(hipMemcpyAsync(c->d_params, d->h_params, sizeof(double) * 21 * (size_t)w, hipMemcpyHostToDevice, d->s),
+    HB_TRY(hipMemcpyAsync(c->d_params, l.h_params, sizeof(double) * 21 * (size_t)w, hipMemcpyHostToDevice, l.s),
            "drop-in upload");
   if (prof) HB_TRY(wait(), "hipStreamSynchronize");
   const double t1 = hbdrop::now_s();
-  rc = run_batch(c, dp, w, dout, nullptr, d->s);
+  rc = run_batch(c, dp, w, dout, nullptr, l.s);
   if (rc) return rc;
   if (prof) HB_TRY(wait(), "hipStreamSynchronize");
   const double t2 = hbdrop::now_s();
   if (!pol.zc)
-    HB_TRY(hipMemcpyAsync(d->h_out, c->d_out, sizeof(double) * (size_t)w, hipMemcpyDeviceToHost, d->s),
+    HB_TRY(hipMemcpyAsync(l.h_out, c->d_out, sizeof(double) * (size_t)w, hipMemcpyDeviceToHost, l.s),
            "drop-in download");
   HB_TRY(wait(), "hipStreamSynchronize");
   const double t3 = hbdrop::now_s();
-  memcpy(out, d->h_out, sizeof(double) * (size_t)w);
+  memcpy(out, l.h_out, sizeof(double) * (size_t)w);
   tm->upload = t1 - t0;
   tm->launch = t2 - t1;
   tm->download = t3 - t2;
@@ -954,6 +1006,7 @@ hbdrop::Cache<DropCtx>& dropin_cache() {
                                       [](hbdrop::Entry<DropCtx>& e) {
                                         e.spin_s = drop_policy().spin_s;
                                         e.window_s = drop_policy().window_s;
+                                        e.lanes = e.ctx->nlanes;
                                       });
   }();
   return *c;
@@ -1025,7 +1078,7 @@ void dropin_write_stats() {
 
 double dropin_loglik(hbdrop::Entry<DropCtx>& d, const double* params) {
   static const hbdrop::Eval<DropCtx> eval = dropctx_eval;
-  static const std::function<double*(DropCtx*, int)> stage = dropctx_stage;
+  static const hbdrop::Stage<DropCtx> stage = dropctx_stage;
   double v = 0.0;
   if (d.call(params, &v, eval, stage) != 0) hb_fatal("hb_loglik_batch failed");
   return v;
@@ -1093,6 +1146,27 @@ extern "C" int hbx_dropin_stats(double* out, int n) {
   const int k = std::min(n, 11);
   for (int i = 0; i < k; ++i) out[i] = v[i];
   return k;
+}
+
+// internal (tests): the eval kernels' cold Kepler start + Newton loop on n
+// mean anomalies (hb_kepler_probe_kernel); out = 4 n doubles {E, converged,
+// sin E, cos E}; tab: the walker is on the phase table (series start for
+// |e| <= 0.25)
+extern "C" int hbx_kepler_probe(const double* m, long n, double e, int tab, double* out) {
+  if (n <= 0) return 0;
+  if (!m || !out) return set_err_msg("hbx_kepler_probe: null pointer");
+  runtime_init();
+  if (g_ndev <= 0) return set_err_msg("hbx_kepler_probe: no HIP device");
+  HB_TRY(hipSetDevice(0), "hipSetDevice");
+  double *dm = nullptr, *dout = nullptr;
+  hipError_t er = hipMalloc(&dm, sizeof(double) * (size_t)n);
+  if (er == hipSuccess) er = hipMalloc(&dout, sizeof(double) * 4 * (size_t)n);
+  if (er == hipSuccess) er = hipMemcpy(dm, m, sizeof(double) * (size_t)n, hipMemcpyHostToDevice);
+  if (er == hipSuccess) er = hbk::launch_kepler_probe(dm, n, e, tab, dout, nullptr);
+  if (er == hipSuccess) er = hipMemcpy(out, dout, sizeof(double) * 4 * (size_t)n, hipMemcpyDeviceToHost);
+  if (dm) (void)hipFree(dm);
+  if (dout) (void)hipFree(dout);
+  return er == hipSuccess ? 0 : set_err("hbx_kepler_probe", er);
 }
 
 // internal (tests, A/B): the logL memo on (1) or off (0) for later calls

@@ -172,10 +172,18 @@ inline double now_s() {
   return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
-// Evaluate w parameter rows (w x 21, row-major, in `params`) into out[w];
-// returns 0 or an error code.
+// Evaluate w parameter rows (w x 21, row-major, in `params`) on evaluation
+// lane `lane` into out[w]; returns 0 or an error code.  Lanes are independent
+// (libhbmi: one context and stream each), so batches on different lanes may
+// run at the same time.
 template <class Ctx>
-using Eval = std::function<int(Ctx*, const double* params, int w, double* out, Times* tm)>;
+using Eval = std::function<int(Ctx*, int lane, const double* params, int w, double* out, Times* tm)>;
+// A staging area of w x 21 doubles for lane `lane` that Eval reads in place
+// (pinned memory), or nullptr for the entry's own vector.
+template <class Ctx>
+using Stage = std::function<double*(Ctx*, int lane, int w)>;
+
+constexpr int kMaxLanes = 8;
 
 template <class Ctx>
 struct Entry {
@@ -195,20 +203,23 @@ struct Entry {
   std::condition_variable cv;
   std::vector<Req*> pending;
   std::atomic<int> npending{0};
-  std::atomic<bool> busy{false};
+  std::atomic<int> inflight{0};  // batches being evaluated (at most `lanes`)
+  unsigned lane_busy = 0;        // bit k: lane k holds a batch (under mu)
   Memo memo;
   std::atomic<bool> use_memo{true};
-  std::vector<double> params, out;  // the leader's staging (when Eval stages itself, unused)
+  std::vector<double> params[kMaxLanes], out[kMaxLanes];  // per-lane staging (when Stage gives none)
   Stats st;
   std::atomic<uint64_t> wake_ns{0};
-  // Waiting policy (set by the owner before use):
+  // Policy (set by the owner before use):
+  //  * lanes: batches that may be in flight at once, each on its own lane;
+  //    a caller that finds a free lane leads a batch right away instead of
+  //    waiting for the running one to finish;
   //  * spin_s: a caller whose request rides in another caller's batch polls
   //    its done flag (lock released) this long before it sleeps on the
-  //    condition variable -- a futex wake-up costs tens of us on a loaded host;
+  //    condition variable;
   //  * window_s: a new leader waits up to this long for the queue to reach
-  //    the largest batch of the last kWindowHist batches before it launches,
-  //    so callers that arrive together (the sampler's threads after their
-  //    OpenMP barrier) ride in one batch instead of a train of small ones.
+  //    the largest batch of the last kWindowHist batches before it launches.
+  int lanes = 1;
   double spin_s = 0, window_s = 0;
   static constexpr int kWindowHist = 16;
   int hist[kWindowHist] = {0};
@@ -221,10 +232,7 @@ struct Entry {
   }
 
   // loglikelihood() of one parameter vector: memo, else combined evaluation.
-  // `stage(w)` may hand the leader a staging area of w x 21 doubles that Eval
-  // reads in place (pinned memory); nullptr: the entry's own vector.
-  int call(const double* p, double* result, const Eval<Ctx>& eval,
-           const std::function<double*(Ctx*, int)>& stage = nullptr) {
+  int call(const double* p, double* result, const Eval<Ctx>& eval, const Stage<Ctx>& stage = nullptr) {
     std::unique_lock<std::mutex> lk(mu);
     ++st.calls;
     if (use_memo && memo.find(p, result)) {
@@ -235,6 +243,7 @@ struct Entry {
     r.p = p;
     pending.push_back(&r);
     npending.store((int)pending.size(), std::memory_order_release);
+    const int nl = lanes < 1 ? 1 : lanes > kMaxLanes ? kMaxLanes : lanes;
     bool spun = false;
     for (;;) {
       if (r.done.load(std::memory_order_acquire)) {
@@ -242,8 +251,11 @@ struct Entry {
         *result = r.out;
         return r.rc;
       }
-      if (!busy.load(std::memory_order_relaxed)) {  // lead: every queued request (this one included)
-        busy.store(true, std::memory_order_relaxed);
+      if (inflight.load(std::memory_order_relaxed) < nl && !pending.empty()) {  // lead a batch on a free lane
+        int lane = 0;
+        while (lane_busy >> lane & 1u) ++lane;
+        lane_busy |= 1u << lane;
+        inflight.fetch_add(1, std::memory_order_relaxed);
         int target = 0;
         for (int i = 0; i < nhist; ++i) target = hist[i] > target ? hist[i] : target;
         if (window_s > 0 && (int)pending.size() < target) {
@@ -261,21 +273,21 @@ struct Entry {
         lk.unlock();
         const double t0 = now_s();
         const int w = (int)batch.size();
-        double* rows = stage ? stage(ctx, w) : nullptr;
+        double* rows = stage ? stage(ctx, lane, w) : nullptr;
         if (!rows) {
-          params.resize((size_t)w * kNPars);
-          rows = params.data();
+          params[lane].resize((size_t)w * kNPars);
+          rows = params[lane].data();
         }
-        out.resize((size_t)w);
+        out[lane].resize((size_t)w);
         for (int i = 0; i < w; ++i) memcpy(rows + (size_t)i * kNPars, batch[(size_t)i]->p, kNPars * sizeof(double));
         const double t1 = now_s();
         Times tm;
-        const int rc = eval(ctx, rows, w, out.data(), &tm);
+        const int rc = eval(ctx, lane, rows, w, out[lane].data(), &tm);
         lk.lock();
         const double t2 = now_s();
         for (int i = 0; i < w; ++i) {
           Req* q = batch[(size_t)i];
-          q->out = out[(size_t)i];
+          q->out = out[lane][(size_t)i];
           q->rc = rc;
           q->t_done = t2;
           if (rc == 0 && use_memo) memo.put(q->p, q->out);
@@ -289,15 +301,17 @@ struct Entry {
         st.s_upload += tm.upload;
         st.s_launch += tm.launch;
         st.s_download += tm.download;
-        busy.store(false, std::memory_order_relaxed);
+        lane_busy &= ~(1u << lane);
+        inflight.fetch_sub(1, std::memory_order_relaxed);
         cv.notify_all();
-        continue;  // own request done: returns above
+        continue;  // own request done (it was in the batch): returns above
       }
       if (spin_s > 0 && !spun) {  // poll first, sleep after
         spun = true;
         lk.unlock();
         const double t_end = now_s() + spin_s;
-        for (int k = 1; !r.done.load(std::memory_order_acquire) && busy.load(std::memory_order_relaxed); ++k) {
+        for (int k = 1; !r.done.load(std::memory_order_acquire) && inflight.load(std::memory_order_relaxed) >= nl;
+             ++k) {
           if ((k & 63) == 0) {
             if (now_s() > t_end) break;
             std::this_thread::yield();

@@ -114,10 +114,24 @@ struct CatSegs {
   int lds_per[kCatSegs];  // LDS bytes per walker (a wave's slice, or the pair's)
   long long dq[kCatSegs]; // byte offset of the segment's deferred queues in the dq buffer
 };
-hipError_t launch_eval_catalog(const CatSegs& sg, const double* t, const double2* ph, const double* f,
-                               const double* isg, const double* rows, const TargetDesc* tab, const int* wt,
-                               const int* list, const hbdev::WalkerConst* wc, double* logl, unsigned char* dq,
-                               hipStream_t s);
+// One wave's work in the catalog eval launch, built by catalog_layout from
+// CatSegs: wave h of workgroup b reads job 2 b + h (a pair's two waves read
+// the same walker).  Everything the wave needs besides its target's
+// TargetDesc and its walker's record, in one 32-B row read by scalar loads --
+// no segment search and no runtime-indexed kernel-argument arrays.
+struct alignas(32) CatJob {
+  int wv;         // walker (logL index); -1: nothing to do (the last one-wave workgroup's second wave)
+  int tgt;        // its target (TargetDesc row)
+  int pos;        // its position in the segment (deferred-queue region)
+  int slab;       // slab bytes per walker
+  long long dq;   // byte offset of the segment's deferred queues in the dq buffer
+  int lds_per;    // LDS bytes per walker
+  int geo;        // VPT | WPW << 8
+};
+static_assert(sizeof(CatJob) == 32, "CatJob layout");
+hipError_t launch_eval_catalog(const CatSegs& sg, const CatJob* jobs, const double* t, const double2* ph,
+                               const double* f, const double* isg, const double* rows, const TargetDesc* tab,
+                               const hbdev::WalkerConst* wc, double* logl, unsigned char* dq, hipStream_t s);
 // The fused launch: per-walker records (hb_prep.hpp) in the prologue of the
 // one-wave eval kernel, WPB walkers per workgroup (hb_kernels.hip
 // launch_eval_fused); the records and the shared-period phase table are also
@@ -154,6 +168,7 @@ hipError_t launch_eval(const EvalPlan& pl, const double* t, const double2* ph, c
 hipError_t launch_traj(const double* d_times, int nt, const TrajArgs& ta, double* d, double* z1,
                        double* z2, double* rr, double* ff, hipStream_t s);
 hipError_t launch_probe(int op, const double* d_in, double* d_out, hipStream_t s);
+hipError_t launch_kepler_probe(const double* d_m, long n, double e, int tab, double* d_out, hipStream_t s);
 hipError_t launch_partition(double* d_a, int lo, int hi, int* d_res, hipStream_t s);
 hipError_t launch_median(double* d_a, long n, long kth, hipStream_t s);
 // ascending sort of d_in[0..n) into d_out (bitonic over order-preserving keys;

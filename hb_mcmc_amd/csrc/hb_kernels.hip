@@ -646,35 +646,37 @@ __device__ __forceinline__ void cat_walker(const double* __restrict__ t, const d
   eval_wave_body<VPT, false, WPW>(t + td.off, ph + td.off, f + td.off, isg + td.off, rows + td.roff, td.n, td.kth, w,
                                   wv, pos, logl, nullptr, 0, slab, slab, td.gap, hbds::AccArgs{}, smem, dq);
 }
+// Each wave reads its CatJob row (catalog_layout), its target's TargetDesc and
+// its walker's record through constant-address-space pointers: scalar loads
+// at the use, nothing indexed at run time in the kernel arguments (the round-5
+// CatSegs argument, indexed by the segment, held 262 SGPR spills).
 __global__ __launch_bounds__(128) HB_WPE_ATTR void hb_eval_catalog_kernel(
-    const double* __restrict__ t, const double2* __restrict__ ph, const double* __restrict__ f,
-    const double* __restrict__ isg, const double* __restrict__ rows, const TargetDesc* __restrict__ tab,
-    const int* __restrict__ wt, const int* __restrict__ list, const WalkerConst* __restrict__ wcs,
-    double* __restrict__ logl, unsigned char* __restrict__ dqb, CatSegs sg) {
+    const CatJob* __restrict__ jobs, const double* __restrict__ t, const double2* __restrict__ ph,
+    const double* __restrict__ f, const double* __restrict__ isg, const double* __restrict__ rows,
+    const TargetDesc* __restrict__ tab, const WalkerConst* __restrict__ wcs, double* __restrict__ logl,
+    unsigned char* __restrict__ dqb) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_all[];
-  const int b = (int)blockIdx.x;
-  int s = 0;
-#pragma unroll
-  for (int q = 1; q < kCatSegs; ++q) s += (q < sg.nseg && b >= sg.first[q]) ? 1 : 0;
+  typedef const __attribute__((address_space(4))) CatJob cjob_t;
+  typedef const __attribute__((address_space(4))) TargetDesc ctd_t;
+  typedef const __attribute__((address_space(4))) WalkerConst cwc_t;
   const int h = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-  const int wpw = sg.wpw[s];
-  const int pos = wpw == 2 ? b - sg.first[s] : 2 * (b - sg.first[s]) + h;
-  if (pos >= sg.cnt[s]) return;  // the last one-wave workgroup's second wave (a pair: both waves)
-  const int wv = list[sg.off[s] + pos];
-  const TargetDesc& td = tab[wt[wv]];
-  unsigned char* smem = smem_all + (wpw == 2 ? 0 : h * sg.lds_per[s]);
-  double* dq = reinterpret_cast<double*>(dqb + sg.dq[s]);
-  const int slab = sg.slab[s];
-  if (wpw == 2) {
-    cat_walker<16, 2>(t, ph, f, isg, rows, td, wcs[wv], wv, pos, logl, slab, smem, dq);
-    return;
-  }
-  switch (sg.vpt[s]) {
-    case 16: cat_walker<16, 1>(t, ph, f, isg, rows, td, wcs[wv], wv, pos, logl, slab, smem, dq); break;
-    case 8: cat_walker<8, 1>(t, ph, f, isg, rows, td, wcs[wv], wv, pos, logl, slab, smem, dq); break;
-    case 4: cat_walker<4, 1>(t, ph, f, isg, rows, td, wcs[wv], wv, pos, logl, slab, smem, dq); break;
-    case 2: cat_walker<2, 1>(t, ph, f, isg, rows, td, wcs[wv], wv, pos, logl, slab, smem, dq); break;
-    default: cat_walker<1, 1>(t, ph, f, isg, rows, td, wcs[wv], wv, pos, logl, slab, smem, dq); break;
+  const CatJob* jb = (const CatJob*)(cjob_t*)jobs;
+  const CatJob& j = jb[2 * (int)blockIdx.x + h];
+  const int wv = j.wv;
+  if (wv < 0) return;
+  const TargetDesc& td = ((const TargetDesc*)(ctd_t*)tab)[j.tgt];
+  const WalkerConst& w = ((const WalkerConst*)(cwc_t*)wcs)[wv];
+  const int geo = j.geo;
+  unsigned char* smem = smem_all + ((geo >> 8) == 2 ? 0 : h * j.lds_per);
+  double* dq = reinterpret_cast<double*>(dqb + j.dq);
+  const int slab = j.slab, pos = j.pos;
+  switch (geo) {
+    case 16 | 2 << 8: cat_walker<16, 2>(t, ph, f, isg, rows, td, w, wv, pos, logl, slab, smem, dq); break;
+    case 16 | 1 << 8: cat_walker<16, 1>(t, ph, f, isg, rows, td, w, wv, pos, logl, slab, smem, dq); break;
+    case 8 | 1 << 8: cat_walker<8, 1>(t, ph, f, isg, rows, td, w, wv, pos, logl, slab, smem, dq); break;
+    case 4 | 1 << 8: cat_walker<4, 1>(t, ph, f, isg, rows, td, w, wv, pos, logl, slab, smem, dq); break;
+    case 2 | 1 << 8: cat_walker<2, 1>(t, ph, f, isg, rows, td, w, wv, pos, logl, slab, smem, dq); break;
+    default: cat_walker<1, 1>(t, ph, f, isg, rows, td, w, wv, pos, logl, slab, smem, dq); break;
   }
 }
 
@@ -872,6 +874,42 @@ __global__ void hb_traj_kernel(const double* __restrict__ times, int nt, TrajArg
   const double zz = o.rR * o.su * ta.w.si;
   z1[i] = zz * ta.fz1;
   z2[i] = -zz * ta.fz2;
+}
+
+// Kepler probe (tests/test_gpu_parity.py::test_kepler_cold_start_against_
+// reference_root): the cold path's start and Newton loop exactly as the eval
+// kernels run them -- cold_start_k (the fifth-order series start when the
+// walker is on the phase table and |e| <= kSeriesEmax, else the reference's
+// E0 = M + 0.85 e sign(sin M), likelihood3.c:155-157) then newton_k with its
+// stopping rule -- one lane per mean anomaly M in (-2pi, 2pi) \ {0} (what
+// mean_anomaly_k hands over), the table entry (sin, cos)(M) as the prep kernel
+// writes it (psi = 0).  out[4 i ..] = {E, converged, sin E, cos E}.
+__global__ void hb_kepler_probe_kernel(const double* __restrict__ M, long n, double e, int tab,
+                                       double* __restrict__ out) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool act = i < n;
+  WalkerConst w = {};
+  w.e = e;
+  w.e085 = 0.85 * e;
+  w.cpsi = 1.0;
+  w.spsi = 0.0;
+  sincos_table(0.85 * e, w.sdel, w.cdel);
+  w.mA = 1.0;
+  double m[1] = {act ? M[i] : 1.0};
+  const double t[1] = {m[0] / kDay};  // read only on lanes flagged exact: none here
+  const bool plus[1] = {(fabs(m[0]) <= kPi) != (m[0] < 0.0)};
+  double2 ph[1];
+  sincos_table(m[0], ph[0].x, ph[0].y);
+  double E[1], sv[1], cv[1], yk[1];
+  bool ok = true;
+  cold_start_k<1>(t, ph, tab != 0, false, w, m, plus, E, sv, cv, ok);
+  const bool conv = newton_k<1>(e, m, E, sv, cv, yk, ok);
+  if (act) {
+    out[4 * i] = E[0];
+    out[4 * i + 1] = conv ? 1.0 : 0.0;
+    out[4 * i + 2] = sv[0];
+    out[4 * i + 3] = cv[0];
+  }
 }
 
 // scalar entry points, evaluated by one device lane
@@ -1214,10 +1252,9 @@ static hipError_t launch_wave_acc_t(const EvalPlan& pl, const double* t, const d
                                   pl.gap, acc, dq);
 }
 
-hipError_t launch_eval_catalog(const CatSegs& sg, const double* t, const double2* ph, const double* f,
-                               const double* isg, const double* rows, const TargetDesc* tab, const int* wt,
-                               const int* list, const WalkerConst* wc, double* logl, unsigned char* dq,
-                               hipStream_t s) {
+hipError_t launch_eval_catalog(const CatSegs& sg, const CatJob* jobs, const double* t, const double2* ph,
+                               const double* f, const double* isg, const double* rows, const TargetDesc* tab,
+                               const WalkerConst* wc, double* logl, unsigned char* dq, hipStream_t s) {
   if (sg.nseg <= 0 || sg.nseg > kCatSegs) return sg.nseg == 0 ? hipSuccess : hipErrorInvalidValue;
   size_t lds = 0;
   for (int q = 0; q < sg.nseg; ++q) {
@@ -1239,8 +1276,8 @@ hipError_t launch_eval_catalog(const CatSegs& sg, const double* t, const double2
     if (e != hipSuccess) return e;
     attr_set = true;
   }
-  hipLaunchKernelGGL(hb_eval_catalog_kernel, dim3(sg.first[sg.nseg]), dim3(128), lds, s, t, ph, f, isg, rows, tab, wt,
-                     list, wc, logl, dq, sg);
+  hipLaunchKernelGGL(hb_eval_catalog_kernel, dim3(sg.first[sg.nseg]), dim3(128), lds, s, jobs, t, ph, f, isg, rows,
+                     tab, wc, logl, dq);
   return hipGetLastError();
 }
 
@@ -1301,6 +1338,12 @@ hipError_t launch_traj(const double* d_times, int nt, const TrajArgs& ta, double
   if (nt <= 0) return hipSuccess;
   hipLaunchKernelGGL(hb_traj_kernel, dim3((nt + 255) / 256), dim3(256), 0, s, d_times, nt, ta, d, z1, z2,
                      rr, ff);
+  return hipGetLastError();
+}
+
+hipError_t launch_kepler_probe(const double* d_m, long n, double e, int tab, double* d_out, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(hb_kepler_probe_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, d_m, n, e, tab, d_out);
   return hipGetLastError();
 }
 

@@ -151,6 +151,21 @@ void orc_orbit(const double *tt, const double *op, double *sep_sky,
     }
 }
 
+/* The Kepler solve of orc_orbit alone, from the mean anomaly: start      */
+/* M + 0.85 e sign(sin M), five Newton steps (likelihood3.c:152-160).     */
+void orc_kepler(const double *mean, long n, double ecc, double *out)
+{
+    for (long k = 0; k < n; ++k) {
+        double mean_an = mean[k];
+        double ecc_an = mean_an;
+        double sm = sin(mean_an);
+        if (sm != 0.0) ecc_an = mean_an + 0.85 * ecc * sm / fabs(sm);
+        for (int it = 0; it < 5; ++it)
+            ecc_an = ecc_an - (ecc_an - ecc * sin(ecc_an) - mean_an) / (1 - ecc * cos(ecc_an));
+        out[k] = ecc_an;
+    }
+}
+
 /* ------------------------------------------------------------------ */
 /* Doppler beaming coefficient table, Claret et al. 2020 (l3.c:194-209)  */
 /* ------------------------------------------------------------------ */

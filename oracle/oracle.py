@@ -203,6 +203,16 @@ class Oracle(_Base):
         L.orc_light_curve_batch.argtypes = [_PD, _L, _PD, _L, _PD, _I]
         L.orc_median_value.restype = _D
         L.orc_median_value.argtypes = [_PD, _L]
+        L.orc_kepler.argtypes = [_PD, _L, _D, _PD]
+
+    def kepler(self, mean, ecc):
+        """The reference's Kepler solve from the mean anomaly (likelihood3.c:
+        152-160: start M + 0.85 e sign(sin M), five Newton steps) -- the
+        same lines as orc_orbit, which the traj goldens pin."""
+        mean = np.ascontiguousarray(mean, dtype=np.float64)
+        out = np.empty(len(mean))
+        self.lib.orc_kepler(_ptr(mean), len(mean), float(ecc), _ptr(out))
+        return out
 
     def loglike_batch(self, t, f, s, P, mag, magerr, nthreads=0):
         t = np.ascontiguousarray(t, dtype=np.float64)

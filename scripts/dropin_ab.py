@@ -16,14 +16,14 @@ import bench  # noqa: E402
 VARIANTS = {
     "base": {},
     "memo_off": {"HBMI_DROPIN_MEMO": "0"},
-    "spin": {"HBMI_DROPIN_SPIN_US": "300"},
+    "lanes2": {"HBMI_DROPIN_LANES": "2"},
+    "lanes4": {"HBMI_DROPIN_LANES": "4"},
+    "lanes4_spin": {"HBMI_DROPIN_LANES": "4", "HBMI_DROPIN_SPIN_US": "200"},
+    "lanes4_zc": {"HBMI_DROPIN_LANES": "4", "HBMI_DROPIN_ZC": "1"},
+    "lanes8": {"HBMI_DROPIN_LANES": "8"},
+    "lanes4_lat": {"HBMI_DROPIN_LANES": "4", "HBMI_DROPIN_LAT": "1"},
+    "lanes4_omp_passive": {"HBMI_DROPIN_LANES": "4", "OMP_WAIT_POLICY": "passive"},
     "spin_win": {"HBMI_DROPIN_SPIN_US": "300", "HBMI_DROPIN_WINDOW_US": "30"},
-    "spin_win_poll": {"HBMI_DROPIN_SPIN_US": "300", "HBMI_DROPIN_WINDOW_US": "30", "HBMI_DROPIN_POLL": "1"},
-    "spin_win_zc": {"HBMI_DROPIN_SPIN_US": "300", "HBMI_DROPIN_WINDOW_US": "30", "HBMI_DROPIN_ZC": "1"},
-    "spin_win_zc_poll": {"HBMI_DROPIN_SPIN_US": "300", "HBMI_DROPIN_WINDOW_US": "30", "HBMI_DROPIN_ZC": "1",
-                         "HBMI_DROPIN_POLL": "1"},
-    "all_lat": {"HBMI_DROPIN_SPIN_US": "300", "HBMI_DROPIN_WINDOW_US": "30", "HBMI_DROPIN_ZC": "1",
-                "HBMI_DROPIN_POLL": "1", "HBMI_DROPIN_LAT": "1"},
 }
 
 

@@ -40,11 +40,18 @@ static double model(const Fake* c, const double* p) {
 
 static int g_eval_us = 0;  // a GPU round trip's duration (section 4)
 
-static int eval(Fake* c, const double* rows, int w, double* out, Times* tm) {
+static std::atomic<int> g_conc{0}, g_conc_max{0};
+
+static int eval(Fake* c, int lane, const double* rows, int w, double* out, Times* tm) {
+  const int k = ++g_conc;
+  for (int m = g_conc_max; k > m && !g_conc_max.compare_exchange_weak(m, k);) {
+  }
+  if (lane < 0 || lane >= kMaxLanes) abort();
   if (g_eval_us) std::this_thread::sleep_for(std::chrono::microseconds(g_eval_us));
   for (int i = 0; i < w; ++i) out[i] = model(c, rows + (size_t)i * kNPars);
   c->evals += w;
   ++g_batches;
+  --g_conc;
   tm->upload = tm->launch = tm->download = 0;
   return 0;
 }
@@ -138,12 +145,15 @@ int main() {
   //    with the waiters sleeping at once, and with the spin / batch-window
   //    policy libhbmi can switch on
   g_eval_us = 20;
-  for (int pol = 0; pol < 3; ++pol) {
+  for (int pol = 0; pol < 5; ++pol) {
     std::vector<double> fp(f2);
     fp[0] += 1e-6 * (pol + 1);  // a fresh context per policy
     auto e = cache.get(t.data(), fp.data(), s.data(), n, mag, err);
     e->spin_s = pol >= 1 ? 200e-6 : 0.0;
     e->window_s = pol == 2 ? 30e-6 : 0.0;
+    e->lanes = pol >= 3 ? 4 : 1;  // policy 3: four lanes with spinning, 4: four lanes, sleeping waiters
+    if (pol == 4) e->spin_s = 0.0;
+    g_conc_max = 0;
     const int nth = 25, iters = 40;
     const int ev0 = e->ctx->evals;
     g_batches = 0;
@@ -174,8 +184,10 @@ int main() {
     CHECK(evals >= nth + nth * iters && evals <= nth + nth * iters + nth * iters / 10);
     CHECK(g_batches < evals);
     CHECK(e->st.calls == (uint64_t)(2 * nth * iters) && e->st.walkers == (uint64_t)evals);
-    printf("policy %d: %d evaluations in %d batches\n", pol, evals, (int)g_batches);
-    CHECK(e->npending.load() == 0 && !e->busy.load() && e->pending.empty());
+    CHECK(g_conc_max <= e->lanes && (e->lanes == 1 || g_conc_max > 1));
+    printf("policy %d: %d evaluations in %d batches, up to %d at once\n", pol, evals, (int)g_batches,
+           (int)g_conc_max);
+    CHECK(e->npending.load() == 0 && e->inflight.load() == 0 && e->lane_busy == 0 && e->pending.empty());
   }
   printf("ok\n");
   return 0;
