@@ -325,7 +325,24 @@ def sampler_e2e_sharded(L, w, iters, rank, world, warm=20):
                                     "exchange_bytes_per_rank_per_iter": 8.0 * exch / (warm + iters)}}
 
 
-def prior_spread(L, n, w, steps, stream, dev, timer, ks=50):
+def computed_prior_walkers(L, w, seed, dev, stream):
+    """w walkers from the set_limits box (synth.prior_walkers) conditioned on a
+    light curve being computed: no Roche overflow and |e| < 1 (logL neither
+    the -5e14 sentinel nor NaN), i.e. the prior-box walkers whose cost is the
+    model itself (mcmc_wrapper2.c:236-252; likelihood3.c:866-869).  The filter
+    is one untimed evaluation of the candidates."""
+    keep, k = [], 0
+    while sum(len(x) for x in keep) < w:
+        cand = synth.prior_walkers(4 * w, seed=seed + 7919 * k)
+        out = torch.empty(len(cand), dtype=torch.float64, device=dev)
+        L.loglike_dev(torch.from_numpy(cand).to(dev), out, stream)
+        lv = out.cpu().numpy()
+        keep.append(cand[np.isfinite(lv) & (lv != -5e14) & (np.abs(cand[:, 3]) < 1.0)])
+        k += 1
+    return np.ascontiguousarray(np.concatenate(keep)[:w])
+
+
+def prior_spread(L, n, w, steps, stream, dev, timer, ks=50, computed=False):
     """The headline shape (one hb_loglik_batch_dev of w walkers over n
     cadences per step) on walkers drawn from the set_limits box like the
     reference's random initial state (mcmc_wrapper2.c:236-252, synth.
@@ -334,7 +351,11 @@ def prior_spread(L, n, w, steps, stream, dev, timer, ks=50):
     (every one on the warm Kepler chains).  Reported beside the headline, not
     as `value`."""
     nb = 4
-    Ph = [synth.prior_walkers(w, seed=3000 + k) for k in range(nb)]
+    if computed:
+        L.reserve(4 * w)
+        Ph = [computed_prior_walkers(L, w, 5000 + 131 * k, dev, stream) for k in range(nb)]
+    else:
+        Ph = [synth.prior_walkers(w, seed=3000 + k) for k in range(nb)]
     P = [torch.from_numpy(x).to(dev) for x in Ph]
     out = torch.empty(w, dtype=torch.float64, device=dev)
     for k in range(10):
@@ -359,9 +380,12 @@ def prior_spread(L, n, w, steps, stream, dev, timer, ks=50):
             "ms_per_step": wall / steps * 1e3, "kernel_ms": kms, "kernel_event_samples": ks,
             "last_batch": {"roche_frac": float(roche.mean()),
                            "e_gt_0p8_not_roche_frac": float(((x[:, 3] > 0.8) & ~roche).mean()),
+                           "e_gt_0p84_cold_path_frac": float(((x[:, 3] > 0.84) & ~roche).mean()),
                            "nonfinite": int((~np.isfinite(lv)).sum())},
             "walkers_from": "synth.prior_walkers: uniform over the set_limits box (mcmc_wrapper2.c:236-252), "
-                            "log P fixed, T0 folded"}
+                            "log P fixed, T0 folded" + (
+                                "; conditioned on a computed light curve (no Roche overflow, |e| < 1: "
+                                "bench.computed_prior_walkers)" if computed else "")}
 
 
 DROPIN_LEGS = (("dropin", "hb_mcmc_ref_hbmi", {}),
@@ -776,6 +800,8 @@ def main():
                                        "what": "last timed step's gathered logL equals each rank's own, on every rank"}
         if world == 1 and a.prior_steps > 0 and n <= 2048:
             line["c2_prior_spread"] = prior_spread(L, n, w, a.prior_steps, stream, dev, a.timer)
+            line["c2_prior_spread_computed"] = prior_spread(L, n, w, a.prior_steps, stream, dev, a.timer,
+                                                            computed=True)
         if world == 1 and a.sampler_iters > 0:
             line["sampler_end_to_end"] = sampler_e2e(L, w, a.sampler_iters)
         if world > 1 and e2e is not None:

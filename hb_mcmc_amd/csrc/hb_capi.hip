@@ -175,6 +175,11 @@ struct hb_ctx {
   double* d_s = nullptr;          // 1 / max(sigma, 1e-5)
   double2* d_ph = nullptr;        // shared-period phase table, written by every prep launch
   double* d_tab_pc = nullptr;     // its period [s] (NaN: none yet); one word behind the table
+  // fused launches' table words (d_tab_pc[1 + (k & 1)]: the period launch k
+  // found or wrote; hbk::PreArgs::tab_prev / tab_mark); tab_chain false after
+  // any other launch that writes the table (hb_prep_kernel)
+  unsigned tab_seq = 0;
+  bool tab_chain = false;
   double* d_rows = nullptr;       // t, f, 1/sigma in lane-row order (hbk::build_rows; one-wave path)
   // per-walker workspace
   int cap = 0;
@@ -279,17 +284,17 @@ extern "C" hb_ctx* hb_create(const double* t, const double* f, const double* sig
   }
   const size_t bytes = sizeof(double) * (size_t)n;
   if (hipMalloc(&c->d_t, bytes) != hipSuccess || hipMalloc(&c->d_f, bytes) != hipSuccess ||
-      hipMalloc(&c->d_s, bytes) != hipSuccess || hipMalloc(&c->d_ph, 2 * bytes + 16) != hipSuccess) {
+      hipMalloc(&c->d_s, bytes) != hipSuccess || hipMalloc(&c->d_ph, 2 * bytes + 32) != hipSuccess) {
     set_err_msg("hb_create: hipMalloc failed");
     hb_destroy(c.release());
     return nullptr;
   }
   c->d_tab_pc = reinterpret_cast<double*>(c->d_ph + n);
-  const double no_tab = __builtin_nan("");
+  const double no_tab[3] = {__builtin_nan(""), __builtin_nan(""), __builtin_nan("")};
   if (hipMemcpy(c->d_t, t, bytes, hipMemcpyHostToDevice) != hipSuccess ||
       hipMemcpy(c->d_f, f, bytes, hipMemcpyHostToDevice) != hipSuccess ||
       hipMemcpy(c->d_s, s.data(), bytes, hipMemcpyHostToDevice) != hipSuccess ||
-      hipMemcpy(c->d_tab_pc, &no_tab, sizeof(double), hipMemcpyHostToDevice) != hipSuccess) {
+      hipMemcpy(c->d_tab_pc, no_tab, sizeof no_tab, hipMemcpyHostToDevice) != hipSuccess) {
     set_err_msg("hb_create: upload failed");
     hb_destroy(c.release());
     return nullptr;
@@ -354,15 +359,21 @@ static int run_batch(hb_ctx* c, const double* d_params, int w, double* d_logl, d
   // the eval kernel's prologue (hbk::launch_eval_fused)
   const int fw = (prep && acc == nullptr && d_tmpl == nullptr && &pl == &c->plan) ? hbk::fused_wpb(pl, w, c->cus) : 0;
   if (fw > 0) {
-    const hbk::PreArgs pa{d_params, c->mags, c->d_wc, c->d_ph, c->d_tab_pc};
+    const hbk::PreArgs pa{d_params, c->mags, c->d_wc, c->d_ph, c->d_tab_pc,
+                          c->tab_chain ? c->d_tab_pc + 1 + ((c->tab_seq + 1) & 1) : nullptr,
+                          c->d_tab_pc + 1 + (c->tab_seq & 1)};
     HB_TRY(hbk::launch_eval_fused(pl, fw, pa, c->d_t, c->d_f, c->d_s, c->d_rows, w, d_logl, s, c->d_dq),
            "hb_eval_wave_kernel (fused)");
+    c->tab_chain = true;
+    ++c->tab_seq;
     return 0;
   }
-  if (prep)
+  if (prep) {
     HB_TRY(hbk::launch_prep(d_params, w, c->mags, c->d_wc, s, nullptr, nullptr, c->d_t, c->plan.n, c->d_ph, nullptr,
                             0, c->d_tab_pc),
            "hb_prep_kernel");
+    c->tab_chain = false;  // the table may hold another period now
+  }
   HB_TRY(hbk::launch_eval(pl, c->d_t, c->d_ph, c->d_f, c->d_s, c->d_rows, c->d_wc, w, d_logl, d_tmpl, c->d_scratch,
                           d_tmpl ? 1 : 0, s, acc, c->d_dq),
          "hb_eval_kernel");
@@ -408,6 +419,7 @@ extern "C" int hb_prepare_dev(hb_ctx* c, const double* d_params, int w, void* st
   HB_TRY(hbk::launch_prep(d_params, w, c->mags, c->d_wc, (hipStream_t)stream, nullptr, nullptr, c->d_t, c->plan.n,
                           c->d_ph, nullptr, 0, c->d_tab_pc),
          "hb_prep_kernel");
+  c->tab_chain = false;  // the table may hold another period now
   return 0;
 }
 

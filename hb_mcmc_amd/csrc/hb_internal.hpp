@@ -142,6 +142,13 @@ struct PreArgs {
   hbdev::WalkerConst* wc;   // records out (then read back by the eval waves)
   double2* ph;              // the global phase table (each workgroup writes a slice)
   double* tab_pc;           // its period [s]
+  // The previous fused launch's table period (a word only that launch wrote;
+  // the host alternates two, hb_ctx::tab_seq), or null when another kernel
+  // may have rewritten the table since: equal to this launch's P0, the global
+  // table is complete for it and the prologue loads it instead of computing
+  // it.  tab_mark: the word this launch writes for the next one.
+  const double* tab_prev;
+  double* tab_mark;
 };
 // walkers per workgroup of the fused launch for w walkers on `cus` CUs (0: the
 // two-launch path: prep + eval)

@@ -530,20 +530,31 @@ __device__ __forceinline__ void fused_prologue(const PreArgs& pa, int count, int
   // the table period: walker 0's (hb_prep_kernel's tab_pc of a single context)
   const double Pc0 = exp10(pa.params[2]) * kDay;
   auto tab_pc = [&](int) -> double { return Pc0; };
+  // The previous fused launch left the global table complete for Pc0 (the
+  // sampler's and the bench's steady state: the period is a sampler
+  // constant): load it (16 KB at N = 1024) instead of 1024 sincos per
+  // workgroup.  tab_prev is a word no workgroup of this launch writes, so
+  // every workgroup takes the same branch.
+  const bool cached = pa.tab_prev != nullptr && *pa.tab_prev == Pc0;
   // (sin, cos)(t_i DAY 2pi/Pc0) for i = first, first + stride, ... < n, into
   // LDS; this workgroup's slice [lo, hi) of the cadences also to the global table
   auto table = [&](int first, int stride) {
-    const double mA0 = kTwoPi / Pc0;
-    const int G = (int)gridDim.x;
-    const int lo = (int)((long)n * blockIdx.x / G), hi = (int)((long)n * (blockIdx.x + 1) / G);
-    for (int i = first; i < n; i += stride) {
-      double sv, cv;
-      sincos_table((t[i] * kDay) * mA0, sv, cv);
-      const double2 e = make_double2(sv, cv);
-      tabl[i] = e;
-      if (i >= lo && i < hi) pa.ph[i] = e;
+    if (cached) {
+      for (int i = first; i < n; i += stride) tabl[i] = pa.ph[i];
+    } else {
+      const double mA0 = kTwoPi / Pc0;
+      const int G = (int)gridDim.x;
+      const int lo = (int)((long)n * blockIdx.x / G), hi = (int)((long)n * (blockIdx.x + 1) / G);
+      for (int i = first; i < n; i += stride) {
+        double sv, cv;
+        sincos_table((t[i] * kDay) * mA0, sv, cv);
+        const double2 e = make_double2(sv, cv);
+        tabl[i] = e;
+        if (i >= lo && i < hi) pa.ph[i] = e;
+      }
+      if (blockIdx.x == 0 && first == 0 && pa.tab_pc != nullptr) *pa.tab_pc = Pc0;
     }
-    if (blockIdx.x == 0 && first == 0 && pa.tab_pc != nullptr) *pa.tab_pc = Pc0;
+    if (blockIdx.x == 0 && first == 0 && pa.tab_mark != nullptr) *pa.tab_mark = Pc0;
   };
   __syncthreads();
   HB_PCLK(1, 0);

@@ -704,6 +704,60 @@ def test_fused_launch_equals_two_launches(hbmi, oracle, n, w):
     close_logl(b[idx], oracle.loglike_batch(t, f, s, P[idx], synth.MAG_DEFAULT, synth.MAGERR_DEFAULT, 8))
 
 
+@pytest.mark.parametrize("w", [4096, 333])
+def test_fused_launch_phase_table_cache(hbmi, oracle, w):
+    """A fused launch that follows a fused launch of the same table period
+    loads the global phase table instead of computing it (fused_prologue,
+    PreArgs::tab_prev).  A sequence on one context -- period A twice, a batch
+    whose walker 0 has period B (the table is rebuilt), B again (cached), a
+    two-launch prep with period A in between (the chain breaks), then A, A --
+    gives every fused batch bit for bit the values of the two-launch path on
+    a fresh context, and the table it leaves serves hb_evaluate_dev."""
+    import torch
+
+    from hb_mcmc_amd import synth
+    from hb_mcmc_amd.likelihood import HBLikelihood
+
+    n = 1024
+    t, f, s = synth.dataset(n, oracle.light_curve)
+    PA = synth.walkers(w, seed=71)
+    PB = synth.walkers(w, seed=72)
+    PB[:, 2] += 3e-4            # every walker on period B (the table period of its batch)
+    PA[1::5, 2] += 1e-4         # a few off the table period: direct sincos
+    dev = torch.device("cuda", 0)
+
+    def two_launch(P):
+        with HBLikelihood(t, f, s) as R:
+            R.reserve(w)
+            o = torch.empty(w, dtype=torch.float64, device=dev)
+            R.prepare_dev(torch.from_numpy(P).to(dev))
+            R.evaluate_dev(w, o)
+            torch.cuda.synchronize()
+            return o.cpu().numpy()
+
+    want = {"A": two_launch(PA), "B": two_launch(PB)}
+    seq = ["A", "A", "B", "B", "prepA", "A", "A", "B", "A"]
+    with HBLikelihood(t, f, s) as L:
+        L.reserve(w)
+        assert L.fused_wpb(w) > 0
+        for k, name in enumerate(seq):
+            P = PA if name.endswith("A") else PB
+            Pd = torch.from_numpy(P).to(dev)
+            o = torch.empty(w, dtype=torch.float64, device=dev)
+            if name.startswith("prep"):
+                L.prepare_dev(Pd)
+                L.evaluate_dev(w, o)
+            else:
+                L.loglike_dev(Pd, o)
+            c = torch.empty(w, dtype=torch.float64, device=dev)
+            L.evaluate_dev(w, c)  # the records and global table this launch left behind
+            torch.cuda.synchronize()
+            got, again = o.cpu().numpy(), c.cpu().numpy()
+            ref = want[name[-1]]
+            assert np.array_equal(got, ref, equal_nan=True), f"step {k} ({name})"
+            assert np.array_equal(again, ref, equal_nan=True), f"step {k} ({name}): table left behind"
+
+
 # ------------------------------------------------- full-size (config C2)
 def test_full_size_c2_against_oracle_and_properties(hbmi, oracle):
     """W=4096, N=1024: oracle on a 256-walker sample; size-independent
