@@ -73,6 +73,8 @@ def parse():
                     help="launch and rendezvous only: every rank all-gathers its rank id (gloo/RCCL) and rank 0 "
                          "prints n_gpus; no GPU work (tests the --gpus N launcher on a CPU host)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline sample length")
+    ap.add_argument("--settle-ms", type=float, default=200.0,
+                    help="untimed back-to-back steps before the warmup steps (shader clock ramp; 0: none)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--timer", choices=("hip", "torch"), default="hip",
                     help="hip: libhbmi's fence-free HIP events (hb_timer_*); torch: torch.cuda.Event")
@@ -80,6 +82,8 @@ def parse():
                     help="steps of the kernel-timing pass after the timed region: HIP events around every "
                          "step's prep and eval launches (an event pair costs ~5 us of stream time, so the "
                          "timed steps carry none)")
+    ap.add_argument("--two-stream-steps", type=int, default=200,
+                    help="C2 batches through two contexts on two streams (c2_two_streams key; 0: skip)")
     ap.add_argument("--prior-steps", type=int, default=100,
                     help="C2 shape on prior-spread walkers (c2_prior_spread key; 0: skip)")
     ap.add_argument("--sampler-iters", type=int, default=100,
@@ -246,20 +250,24 @@ def sampler_e2e(L, w, iters, warm=20):
 
     logp = float(synth.THETA_STAR[2])
     out = {"walkers": w, "iters_timed": iters, "unit": "walker-steps/s (1 likelihood eval each)"}
+    # (the iterations timed are 20..320 of the run, as in every round: the
+    # chains' burn-in changes what an iteration costs; the shader clock is
+    # already settled by the likelihood legs that run first)
+    dwarm = warm
     # the device loop: three consecutive runs of `iters` iterations, the median
     # quoted (the swap schedules come from host producer threads, so a host
     # hiccup of a few ms shows up in one run of 10 ms, not in the others)
     reps = 3
-    S = SlotSampler(warm + reps * iters, w, logp, 0, w, run=0, npast=500, ladder=1, nthreads=16)
+    S = SlotSampler(dwarm + reps * iters, w, logp, 0, w, run=0, npast=500, ladder=1, nthreads=16)
     runs = []
     with DeviceSampler(S, L) as D:
         D.init_logl()
-        for it in range(warm):
+        for it in range(dwarm):
             D.step(it)
         D.sync()
         for r in range(reps):
             t0 = time.perf_counter()
-            for it in range(warm + r * iters, warm + (r + 1) * iters):
+            for it in range(dwarm + r * iters, dwarm + (r + 1) * iters):
                 D.step(it)
             D.sync()
             runs.append(time.perf_counter() - t0)
@@ -323,6 +331,49 @@ def sampler_e2e_sharded(L, w, iters, rank, world, warm=20):
             "unit": "walker-steps/s (1 likelihood eval each), all ranks",
             "device_loop_sharded": {"ms_per_iter": dt / iters * 1e3, "value": W * iters / dt,
                                     "exchange_bytes_per_rank_per_iter": 8.0 * exch / (warm + iters)}}
+
+
+def two_streams(L, t, f, s, P, w, steps, stream, dev):
+    """The same batches through two contexts on two HIP streams taking
+    alternate steps: consecutive batches are independent (different walker
+    sets), so a batch's workgroups start on the CUs the previous batch frees
+    while its last waves drain, instead of after the whole launch.  Reported
+    beside the headline (which keeps one stream, the reference sampler's
+    dependent-step shape), with every logL compared bit for bit."""
+    L2 = HBLikelihood(t, f, s, device=dev.index)
+    L2.reserve(w)
+    ctx = [L, L2]
+    st = [stream, torch.cuda.Stream(device=dev)]
+    nb = len(P)
+    outs = [torch.empty(w, dtype=torch.float64, device=dev) for _ in range(nb)]
+
+    def run(two, k0, k1):
+        for k in range(k0, k1):
+            i = k & 1 if two else 0
+            ctx[i].loglike_dev(P[k % nb], outs[k % nb], st[i])
+
+    res = {}
+    for mode in ("one", "two"):
+        run(mode == "two", 0, 20)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        run(mode == "two", 0, steps)
+        torch.cuda.synchronize()
+        res[mode] = (time.perf_counter() - t0) / steps
+    ref = []
+    for k in range(nb):
+        L.loglike_dev(P[k], outs[k], stream)
+    torch.cuda.synchronize()
+    ref = [o.cpu().numpy().copy() for o in outs]
+    run(True, 0, 2 * nb)
+    torch.cuda.synchronize()
+    same = all(np.array_equal(ref[k], outs[k].cpu().numpy(), equal_nan=True) for k in range(nb))
+    L2.close()
+    return {"steps": steps, "walkers": w, "unit": "evals/s",
+            "one_stream": {"ms_per_step": res["one"] * 1e3, "value": w / res["one"]},
+            "two_streams": {"ms_per_step": res["two"] * 1e3, "value": w / res["two"]},
+            "logl_bit_identical": bool(same),
+            "what": "two contexts on two streams take alternate batches (independent walker sets); not the headline"}
 
 
 def computed_prior_walkers(L, w, seed, dev, stream):
@@ -525,6 +576,32 @@ def roofline(config, kernel_ms, evals_per_call, hbm_bytes_per_call, extra):
     return out
 
 
+def settle_clock(step, ms, drain=None):
+    """Back-to-back steps for `ms` milliseconds before the warmup steps: the
+    shader clock ramps up over the first milliseconds of sustained work
+    (MI355X_MICROARCH.md, DVFS item 6: measure after back-to-back launches),
+    so a handful of warmup steps alone leaves the timed steps on a rising
+    clock -- 38-41 us per C2 step after 5 warmup steps against 35-36 us at
+    steady state on the same box (profiles/r06/r06l_*).  Untimed; the line
+    reports what ran."""
+    if ms <= 0:
+        return {"ms": 0.0, "steps": 0}
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    k = 0
+    while True:
+        for _ in range(16):
+            step(k)
+            k += 1
+        if drain is not None:
+            drain()
+        torch.cuda.synchronize()
+        if (time.perf_counter() - t0) * 1e3 >= ms:
+            break
+    return {"ms": (time.perf_counter() - t0) * 1e3, "steps": k,
+            "why": "untimed back-to-back steps before the warmup: the shader clock ramps up under sustained load"}
+
+
 def make_event(kind):
     return _HipEvent() if kind == "hip" else torch.cuda.Event(enable_timing=True)
 
@@ -572,6 +649,7 @@ def run_c5(a, rank, world, local, dev, pg):
          for k in range(nb)]
     out = torch.empty(wtot, dtype=torch.float64, device=dev)
     stream = torch.cuda.current_stream()
+    settle = settle_clock(lambda k: cat.loglike_dev(P[k % nb], wpt, out, stream), a.settle_ms)
     for k in range(a.warmup):
         cat.loglike_dev(P[k % nb], wpt, out, stream)
     torch.cuda.synchronize()
@@ -612,6 +690,7 @@ def run_c5(a, rank, world, local, dev, pg):
                            "targets": a.targets, "walkers_per_target": a.walkers_per_target,
                            "global_walkers": a.targets * a.walkers_per_target,
                            "parallelism": f"targets dealt over {world} GPU(s) by cadence count, no collective"},
+                "settle": settle,
                 "roofline": roofline("C5", call_ms, float(wtot), bytes_step,
                                      {"kernel": "hb_catalog call (hb_prep_kernel + hb_eval_catalog_kernel, every "
                                                 "size class in one launch), rank 0", "kernel_ms": call_ms, "kernel_event_samples": ks,
@@ -706,6 +785,7 @@ def main():
                 pending[b].wait()
                 pending[b] = None
 
+    settle = settle_clock(step, a.settle_ms, drain)
     for k in range(a.warmup):
         step(k)
     drain()
@@ -792,12 +872,15 @@ def main():
                                   "kernel_event_samples": len(timed), "kernel_timer": a.timer,
                                   "bytes_per_eval": bytes_per_eval}),
             "kernel_only_evals_per_s": w / ((eval_ms + prep_ms) * 1e-3),
+            "settle": settle,
             "nonfinite_logl_last_batch": nonfinite,
         }
         if world > 1:
             line["process_group"] = pg
             line["allgather_check"] = {"ok": gather_ok, "doubles_per_step": world * w,
                                        "what": "last timed step's gathered logL equals each rank's own, on every rank"}
+        if world == 1 and a.two_stream_steps > 0:
+            line["c2_two_streams"] = two_streams(L, t, f, s, P, w, a.two_stream_steps, stream, dev)
         if world == 1 and a.prior_steps > 0 and n <= 2048:
             line["c2_prior_spread"] = prior_spread(L, n, w, a.prior_steps, stream, dev, a.timer)
             line["c2_prior_spread_computed"] = prior_spread(L, n, w, a.prior_steps, stream, dev, a.timer,

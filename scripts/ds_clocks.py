@@ -71,7 +71,16 @@ res = {"span_us": float((rt1.max() - k0) / 100.0),
                    for t in sorted(set(jt.tolist()))},
        "last_64": {"temp_decile_median": float(np.median(dec[np.argsort(rt1)[-64:]])),
                    "life_us_median": float(np.median(life[np.argsort(rt1)[-64:]])),
-                   "start_us_median": float(np.median((rt0[np.argsort(rt1)[-64:]] - k0) / 100.0))},
+                   "start_us_median": float(np.median((rt0[np.argsort(rt1)[-64:]] - k0) / 100.0)),
+                   "phase_cycles_median": dict(zip(names, [float(x) for x in
+                                                            np.median(ph[np.argsort(rt1)[-64:]], axis=0)])),
+                   "phase_cycles_max": dict(zip(names, [float(x) for x in ph[np.argsort(rt1)[-64:]].max(axis=0)])),
+                   "temp_decile_hist": [int(x) for x in np.bincount(dec[np.argsort(rt1)[-64:]], minlength=10)]},
+       "slowest_64_by_life": {"life_us_median": float(np.median(np.sort(life)[-64:])),
+                              "phase_cycles_median": dict(zip(names, [float(x) for x in
+                                                                       np.median(ph[np.argsort(life)[-64:]], axis=0)])),
+                              "temp_decile_hist": [int(x) for x in
+                                                   np.bincount(dec[np.argsort(life)[-64:]], minlength=10)]},
        "shader_clock_ghz_median": float(np.median((ck[:, 7] - ck[:, 0]) / np.maximum(rt1 - rt0, 1)) * 0.1)}
 rp = c[:, 12:16].astype(np.int64)
 if (rp[:, 0] > 0).any():  # the deferred-swap replay (defer builds): staging, levels, entries, levels
