@@ -442,7 +442,11 @@ def prior_spread(L, n, w, steps, stream, dev, timer, ks=50, computed=False):
 DROPIN_LEGS = (("dropin", "hb_mcmc_ref_hbmi", {}),
                ("dropin_memo_off", "hb_mcmc_ref_hbmi", {"HBMI_DROPIN_MEMO": "0"}),
                ("dropin_profile", "hb_mcmc_ref_hbmi", {"HBMI_DROPIN_PROFILE": "1"}),
-               ("reference_cpu", "hb_mcmc_ref", {}))
+               ("reference_cpu", "hb_mcmc_ref", {}),
+               # the caller's OpenMP runtime told not to spin at its barriers: its 25
+               # threads share the box's 16-core CPU share with the drop-in's leader
+               ("dropin_omp_passive", "hb_mcmc_ref_hbmi", {"OMP_WAIT_POLICY": "passive"}),
+               ("reference_cpu_omp_passive", "hb_mcmc_ref", {"OMP_WAIT_POLICY": "passive"}))
 
 
 def dropin_rate(niter, legs=DROPIN_LEGS):

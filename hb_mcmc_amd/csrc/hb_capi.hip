@@ -861,16 +861,19 @@ double env_num(const char* name, double dflt) {
 // written by the kernels in pinned host memory, no DMA copies),
 // HBMI_DROPIN_POLL=1 (the leader polls the stream instead of
 // hipStreamSynchronize), HBMI_DROPIN_LAT=1 (the multi-wave latency plan),
-// HBMI_DROPIN_LANES (batches in flight at once, hb_dropin.hpp).
+// HBMI_DROPIN_LANES (batches in flight at once, hb_dropin.hpp),
+// HBMI_DROPIN_BLOCK=1 (the leader sleeps on a blocking-sync event).
 struct DropPolicy {
   double spin_s, window_s;
   bool zc, poll, lat;
   int lanes;
+  bool block;
 };
 const DropPolicy& drop_policy() {
   static const DropPolicy p{env_num("HBMI_DROPIN_SPIN_US", 0) * 1e-6, env_num("HBMI_DROPIN_WINDOW_US", 0) * 1e-6,
                             env_num("HBMI_DROPIN_ZC", 0) != 0, env_num("HBMI_DROPIN_POLL", 0) != 0,
-                            env_num("HBMI_DROPIN_LAT", 0) != 0, (int)env_num("HBMI_DROPIN_LANES", 1)};
+                            env_num("HBMI_DROPIN_LAT", 0) != 0, (int)env_num("HBMI_DROPIN_LANES", 1),
+                            env_num("HBMI_DROPIN_BLOCK", 0) != 0};
   return p;
 }
 
@@ -881,6 +884,7 @@ struct DropLane {
   double* h_out = nullptr;      // pinned, hcap
   double* dv_params = nullptr;  // their device addresses (zero-copy mode)
   double* dv_out = nullptr;
+  hipEvent_t done = nullptr;    // blocking-sync event (HBMI_DROPIN_BLOCK=1)
   int hcap = 0;
 };
 // One drop-in light curve: `nlanes` identical contexts, each with its own
@@ -901,6 +905,7 @@ void dropctx_destroy(DropCtx* d) {
     if (l.c) (void)hipSetDevice(l.c->device);
     if (l.h_params) (void)hipHostFree(l.h_params);
     if (l.h_out) (void)hipHostFree(l.h_out);
+    if (l.done) (void)hipEventDestroy(l.done);
     if (l.s) (void)hipStreamDestroy(l.s);
     hb_destroy(l.c);
   }
@@ -920,8 +925,10 @@ DropCtx* dropctx_create(const double* t, const double* f, const double* s, long 
       return nullptr;
     }
     if (drop_policy().lat) (void)hb_ctx_set_latency_plan(l.c, 1);
-    if (hipStreamCreateWithFlags(&l.s, hipStreamNonBlocking) != hipSuccess) {
-      set_err_msg("drop-in: hipStreamCreateWithFlags failed");
+    if (hipStreamCreateWithFlags(&l.s, hipStreamNonBlocking) != hipSuccess ||
+        (drop_policy().block &&
+         hipEventCreateWithFlags(&l.done, hipEventBlockingSync | hipEventDisableTiming) != hipSuccess)) {
+      set_err_msg("drop-in: hipStreamCreateWithFlags / hipEventCreateWithFlags failed");
       dropctx_destroy(d.release());
       return nullptr;
     }
@@ -978,6 +985,10 @@ int dropctx_eval(DropCtx* d, int k, const double* rows, int w, double* out, hbdr
   if (rc) return rc;
   if (rows != l.h_params) dropctx_stage(d, k, w), memcpy(l.h_params, rows, sizeof(double) * 21 * (size_t)w);
   auto wait = [&]() -> hipError_t {
+    if (l.done) {  // sleep in the driver instead of spinning: the caller's threads need the cores
+      hipError_t e = hipEventRecord(l.done, l.s);
+      return e != hipSuccess ? e : hipEventSynchronize(l.done);
+    }
     if (!pol.poll) return hipStreamSynchronize(l.s);
     hipError_t e;
     while ((e = hipStreamQuery(l.s)) == hipErrorNotReady) hbdrop::Entry<DropCtx>::relax();

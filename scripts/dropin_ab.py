@@ -16,14 +16,12 @@ import bench  # noqa: E402
 VARIANTS = {
     "base": {},
     "memo_off": {"HBMI_DROPIN_MEMO": "0"},
-    "lanes2": {"HBMI_DROPIN_LANES": "2"},
-    "lanes4": {"HBMI_DROPIN_LANES": "4"},
-    "lanes4_spin": {"HBMI_DROPIN_LANES": "4", "HBMI_DROPIN_SPIN_US": "200"},
-    "lanes4_zc": {"HBMI_DROPIN_LANES": "4", "HBMI_DROPIN_ZC": "1"},
-    "lanes8": {"HBMI_DROPIN_LANES": "8"},
-    "lanes4_lat": {"HBMI_DROPIN_LANES": "4", "HBMI_DROPIN_LAT": "1"},
-    "lanes4_omp_passive": {"HBMI_DROPIN_LANES": "4", "OMP_WAIT_POLICY": "passive"},
+    "block": {"HBMI_DROPIN_BLOCK": "1"},
     "spin_win": {"HBMI_DROPIN_SPIN_US": "300", "HBMI_DROPIN_WINDOW_US": "30"},
+    "block_win": {"HBMI_DROPIN_BLOCK": "1", "HBMI_DROPIN_WINDOW_US": "30"},
+    "lanes2_block": {"HBMI_DROPIN_LANES": "2", "HBMI_DROPIN_BLOCK": "1"},
+    "omp_passive": {"OMP_WAIT_POLICY": "passive"},
+    "block_omp_passive": {"HBMI_DROPIN_BLOCK": "1", "OMP_WAIT_POLICY": "passive"},
 }
 
 
@@ -43,8 +41,9 @@ def main():
                               "batches_per_iter": st.get("batches_per_iter"), "mean_batch": st.get("mean_batch"),
                               "us_per_batch": st.get("us_per_batch"),
                               "us_wake_per_waiter": st.get("us_wake_per_waiter")}), flush=True)
-    ref = bench.dropin_rate(niter, legs=(("reference_cpu", "hb_mcmc_ref", {}),)).get("reference_cpu", {})
-    print(json.dumps({"reference_cpu_iters_per_s": ref.get("iters_per_s")}))
+    for env in ({}, {"OMP_WAIT_POLICY": "passive"}):
+        ref = bench.dropin_rate(niter, legs=(("reference_cpu", "hb_mcmc_ref", env),)).get("reference_cpu", {})
+        print(json.dumps({"reference_cpu_iters_per_s": ref.get("iters_per_s"), "env": env}))
     for k, v in res.items():
         ok = sorted(x for x in v if x)
         print(f"{k:18s} median {ok[len(ok) // 2] if ok else float('nan'):9.1f} it/s  runs {[round(x or 0) for x in v]}")
