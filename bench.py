@@ -89,8 +89,9 @@ def parse():
     ap.add_argument("--sampler-iters", type=int, default=100,
                     help="also time the whole PT-MCMC iteration (mcmc_wrapper2.c loop) at the workload's W and N: "
                          "device-resident sampler vs the host sampler + GPU likelihood (0 = skip)")
-    ap.add_argument("--dropin-iters", type=int, default=1000,
-                    help="iterations of the reference sampler relinked against libhbmi.so (dropin field; 0 = skip)")
+    ap.add_argument("--dropin-iters", type=int, default=2000,
+                    help="iterations of the reference sampler relinked against libhbmi.so (dropin field; each leg "
+                         "also runs a tenth as many to take the process start out of the rate; 0 = skip)")
     a = ap.parse_args()
     if a.walkers is None:
         a.walkers = 8192 if a.config == "C4" else 4096
@@ -449,7 +450,20 @@ DROPIN_LEGS = (("dropin", "hb_mcmc_ref_hbmi", {}),
                ("reference_cpu_omp_passive", "hb_mcmc_ref", {"OMP_WAIT_POLICY": "passive"}))
 
 
-def dropin_rate(niter, legs=DROPIN_LEGS):
+def dropin_workdir(tmp, g):
+    """The directory tree mcmc_wrapper2.c reads and writes under HBREF_ROOT,
+    with TIC 127079833's folded light curve (the trace test's input)."""
+    from hb_mcmc_amd.hbio import write_folded_lc
+
+    d = os.path.join(tmp, "data", "lightcurves", "folded_lightcurves")
+    os.makedirs(d)
+    write_folded_lc(os.path.join(d, "127079833_new.txt"), g["lc_t"], g["lc_f"], g["lc_e"])
+    for sub in ("subpars", "pars", "chains", "logL", "log", "lightcurves/mcmc_lightcurves"):
+        os.makedirs(os.path.join(tmp, "data", sub), exist_ok=True)
+    os.makedirs(os.path.join(tmp, "debug"))
+
+
+def dropin_rate(niter, legs=DROPIN_LEGS, short=None):
     """The literal north_star drop-in: the reference's OWN sampler
     (src/mcmc_wrapper2.c, unmodified, 25 OpenMP threads) relinked against
     libhbmi.so (`make -C oracle dropin` -> oracle/_ref/hb_mcmc_ref_hbmi), so
@@ -457,58 +471,73 @@ def dropin_rate(niter, legs=DROPIN_LEGS):
     mcmc_wrapper2.c:488-489) runs through the likelihood3.h entry point on the
     GPU.  Timed on TIC 127079833's folded light curve (the trace test's input),
     next to the same sampler built with likelihood3.c (oracle/_ref/hb_mcmc_ref)
-    on the host cores.  Child processes; nothing here touches HIP."""
+    on the host cores.  Child processes; nothing here touches HIP.
+
+    Every leg runs twice, `short` and `niter` iterations: `iters_per_s` is the
+    sampler's rate, (niter - short) / (wall(niter) - wall(short)), the same
+    rule for the GPU and the CPU legs; `startup_s` is what the process spends
+    outside its iterations (for the drop-in: HIP runtime start, code-object
+    load, context creation, ≈ 0.35 s, profiles/r06/r06s_dropin_fixed.txt), and
+    `iters_per_s_wall` = niter / wall(niter) includes it."""
     import subprocess
     import tempfile
 
     exe = os.path.join(ROOT, "oracle", "_ref", "hb_mcmc_ref_hbmi")
     if not os.path.exists(exe):
         return {"error": "oracle/_ref/hb_mcmc_ref_hbmi not built (make -C oracle dropin)"}
-    from hb_mcmc_amd.hbio import write_folded_lc
-
+    short = max(20, niter // 10) if short is None else short
+    if not 0 < short < niter:
+        raise ValueError("dropin_rate: need 0 < short < niter")
     g = np.load(os.path.join(ROOT, "tests", "golden", "sampler_127079833.npz"))
-    out = {"niter": niter, "chains": 50, "light_curve": f"TIC 127079833 folded, N = {len(g['lc_t'])}",
-           "unit": "sampler iterations/s (100 scalar loglikelihood() calls each)"}
-    for key, name, extra in legs:
-        path = os.path.join(ROOT, "oracle", "_ref", name)
-        if not os.path.exists(path):
-            continue
+    out = {"niter": niter, "niter_short": short, "chains": 50,
+           "light_curve": f"TIC 127079833 folded, N = {len(g['lc_t'])}",
+           "unit": "sampler iterations/s (100 scalar loglikelihood() calls each), "
+                   "(niter - niter_short) / (wall(niter) - wall(niter_short))"}
+
+    def run(path, name, n, extra):
         with tempfile.TemporaryDirectory() as tmp:
-            d = os.path.join(tmp, "data", "lightcurves", "folded_lightcurves")
-            os.makedirs(d)
-            write_folded_lc(os.path.join(d, "127079833_new.txt"), g["lc_t"], g["lc_f"], g["lc_e"])
-            for sub in ("subpars", "pars", "chains", "logL", "log", "lightcurves/mcmc_lightcurves"):
-                os.makedirs(os.path.join(tmp, "data", sub), exist_ok=True)
-            os.makedirs(os.path.join(tmp, "debug"))
+            dropin_workdir(tmp, g)
             stats_path = os.path.join(tmp, "dropin_stats.json")
             env = dict(os.environ, HBREF_ROOT=tmp, **extra)
             if name == "hb_mcmc_ref_hbmi":
                 env["HBMI_DROPIN_STATS"] = stats_path  # libhbmi writes its drop-in counters at exit
             t0 = time.perf_counter()
-            r = subprocess.run([path, str(niter), "127079833", "0.5021", "0"], cwd=tmp, capture_output=True,
+            r = subprocess.run([path, str(n), "127079833", "0.5021", "0"], cwd=tmp, capture_output=True,
                                text=True, timeout=600, env=env)
             dt = time.perf_counter() - t0
             st = None
             if os.path.exists(stats_path):
                 with open(stats_path) as fp:
                     st = json.load(fp)
-        if r.returncode != 0:
-            out[key] = {"error": r.stderr[-300:]}
+        return r, dt, st
+
+    for key, name, extra in legs:
+        path = os.path.join(ROOT, "oracle", "_ref", name)
+        if not os.path.exists(path):
             continue
-        out[key] = {"iters_per_s": niter / dt, "loglik_calls_per_s": 100.0 * niter / dt, "wall_s": dt}
+        r0, dt0, _ = run(path, name, short, extra)
+        r, dt, st = run(path, name, niter, extra)
+        if r0.returncode != 0 or r.returncode != 0:
+            out[key] = {"error": (r0.stderr if r0.returncode else r.stderr)[-300:]}
+            continue
+        rate = (niter - short) / (dt - dt0) if dt > dt0 else niter / dt
+        out[key] = {"iters_per_s": rate, "loglik_calls_per_s": 100.0 * rate, "iters_per_s_wall": niter / dt,
+                    "wall_s": dt, "wall_short_s": dt0, "startup_s": max(0.0, dt - niter / rate)}
         if extra:
             out[key]["env"] = extra
-        if st:  # per-iteration breakdown of the drop-in's GPU round trips (hb_dropin.hpp Stats)
+        if st:  # per-iteration breakdown of the drop-in's GPU round trips (hb_dropin.hpp Stats), niter run
             b = max(1, st["batches"])
             st["batches_per_iter"] = st["batches"] / niter
             st["mean_batch"] = st["walkers"] / b
             st["memo_hit_frac"] = st["memo_hits"] / max(1, st["calls"])
             st["us_per_batch"] = {k[2:]: st[k] / b * 1e6 for k in ("s_combine", "s_upload", "s_launch",
                                                                    "s_download_sync")}
-            st["us_wake_per_waiter"] = st["s_wake"] / max(1, st["walkers"] - st["batches"]) * 1e6
+            st["us_wake_per_waiter"] = st["s_wake"] / max(1, st.get("waiters", st["walkers"] - st["batches"])) * 1e6
             out[key]["stats"] = st
-    if "iters_per_s" in out.get("dropin", {}) and "iters_per_s" in out.get("reference_cpu", {}):
-        out["speedup_vs_reference_cpu"] = out["dropin"]["iters_per_s"] / out["reference_cpu"]["iters_per_s"]
+    d, c = out.get("dropin", {}), out.get("reference_cpu", {})
+    if "iters_per_s" in d and "iters_per_s" in c:
+        out["speedup_vs_reference_cpu"] = d["iters_per_s"] / c["iters_per_s"]
+        out["speedup_vs_reference_cpu_wall"] = d["iters_per_s_wall"] / c["iters_per_s_wall"]
     return out
 
 

@@ -862,18 +862,20 @@ double env_num(const char* name, double dflt) {
 // HBMI_DROPIN_POLL=1 (the leader polls the stream instead of
 // hipStreamSynchronize), HBMI_DROPIN_LAT=1 (the multi-wave latency plan),
 // HBMI_DROPIN_LANES (batches in flight at once, hb_dropin.hpp),
-// HBMI_DROPIN_BLOCK=1 (the leader sleeps on a blocking-sync event).
+// HBMI_DROPIN_BLOCK=1 (the leader sleeps on a blocking-sync event),
+// HBMI_DROPIN_CHAIN (further batches a leader may lead, hb_dropin.hpp).
 struct DropPolicy {
   double spin_s, window_s;
   bool zc, poll, lat;
   int lanes;
   bool block;
+  int chain;
 };
 const DropPolicy& drop_policy() {
   static const DropPolicy p{env_num("HBMI_DROPIN_SPIN_US", 0) * 1e-6, env_num("HBMI_DROPIN_WINDOW_US", 0) * 1e-6,
                             env_num("HBMI_DROPIN_ZC", 0) != 0, env_num("HBMI_DROPIN_POLL", 0) != 0,
                             env_num("HBMI_DROPIN_LAT", 0) != 0, (int)env_num("HBMI_DROPIN_LANES", 1),
-                            env_num("HBMI_DROPIN_BLOCK", 0) != 0};
+                            env_num("HBMI_DROPIN_BLOCK", 0) != 0, (int)env_num("HBMI_DROPIN_CHAIN", 0)};
   return p;
 }
 
@@ -1030,6 +1032,7 @@ hbdrop::Cache<DropCtx>& dropin_cache() {
                                         e.spin_s = drop_policy().spin_s;
                                         e.window_s = drop_policy().window_s;
                                         e.lanes = e.ctx->nlanes;
+                                        e.chain = drop_policy().chain;
                                       });
   }();
   return *c;
@@ -1067,6 +1070,7 @@ void stats_sum(hbdrop::Stats& a, const hbdrop::Stats& b) {
   a.s_launch += b.s_launch;
   a.s_download += b.s_download;
   a.s_wake += b.s_wake;
+  a.waiters += b.waiters;
 }
 
 hbdrop::Stats dropin_totals(uint64_t* contexts) {
@@ -1076,6 +1080,7 @@ hbdrop::Stats dropin_totals(uint64_t* contexts) {
     std::lock_guard<std::mutex> lk(e->mu);
     hbdrop::Stats x = e->st;
     x.s_wake = 1e-9 * (double)e->wake_ns.load();
+    x.waiters = e->wake_n.load();
     stats_sum(tot, x);
   }
   if (contexts) *contexts = dropin_cache().created();
@@ -1092,10 +1097,11 @@ void dropin_write_stats() {
   fprintf(fp,
           "{\"calls\": %llu, \"memo_hits\": %llu, \"batches\": %llu, \"walkers\": %llu, \"max_batch\": %llu, "
           "\"contexts_created\": %llu, \"profile_mode\": %s, \"s_combine\": %.9g, \"s_upload\": %.9g, "
-          "\"s_launch\": %.9g, \"s_download_sync\": %.9g, \"s_wake\": %.9g}\n",
+          "\"s_launch\": %.9g, \"s_download_sync\": %.9g, \"s_wake\": %.9g, \"waiters\": %llu}\n",
           (unsigned long long)s.calls, (unsigned long long)s.memo_hits, (unsigned long long)s.batches,
           (unsigned long long)s.walkers, (unsigned long long)s.max_batch, (unsigned long long)created,
-          dropin_profile() ? "true" : "false", s.s_combine, s.s_upload, s.s_launch, s.s_download, s.s_wake);
+          dropin_profile() ? "true" : "false", s.s_combine, s.s_upload, s.s_launch, s.s_download, s.s_wake,
+          (unsigned long long)s.waiters);
   fclose(fp);
 }
 

@@ -160,6 +160,7 @@ struct Stats {
   // upload, launch and download + wait (split by Eval, see Times); callers'
   // wake-up after their batch completed
   double s_combine = 0, s_upload = 0, s_launch = 0, s_download = 0, s_wake = 0;
+  uint64_t waiters = 0;
 };
 
 // What an evaluation reports: seconds in its upload, launch and download +
@@ -209,7 +210,7 @@ struct Entry {
   std::atomic<bool> use_memo{true};
   std::vector<double> params[kMaxLanes], out[kMaxLanes];  // per-lane staging (when Stage gives none)
   Stats st;
-  std::atomic<uint64_t> wake_ns{0};
+  std::atomic<uint64_t> wake_ns{0}, wake_n{0};  // callers answered in another caller's batch
   // Policy (set by the owner before use):
   //  * lanes: batches that may be in flight at once, each on its own lane;
   //    a caller that finds a free lane leads a batch right away instead of
@@ -219,8 +220,12 @@ struct Entry {
   //    condition variable;
   //  * window_s: a new leader waits up to this long for the queue to reach
   //    the largest batch of the last kWindowHist batches before it launches.
+  //  * chain: a leader whose own request is answered leads up to this many
+  //    further batches from the queue before it returns, so the next batch is
+  //    launched at once instead of after a waiter wakes up.
   int lanes = 1;
   double spin_s = 0, window_s = 0;
+  int chain = 0;
   static constexpr int kWindowHist = 16;
   int hist[kWindowHist] = {0};
   int nhist = 0;
@@ -245,13 +250,19 @@ struct Entry {
     npending.store((int)pending.size(), std::memory_order_release);
     const int nl = lanes < 1 ? 1 : lanes > kMaxLanes ? kMaxLanes : lanes;
     bool spun = false;
+    int led = 0;  // batches this caller led
     for (;;) {
-      if (r.done.load(std::memory_order_acquire)) {
-        wake_ns.fetch_add((uint64_t)((now_s() - r.t_done) * 1e9), std::memory_order_relaxed);
+      const bool can_lead = inflight.load(std::memory_order_relaxed) < nl && !pending.empty();
+      if (r.done.load(std::memory_order_acquire) && !(can_lead && led > 0 && led <= chain)) {
+        if (led == 0) {
+          wake_ns.fetch_add((uint64_t)((now_s() - r.t_done) * 1e9), std::memory_order_relaxed);
+          wake_n.fetch_add(1, std::memory_order_relaxed);
+        }
         *result = r.out;
         return r.rc;
       }
-      if (inflight.load(std::memory_order_relaxed) < nl && !pending.empty()) {  // lead a batch on a free lane
+      if (can_lead) {  // lead a batch on a free lane
+        ++led;
         int lane = 0;
         while (lane_busy >> lane & 1u) ++lane;
         lane_busy |= 1u << lane;
@@ -304,7 +315,7 @@ struct Entry {
         lane_busy &= ~(1u << lane);
         inflight.fetch_sub(1, std::memory_order_relaxed);
         cv.notify_all();
-        continue;  // own request done (it was in the batch): returns above
+        continue;  // own request done (it was in the first batch): returns above, or chains
       }
       if (spin_s > 0 && !spun) {  // poll first, sleep after
         spun = true;

@@ -22,6 +22,12 @@ VARIANTS = {
     "lanes2_block": {"HBMI_DROPIN_LANES": "2", "HBMI_DROPIN_BLOCK": "1"},
     "omp_passive": {"OMP_WAIT_POLICY": "passive"},
     "block_omp_passive": {"HBMI_DROPIN_BLOCK": "1", "OMP_WAIT_POLICY": "passive"},
+    "chain1": {"HBMI_DROPIN_CHAIN": "1"},
+    "chain2": {"HBMI_DROPIN_CHAIN": "2"},
+    "chain4": {"HBMI_DROPIN_CHAIN": "4"},
+    "chain8": {"HBMI_DROPIN_CHAIN": "8"},
+    "chain64": {"HBMI_DROPIN_CHAIN": "64"},
+    "chain4_omp_passive": {"HBMI_DROPIN_CHAIN": "4", "OMP_WAIT_POLICY": "passive"},
 }
 
 

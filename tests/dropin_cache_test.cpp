@@ -143,9 +143,9 @@ int main() {
   //    mcmc_wrapper2.c:488-489; every result exact, the x calls memo hits
   //    after the first iteration, and batches combine several callers --
   //    with the waiters sleeping at once, and with the spin / batch-window
-  //    policy libhbmi can switch on
+  //    policy libhbmi can switch on, and with leaders chaining batches
   g_eval_us = 20;
-  for (int pol = 0; pol < 5; ++pol) {
+  for (int pol = 0; pol < 7; ++pol) {
     std::vector<double> fp(f2);
     fp[0] += 1e-6 * (pol + 1);  // a fresh context per policy
     auto e = cache.get(t.data(), fp.data(), s.data(), n, mag, err);
@@ -153,6 +153,7 @@ int main() {
     e->window_s = pol == 2 ? 30e-6 : 0.0;
     e->lanes = pol >= 3 ? 4 : 1;  // policy 3: four lanes with spinning, 4: four lanes, sleeping waiters
     if (pol == 4) e->spin_s = 0.0;
+    if (pol >= 5) e->spin_s = 0.0, e->lanes = pol == 5 ? 1 : 2, e->chain = 4;  // leaders chain batches
     g_conc_max = 0;
     const int nth = 25, iters = 40;
     const int ev0 = e->ctx->evals;
