@@ -463,7 +463,7 @@ def dropin_workdir(tmp, g):
     os.makedirs(os.path.join(tmp, "debug"))
 
 
-def dropin_rate(niter, legs=DROPIN_LEGS, short=None):
+def dropin_rate(niter, legs=DROPIN_LEGS, short=None, ref_dir=None):
     """The literal north_star drop-in: the reference's OWN sampler
     (src/mcmc_wrapper2.c, unmodified, 25 OpenMP threads) relinked against
     libhbmi.so (`make -C oracle dropin` -> oracle/_ref/hb_mcmc_ref_hbmi), so
@@ -482,7 +482,8 @@ def dropin_rate(niter, legs=DROPIN_LEGS, short=None):
     import subprocess
     import tempfile
 
-    exe = os.path.join(ROOT, "oracle", "_ref", "hb_mcmc_ref_hbmi")
+    ref_dir = ref_dir or os.path.join(ROOT, "oracle", "_ref")  # (tests pass stand-in programs)
+    exe = os.path.join(ref_dir, "hb_mcmc_ref_hbmi")
     if not os.path.exists(exe):
         return {"error": "oracle/_ref/hb_mcmc_ref_hbmi not built (make -C oracle dropin)"}
     short = max(20, niter // 10) if short is None else short
@@ -512,7 +513,7 @@ def dropin_rate(niter, legs=DROPIN_LEGS, short=None):
         return r, dt, st
 
     for key, name, extra in legs:
-        path = os.path.join(ROOT, "oracle", "_ref", name)
+        path = os.path.join(ref_dir, name)
         if not os.path.exists(path):
             continue
         r0, dt0, _ = run(path, name, short, extra)

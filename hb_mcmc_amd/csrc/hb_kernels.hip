@@ -119,6 +119,7 @@ __global__ __launch_bounds__(kPrepThreads) void hb_prep_kernel(const double* __r
                                                               double* __restrict__ tab_pc_out) {
   constexpr int kPrepWalkers = NW;
   __shared__ PrepShared<kPrepWalkers> L;
+  HB_PCLK(0, 0);  // clock builds: 0 entry, 1 parameters in LDS, 2 records stored, 3/4 waves 0/3 done
   const int G = (int)gridDim.x;
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -158,6 +159,7 @@ __global__ __launch_bounds__(kPrepThreads) void hb_prep_kernel(const double* __r
     }
   }
   __syncthreads();
+  HB_PCLK(1, 0);
   const double lpc_first = cw_first >= 0 ? params[(size_t)cw_first * kNpars + 2] : 0.0;
   // the table period: walker 0's (single context) or the first walker's of
   // the walker's target in this batch (catalog)
@@ -197,6 +199,7 @@ __global__ __launch_bounds__(kPrepThreads) void hb_prep_kernel(const double* __r
       if (i < nb * kWcDoubles) dst[i] = v[u];
     }
   }
+  HB_PCLK(2, 0);
   // Catalog phase tables (WalkerConst::tab), written after the walker records
   // so their latency overlaps the stores: cadence i of target k, for the
   // period of k's first walker cw0[i] in this batch (-1: no walkers), ph[i] =
@@ -216,6 +219,8 @@ __global__ __launch_bounds__(kPrepThreads) void hb_prep_kernel(const double* __r
       ph[i] = make_double2(sv, cv);
     }
   }
+  HB_PCLK(3, 0);
+  HB_PCLK(4, 192);
 }
 
 // ---------------------------------------------------------------------------

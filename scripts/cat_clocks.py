@@ -99,5 +99,19 @@ for q in sorted(set(cls.tolist()), reverse=True):
 edges = np.arange(0, int((rt1.max() - k0) / 100) + 2)
 occ = [int(((rt0 - k0) / 100.0 <= e).sum() - ((rt1 - k0) / 100.0 <= e).sum()) for e in edges]
 res["resident_waves_per_us"] = occ
+# the records launch (hb_prep_kernel<32>, 512 workgroups at C5): prologue marks
+# of the last call, shader cycles from each workgroup's entry
+nwg = (W + 31) // 32
+pb = (C.c_ulonglong * (16 * nwg))()
+assert lib.hb_debug_prologue_clocks(pb, nwg) == 0
+pc = np.frombuffer(pb, dtype=np.uint64).reshape(nwg, 16).astype(np.int64)
+pm = {1: "params in LDS", 5: "role 0 phase 1", 6: "role 1 phase 1", 7: "role 2 phase 1", 8: "role 3 phase 1",
+      9: "role 0 phase 2", 10: "role 1 phase 2", 11: "role 2 phase 2", 12: "role 3 phase 2", 2: "records stored",
+      3: "wave 0 done (catalog table)", 4: "wave 3 done (catalog table)"}
+ok = (pc[:, [0, 1, 2, 3, 4]] > 0).all(axis=1)
+res["prep"] = {"workgroups": int(ok.sum()),
+               "mean_cycles_from_entry": {v: float((pc[ok, k] - pc[ok, 0]).mean()) for k, v in pm.items()},
+               "max_cycles_from_entry": {v: float((pc[ok, k] - pc[ok, 0]).max()) for k, v in pm.items()},
+               "entry_spread_cycles": float(pc[ok, 0].max() - pc[ok, 0].min())}
 print(json.dumps(res, indent=1))
 cat.close()

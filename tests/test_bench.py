@@ -88,3 +88,34 @@ def test_kernel_build_id_tracks_sources():
     assert len(a) == 16 and a == _lib.kernel_build_id()
     for name in _lib.KERNEL_SOURCES:
         assert os.path.exists(os.path.join(_lib.CSRC, name)), name
+
+
+def test_dropin_rate_takes_the_process_start_out(tmp_path):
+    """bench.dropin_rate runs every leg at two lengths and reports the sampler's
+    rate (niter - short) / (wall(niter) - wall(short)), the start-up and the
+    wall rate beside it.  Stand-in programs here: 0.2 s of start-up plus
+    0.1 ms per iteration (10 000 iterations/s), the drop-in one writing the
+    HBMI_DROPIN_STATS file like libhbmi."""
+    sys.path.insert(0, ROOT)
+    import bench
+
+    prog = ("#!{py}\nimport json, os, sys, time\nn = int(sys.argv[1])\ntime.sleep(0.2 + 1e-4 * n)\n"
+            "p = os.environ.get('HBMI_DROPIN_STATS')\n"
+            "if p:\n    json.dump({{'calls': 100 * n, 'memo_hits': 50 * n, 'batches': 6 * n, 'walkers': 50 * n,"
+            " 'max_batch': 24, 'contexts_created': 1, 'profile_mode': False, 's_combine': 0.0, 's_upload': 0.0,"
+            " 's_launch': 0.0, 's_download_sync': 0.0, 's_wake': 0.0, 'waiters': 40 * n}}, open(p, 'w'))\n")
+    for name in ("hb_mcmc_ref_hbmi", "hb_mcmc_ref"):
+        f = tmp_path / name
+        f.write_text(prog.format(py=sys.executable))
+        f.chmod(0o755)
+    legs = (("dropin", "hb_mcmc_ref_hbmi", {}), ("reference_cpu", "hb_mcmc_ref", {}))
+    out = bench.dropin_rate(1000, legs=legs, ref_dir=str(tmp_path))
+    assert out["niter"] == 1000 and out["niter_short"] == 100
+    for key in ("dropin", "reference_cpu"):
+        leg = out[key]
+        assert 7000 < leg["iters_per_s"] < 12000, leg
+        assert 0.1 < leg["startup_s"] < 0.4, leg
+        assert leg["iters_per_s_wall"] < 0.5 * leg["iters_per_s"], leg
+    st = out["dropin"]["stats"]
+    assert st["batches_per_iter"] == 6 and st["memo_hit_frac"] == 0.5 and "waiters" in st
+    assert 0.5 < out["speedup_vs_reference_cpu"] < 2.0
