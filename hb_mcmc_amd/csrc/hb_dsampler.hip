@@ -470,14 +470,61 @@ struct SwapPrev {
 __host__ __device__ inline size_t swap_prev_wave_bytes(int cone, int maxent) {
   return (((size_t)cone * (2 * sizeof(double) + sizeof(int)) + 15) & ~(size_t)15) + sizeof(SwapEnt) * (size_t)maxent;
 }
+// The replay's global loads, issued before ds_propose's table-staging barrier
+// so that their two dependent rounds (the segment's level offsets, then its
+// attempts) overlap the tables, the slot state and the barrier instead of
+// starting after them: the cone's first 64 slots (chain, hs, logL) and the
+// offsets (replay_load_cone, right after the slot is known), then the first
+// kRpEnts x 64 attempts (replay_load_ents, just before the barrier).
+constexpr int kRpEnts = 4;
+struct ReplayLoads {
+  int g, so, c;   // segment; lane <= nlv: level lane's first attempt; lane < Wc: the cone slot's chain
+  double h, L;    // lane < Wc: the slot's inverse-temperature difference and logL
+  int eb, eend;   // the segment's attempts [eb, eend)
+  int eb_[kRpEnts];     // attempts eb + lane + 64 r: b and ln(beta) (scalars, not a SwapEnt
+  double el_[kRpEnts];  // array: that one went to scratch)
+};
+__device__ __forceinline__ void replay_load_cone(const Dev& D, const SwapPrev& SP, int W, int j, int lane,
+                                                 ReplayLoads& R) {
+  const int nlv = SP.nlv;
+  R.g = seg_of(j - D.lo, D.nl, SP.G);
+  const int clo = max(0, j - nlv), Wc = min(W, j + nlv + 1) - clo;
+  R.so = lane <= nlv ? SP.soff[R.g * nlv + lane] : 0;
+  R.c = 0;
+  R.h = R.L = 0.0;
+  if (lane < Wc) {
+    R.c = D.idx[clo + lane];
+    R.h = D.hs[clo + lane];
+    R.L = SP.Ls != nullptr ? SP.Ls[clo + lane] : D.logL[R.c];
+  }
+}
+__device__ __forceinline__ void replay_load_ents(const SwapPrev& SP, int lane, ReplayLoads& R) {
+  const int nlv = SP.nlv;
+  R.eb = __builtin_amdgcn_readfirstlane(R.so);
+  R.eend = nlv < 64 ? __builtin_amdgcn_readlane(R.so, nlv) : SP.soff[R.g * nlv + nlv];
+  const int ne = R.eend - R.eb;
+#pragma unroll
+  for (int r = 0; r < kRpEnts; ++r) {
+    const int q = lane + 64 * r;
+    int b = 0;
+    double l = 0.0;
+    if (q < ne) {
+      const SwapEnt x = SP.ent[R.eb + q];
+      b = x.b;
+      l = x.lnb;
+    }
+    R.eb_[r] = b;
+    R.el_[r] = l;
+  }
+}
 // returns the chain in slot j after the previous iteration's swaps; nacc: the
-// accepted attempts with b = j (wave-uniform)
+// accepted attempts with b = j (wave-uniform); R: the loads issued ahead
+// (replay_load_cone / replay_load_ents)
 __device__ __forceinline__ int replay_prev_swaps(const Dev& D, const SwapPrev& SP, int W, int j, int lane,
                                                  const hbglibc::Tabs& T, unsigned char* scr, int& nacc,
-                                                 unsigned long long* rp = nullptr) {
+                                                 const ReplayLoads& R, unsigned long long* rp = nullptr) {
   if (rp) rp[0] = __builtin_amdgcn_s_memtime();
   const int nlv = SP.nlv;
-  const int g = seg_of(j - D.lo, D.nl, SP.G);
   const int clo = max(0, j - nlv), chi = min(W, j + nlv + 1), Wc = chi - clo;
   double* cL = reinterpret_cast<double*>(scr);
   double* cH = cL + SP.cone;
@@ -485,18 +532,28 @@ __device__ __forceinline__ int replay_prev_swaps(const Dev& D, const SwapPrev& S
   SwapEnt* sE = reinterpret_cast<SwapEnt*>(scr + (((size_t)SP.cone * (2 * sizeof(double) + sizeof(int)) + 15) &
                                                   ~(size_t)15));
   // the segment's level offsets (nlv + 1 <= 65 of them: lane l holds level l's
-  // start, lane 64 the end read apart), then its attempts and the cone's slots
-  const int so = lane <= nlv ? SP.soff[g * nlv + lane] : 0;
-  for (int i = lane; i < Wc; i += 64) {  // issued beside the offsets' load (independent of it)
+  // start, lane 64 the end read apart), its attempts and the cone's slots
+  const int so = R.so;
+  if (lane < Wc) {
+    cC[lane] = R.c;
+    cH[lane] = R.h;
+    cL[lane] = R.L;
+  }
+  for (int i = lane + 64; i < Wc; i += 64) {  // cones wider than a wave (nlv >= 32)
     const int c = D.idx[clo + i];
     cC[i] = c;
     cH[i] = D.hs[clo + i];
     cL[i] = SP.Ls != nullptr ? SP.Ls[clo + i] : D.logL[c];
   }
-  const int eb = __builtin_amdgcn_readfirstlane(so);
-  const int eend = nlv < 64 ? __builtin_amdgcn_readlane(so, nlv) : SP.soff[g * nlv + nlv];
+  const int eb = R.eb, eend = R.eend;
   const int ne = eend - eb;
-  for (int q = lane; q < ne; q += 64) sE[q] = SP.ent[eb + q];
+#pragma unroll
+  for (int r = 0; r < kRpEnts; ++r)
+    if (lane + 64 * r < ne) {
+      sE[lane + 64 * r].b = R.eb_[r];
+      sE[lane + 64 * r].lnb = R.el_[r];
+    }
+  for (int q = lane + 64 * kRpEnts; q < ne; q += 64) sE[q] = SP.ent[eb + q];
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -575,6 +632,9 @@ __device__ __forceinline__ void propose_group(const Dev& D, int W, int NPAST, lo
   const int j = act ? D.order[k] : D.lo;  // global slot
   const int jl = j - D.lo;                // local slot (arrays by slot)
   double* gs = Ls.gs[wv];
+  ReplayLoads rl;
+  if constexpr (SWAP)
+    if (act) replay_load_cone(D, SP, W, j, lane, rl);
   j_out = j;
   act_out = act;
   const double pc_tab = PREP ? *D.tab_pc : 0.0;
@@ -601,14 +661,18 @@ __device__ __forceinline__ void propose_group(const Dev& D, int W, int NPAST, lo
 #define DS_PRINT()
 #endif
   DS_T(0);
-  int chain = SWAP ? 0 : D.idx[j];
-  bool needx = SWAP ? false : !D.logP_ok[chain];
-  double xn = (!SWAP && lane < kNp) ? D.x[(size_t)chain * kNp + lane] : 0.0;
+  // SWAP: the chain in slot j before the previous iteration's swaps, its
+  // state loaded ahead and kept when no accepted swap moved it (the replay)
+  int chain = D.idx[j];
+  bool needx = !D.logP_ok[chain];
+  double xn = lane < kNp ? D.x[(size_t)chain * kNp + lane] : 0.0;
   const double temp = D.temp[j];
   int iset = D.iset[jl];
   double gset = D.gset[jl];
   WaveStream S;
   S.init(D.idum[jl], D.idum2[jl], D.iy[jl], lane < NTAB ? D.iv[(size_t)jl * NTAB + lane] : 0);
+  if constexpr (SWAP)
+    if (act) replay_load_ents(SP, lane, rl);
   __syncthreads();  // tables staged
   if (sgt < n8) sch_dst[sgt] = sv;
   for (long long q = sgt + sgs; q < n8; q += sgs)
@@ -621,16 +685,19 @@ __device__ __forceinline__ void propose_group(const Dev& D, int W, int NPAST, lo
 #else
       unsigned long long* rpp = nullptr;
 #endif
-      chain = replay_prev_swaps(D, SP, W, j, lane, T, scr + (size_t)wv * swap_prev_wave_bytes(SP.cone, SP.maxent),
-                                nacc, rpp);
+      const int c1 = replay_prev_swaps(D, SP, W, j, lane, T,
+                                       scr + (size_t)wv * swap_prev_wave_bytes(SP.cone, SP.maxent), nacc, rl, rpp);
       if (lane == 0) {
-        SP.idx_out[j] = chain;
+        SP.idx_out[j] = c1;
         if (nacc) D.nsw[jl] += nacc;  // this slot's own counter: no contention
         if (SP.iter % 100 == 0) D.DEacc_arr[jl] = D.DEtrial_arr[jl] = 0;  // ds_swap_seg's 100-step reset
-        if (j == 0) swap_tail(D, SP.iter, D.par ^ 1, chain);  // slot 0 (one-process samplers own every slot)
+        if (j == 0) swap_tail(D, SP.iter, D.par ^ 1, c1);  // slot 0 (one-process samplers own every slot)
       }
-      needx = !D.logP_ok[chain];
-      xn = lane < kNp ? D.x[(size_t)chain * kNp + lane] : 0.0;
+      if (c1 != chain) {  // wave-uniform
+        chain = c1;
+        needx = !D.logP_ok[chain];
+        xn = lane < kNp ? D.x[(size_t)chain * kNp + lane] : 0.0;
+      }
     }
   }
   if (act) {  // wave-uniform; every wave reaches the prep group's barriers below
@@ -663,7 +730,9 @@ __device__ __forceinline__ void propose_group(const Dev& D, int W, int NPAST, lo
       ia = (int)S.uniform();
       int ib = ia;
       while (ib == ia) ib = (int)(S.uniform() * NPAST);
-      const double g0 = gauss_pdf(0, 0, 1.e-4, T) - 0.5;
+      // gaussian(c = 0, 0, 1e-4) - 0.5 (:1115): pow(0, 2) = 0 and exp(-0) = 1
+      // exactly, so gauss_pdf's value is its constant factor, folded here
+      const double g0 = (1 / 1.e-4 / kSqrt2Pi) * 1.0 - 0.5;
       const bool scaled = S.uniform() < 0.9;
       const double gamma = 2.388 / sqrt(2. * kNp);  // GAMMA, mcmc_wrapper2.h:13
       const double gd = scaled ? gauss_batch(S, iset, gset, T, gs) : 0.0;
@@ -708,14 +777,22 @@ __device__ __forceinline__ void propose_group(const Dev& D, int W, int NPAST, lo
     if (lane == 1 && y1 > y0) yn = y0;
     if (lane == 2) yn = P->log_lc_period;
     if (lane == 6) yn = fmod(yn, P->LC_PERIOD);
+    // the e-bin slot (the eval order, hbds::eval_slot_by_e): e is final here,
+    // so the returning atomic's latency overlaps the prior terms
+    int ebin = 0, eslot = 0;
+    if (lane == 3 && D.ecnt != nullptr) {
+      ebin = e_bin_desc(yn);
+      eslot = atomicAdd(&D.ecnt[ebin * kEbinStride], 1);
+    }
     DS_T(5);
     // prior terms (:444, :477), summed per slot in the reference's order
     const bool prior = lane < kNp && P->gpflag[lane] == 1;
     const double ty = (prior && !lost) ? prior_term(lane, yn, T) : 0.0;
     const double tx = (needx && prior) ? prior_term(lane, xn, T) : 0.0;
     double lpy = 0., lpx = 0.;
+    const uint64_t pmask = __ballot(prior);  // the flags as one mask: no scalar load per term
     for (int i = 0; i < kNp; ++i) {
-      if (P->gpflag[i] != 1) continue;
+      if (!((pmask >> i) & 1u)) continue;
       lpy += rld(ty, i);
       if (needx) lpx += rld(tx, i);
     }
@@ -729,10 +806,7 @@ __device__ __forceinline__ void propose_group(const Dev& D, int W, int NPAST, lo
       D.y[(size_t)jl * kNp + lane] = yn;
       if (PREP) PL.sp[wv * hbk::kNpars + lane] = yn;
     }
-    if (lane == 3 && D.ecnt != nullptr) {  // the eval order (hbds::eval_slot_by_e)
-      const int b = e_bin_desc(yn);
-      D.elist[(size_t)b * D.nl + atomicAdd(&D.ecnt[b * kEbinStride], 1)] = jl;
-    }
+    if (lane == 3 && D.ecnt != nullptr) D.elist[(size_t)ebin * D.nl + eslot] = jl;
     if (lane < NTAB) D.iv[(size_t)jl * NTAB + lane] = S.b_tab;
     if (lane == 0) {
       jl_s[wv] = jl;
