@@ -610,7 +610,24 @@ def roofline(config, kernel_ms, evals_per_call, hbm_bytes_per_call, extra):
     return out
 
 
-def settle_clock(step, ms, drain=None):
+def settle_agreement(a, dev, world):
+    """For world > 1: a function that turns this rank's "settled" into the
+    group's (every rank settled), so that every rank runs the same number of
+    settle chunks -- the steps hold a collective (the logL all-gather), and a
+    rank that ran one chunk more than another would leave its all-gathers
+    unmatched (the group then hangs at the next barrier)."""
+    if world <= 1:
+        return None
+    flag = torch.zeros(1, dtype=torch.int32, device=dev if a.backend == "nccl" else "cpu")
+
+    def agree(done):
+        flag.fill_(0 if done else 1)
+        dist.all_reduce(flag, op=dist.ReduceOp.MAX)
+        return int(flag.item()) == 0
+    return agree
+
+
+def settle_clock(step, ms, drain=None, agree=None):
     """Back-to-back steps for `ms` milliseconds before the warmup steps: the
     shader clock ramps up over the first milliseconds of sustained work
     (MI355X_MICROARCH.md, DVFS item 6: measure after back-to-back launches),
@@ -630,7 +647,10 @@ def settle_clock(step, ms, drain=None):
         if drain is not None:
             drain()
         torch.cuda.synchronize()
-        if (time.perf_counter() - t0) * 1e3 >= ms:
+        done = (time.perf_counter() - t0) * 1e3 >= ms
+        if agree is not None:
+            done = agree(done)  # the same chunk count on every rank
+        if done:
             break
     return {"ms": (time.perf_counter() - t0) * 1e3, "steps": k,
             "why": "untimed back-to-back steps before the warmup: the shader clock ramps up under sustained load"}
@@ -683,7 +703,8 @@ def run_c5(a, rank, world, local, dev, pg):
          for k in range(nb)]
     out = torch.empty(wtot, dtype=torch.float64, device=dev)
     stream = torch.cuda.current_stream()
-    settle = settle_clock(lambda k: cat.loglike_dev(P[k % nb], wpt, out, stream), a.settle_ms)
+    settle = settle_clock(lambda k: cat.loglike_dev(P[k % nb], wpt, out, stream), a.settle_ms,
+                          agree=settle_agreement(a, dev, world))
     for k in range(a.warmup):
         cat.loglike_dev(P[k % nb], wpt, out, stream)
     torch.cuda.synchronize()
@@ -819,7 +840,7 @@ def main():
                 pending[b].wait()
                 pending[b] = None
 
-    settle = settle_clock(step, a.settle_ms, drain)
+    settle = settle_clock(step, a.settle_ms, drain, settle_agreement(a, dev, world))
     for k in range(a.warmup):
         step(k)
     drain()

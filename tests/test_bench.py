@@ -119,3 +119,53 @@ def test_dropin_rate_takes_the_process_start_out(tmp_path):
     st = out["dropin"]["stats"]
     assert st["batches_per_iter"] == 6 and st["memo_hit_frac"] == 0.5 and "waiters" in st
     assert 0.5 < out["speedup_vs_reference_cpu"] < 2.0
+
+
+def _settle_rank(rank, world, port, q):
+    import time
+
+    import torch
+    import torch.distributed as dist
+
+    sys.path.insert(0, ROOT)
+    import bench
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    bench.torch.cuda.synchronize = lambda: None  # CPU stand-in: no device here
+
+    class A:
+        backend = "gloo"
+
+    t = torch.ones(4)
+
+    def step(k):  # a collective per step, like the logL all-gather; rank 1 twice as slow
+        time.sleep(0.0005 * (1 + rank))
+        dist.all_reduce(t)
+
+    s = bench.settle_clock(step, 30.0, None, bench.settle_agreement(A, None, world))
+    dist.barrier()
+    q.put((rank, s["steps"]))
+    dist.destroy_process_group()
+
+
+def test_settle_chunks_agree_across_ranks():
+    """bench.settle_clock with world > 1: the ranks run the same number of
+    settle chunks (the steps hold a collective), though one rank steps twice
+    as slowly -- a time-based count per rank would leave collectives unmatched
+    and hang the group (two gloo ranks on the CPU)."""
+    import torch.multiprocessing as mp
+
+    sys.path.insert(0, ROOT)
+    import bench
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = bench.free_port()
+    ps = [ctx.Process(target=_settle_rank, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    got = dict(q.get(timeout=120) for _ in ps)
+    for p in ps:
+        p.join(timeout=60)
+    assert got[0] == got[1] and got[0] % 16 == 0 and got[0] >= 16, got
