@@ -98,7 +98,13 @@ for q in sorted(set(cls.tolist()), reverse=True):
 # resident waves over the span (100 MHz ticks binned to 1 us)
 edges = np.arange(0, int((rt1.max() - k0) / 100) + 2)
 occ = [int(((rt0 - k0) / 100.0 <= e).sum() - ((rt1 - k0) / 100.0 <= e).sum()) for e in edges]
-res["resident_waves_per_us"] = occ
+res["resident_waves_per_us"] = occ  # walkers (a pair's two waves counted once)
+wt = np.where(cls == 5, 2, 1)  # wave slots held: a pair walker holds two
+res["resident_wave_slots_per_us"] = [int((wt * (((rt0 - k0) / 100.0 <= e) & ((rt1 - k0) / 100.0 > e))).sum())
+                                     for e in edges]
+res["resident_wave_slots_by_class_per_4us"] = {
+    names[q]: [int((wt * (cls == q) * (((rt0 - k0) / 100.0 <= e) & ((rt1 - k0) / 100.0 > e))).sum())
+               for e in edges[::4]] for q in sorted(set(cls.tolist()), reverse=True)}
 # the records launch (hb_prep_kernel<32>, 512 workgroups at C5): prologue marks
 # of the last call, shader cycles from each workgroup's entry
 nwg = (W + 31) // 32
