@@ -769,9 +769,20 @@ __device__ __forceinline__ void propose_group(const Dev& D, int W, int NPAST, lo
     const bool e_kept = (e_pre >= P->lim_lo[3] || (P->fl_lo[3] != 1 && P->fl_lo[3] != 2)) &&
                         (e_pre <= P->lim_hi[3] || (P->fl_hi[3] != 1 && P->fl_hi[3] != 2));  // the walls leave e alone
     const bool lost = e_pre > 1.0 && e_kept;  // profiles/r05/r05p_ds_lost_acc_ab.txt
-    // walls (:440-467), one coordinate per lane
+    // walls (:440-467), one coordinate per lane.  A slot whose proposal lands
+    // many ranges outside (the hot rungs) folds for thousands of cycles, a
+    // dependent chain that sets the launch's tail: its wave takes issue
+    // priority over the throughput-bound waves beside it for the duration
+#ifndef HB_DS_WALL_PRIO
+#define HB_DS_WALL_PRIO 1
+#endif
+    const bool wfar = HB_DS_WALL_PRIO && __ballot(lane < kNp && (!lost || lane == 3) &&
+                                                  fabs(yn - 0.5 * (P->lim_lo[lane] + P->lim_hi[lane])) >
+                                                      8.0 * (P->lim_hi[lane] - P->lim_lo[lane])) != 0;
+    if (wfar) __builtin_amdgcn_s_setprio(3);
     if (lane < kNp && (!lost || lane == 3))
       yn = hbwall::apply_wall(yn, P->lim_lo[lane], P->lim_hi[lane], P->fl_lo[lane], P->fl_hi[lane]);
+    if (wfar) __builtin_amdgcn_s_setprio(0);
     // "order the masses" (:470-475) as written: y[1] = y[0]; period fixed; T0 folded
     const double y0 = rld(yn, 0), y1 = rld(yn, 1);
     if (lane == 1 && y1 > y0) yn = y0;
