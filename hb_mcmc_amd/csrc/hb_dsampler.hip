@@ -1127,6 +1127,22 @@ __global__ void ds_math_probe(int fn, const double* x, const double* y, long n, 
          : fn == 3 ? sqrt(a) : a / b;
 }
 
+// Wall folds timed per wave, for diagnosis (scripts/wall_probe.py): lane i
+// folds v[i] into [lo[i], hi[i]] (both walls reflecting); cyc[w]: the shader
+// cycles wave w spent in hbwall::apply_wall.  One wave per workgroup.
+__global__ void ds_wall_probe(const double* v, const double* lo, const double* hi, long n, double* out,
+                              long long* cyc) {
+  const long i = (long)blockIdx.x * 64 + (threadIdx.x & 63);
+  const bool ok = i < n;
+  const double x = ok ? v[i] : 0.0, l = ok ? lo[i] : 0.0, h = ok ? hi[i] : 1.0;
+  long long t0, t1;
+  __asm__ volatile("s_waitcnt vmcnt(0)\n\ts_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t0) : "v"(x), "v"(l), "v"(h));
+  const double y = hbwall::apply_wall(x, l, h, 1.0, 1.0);
+  __asm__ volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t1) : "v"(y));
+  if (ok) out[i] = y;
+  if ((threadIdx.x & 63) == 0) cyc[blockIdx.x] = t1 - t0;
+}
+
 }  // namespace hbds
 
 using namespace hbds;
@@ -2143,6 +2159,34 @@ extern "C" int hb_dsampler_sync(hb_dsampler* d) {
   if (!d) return hbx_set_error("hb_dsampler_sync: null");
   if (const int rc = ds_flush(d)) return rc;
   DS_TRY(hipStreamSynchronize(d->st), "sync");
+  return 0;
+}
+
+// internal (scripts/wall_probe.py): hbwall::apply_wall on n values, one wave
+// per 64 of them, with each wave's shader cycles (cyc: ceil(n / 64) entries)
+extern "C" int hbx_wall_probe(const double* v, const double* lo, const double* hi, long n, double* out,
+                              long long* cyc) {
+  if (n <= 0) return 0;
+  const long nw = (n + 63) / 64;
+  double *dv = nullptr, *dl = nullptr, *dh = nullptr, *dout = nullptr;
+  long long* dc = nullptr;
+  const size_t bytes = sizeof(double) * (size_t)n;
+  hipError_t e = hipMalloc((void**)&dv, bytes);
+  if (e == hipSuccess) e = hipMalloc((void**)&dl, bytes);
+  if (e == hipSuccess) e = hipMalloc((void**)&dh, bytes);
+  if (e == hipSuccess) e = hipMalloc((void**)&dout, bytes);
+  if (e == hipSuccess) e = hipMalloc((void**)&dc, sizeof(long long) * (size_t)nw);
+  if (e == hipSuccess) e = hipMemcpy(dv, v, bytes, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(dl, lo, bytes, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(dh, hi, bytes, hipMemcpyHostToDevice);
+  if (e == hipSuccess) {
+    ds_wall_probe<<<(unsigned)nw, 64>>>(dv, dl, dh, n, dout, dc);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) e = hipMemcpy(out, dout, bytes, hipMemcpyDeviceToHost);
+  if (e == hipSuccess) e = hipMemcpy(cyc, dc, sizeof(long long) * (size_t)nw, hipMemcpyDeviceToHost);
+  for (void* p : {(void*)dv, (void*)dl, (void*)dh, (void*)dout, (void*)dc}) (void)hipFree(p);
+  DS_TRY(e, "hbx_wall_probe");
   return 0;
 }
 

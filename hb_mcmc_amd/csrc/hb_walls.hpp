@@ -74,7 +74,7 @@ HBW_FN double ff_double_folds(double v, double lo, double hi, int folds_left, in
   // the end (no early exits: on a GPU lane the tests would serialise into
   // exec-mask branches); garbage from a failed test is discarded
   const double av = fabs(v);
-  const bool finite = av < 0x1p1000 && av > 0.0;
+  const bool finite = (av < 0x1p1000) & (av > 0.0);
   int e;
   frexp(av, &e);                       // av = f 2^e, f in [0.5, 1): binade [2^(e-1), 2^e)
   const int eb = finite ? e - 1 : 0;   // av in [2^eb, 2^(eb+1))
@@ -83,21 +83,22 @@ HBW_FN double ff_double_folds(double v, double lo, double hi, int folds_left, in
   const bool far = bottom > 2.0 * lim;
   const double scale = ldexp(1.0, 52 - eb);  // 1/g
   const double clo = 2.0 * lo * scale, chi = 2.0 * hi * scale;  // exact (power-of-2 scaling), |.| < 2^52
-  const bool tie = clo - floor(clo) == 0.5 || chi - floor(chi) == 0.5;  // rounding ties: no translation
+  const bool tie_lo = clo - floor(clo) == 0.5, tie_hi = chi - floor(chi) == 0.5;
+  const bool tie = tie_lo | tie_hi;  // rounding ties: no translation
   const double rlo = rint(clo), rhi = rint(chi);
   const double D = rhi - rlo;                  // exact integer
   const double K = av * scale;                 // exact integer in [2^52, 2^53)
   const double c1 = v < 0.0 ? rlo : -rhi;
-  const bool fits = D > 0.0 && K + (c1 > 0.0 ? c1 : 0.0) <= 0x1p53 - 2.0;
+  const bool fits = (D > 0.0) & (K + (c1 > 0.0 ? c1 : 0.0) <= 0x1p53 - 2.0);
   // m pairs: K - (m-1) D + c1 >= 2^52 + 1 and K - m D >= 2^52 + 1
   const double n1 = K - 0x1p52 - 1.0, n2 = K + c1 - 0x1p52 - 1.0;
-  const bool room = n1 >= D && n2 >= 0.0;
+  const bool room = (n1 >= D) & (n2 >= 0.0);
   double m = floor_div(n1, D);
   const double m2 = floor_div(n2, D) + 1.0;
   if (m2 < m) m = m2;
   const double cap = (double)(folds_left / 2);
   if (m > cap) m = cap;
-  const bool go = finite && far && !tie && fits && room && m >= 1.0;
+  const bool go = finite & far & !tie & fits & room & (m >= 1.0);
   mode = go ? kFfDone
             : !finite ? kFfTop : !far ? kFfNear : tie ? kFfTie : !fits ? kFfTop : !room ? kFfBinade : kFfTop;
   m_out = go ? (int)m : 0;
@@ -154,7 +155,11 @@ HBW_FN double apply_wall(double v, double lo, double hi, double fl, double fh) {
   if (fl == 1 && fh == 1) {
     const double lim2 = 2.0 * (fabs(lo) > fabs(hi) ? fabs(lo) : fabs(hi));
     const double lo2 = 2.0 * lo, hi2 = 2.0 * hi;  // exact
-    while (guard < kGuard && (v < lo || v > hi)) {
+    // conditions combined with bitwise & / | (not && / ||): on a GPU lane each
+    // short-circuit became its own exec-mask branch, ≈ 500 shader cycles per
+    // trip of the fold loop below against ≈ 80 with one exit per trip
+    // (scripts/wall_probe.py); the values and the fold count are the same
+    while ((guard < kGuard) & ((v < lo) | (v > hi))) {
       int m, mode;
       double bottom;
       v = ff_double_folds(v, lo, hi, kGuard - guard, m, mode, bottom);
@@ -178,26 +183,28 @@ HBW_FN double apply_wall(double v, double lo, double hi, double fl, double fh) {
       // short runs measured 0.8 us per iteration slower): the second is taken under the
       // same test, so the sequence and the count are unchanged, and a GPU
       // lane pays one exec-mask branch per two dependent folds
-      for (int s = 0;;) {
-        if (!(guard < kGuard && (v < lo || v > hi) && (s < 4 || (s < smax && fabs(v) > stop)))) break;
+      int s = 0;
+      bool go = (guard < kGuard) & ((v < lo) | (v > hi)) & ((s < 4) | ((s < smax) & (fabs(v) > stop)));
+      while (go) {
         const double v1 = (v < lo ? lo2 : hi2) - v;
-        const bool two = guard + 1 < kGuard && (v1 < lo || v1 > hi) && (s + 1 < 4 || (s + 1 < smax && fabs(v1) > stop));
+        const bool two = (guard + 1 < kGuard) & ((v1 < lo) | (v1 > hi)) &
+                         ((s + 1 < 4) | ((s + 1 < smax) & (fabs(v1) > stop)));
         v = two ? (v1 < lo ? lo2 : hi2) - v1 : v1;
         s += two ? 2 : 1;
         guard += two ? 2 : 1;
-        if (!two) break;
+        go = two & (guard < kGuard) & ((v < lo) | (v > hi)) & ((s < 4) | ((s < smax) & (fabs(v) > stop)));
       }
     }
   } else {
     for (; guard < kGuard; ++guard) {
-      const bool below = (fl == 1) && (v < lo);
-      const bool above = (fh == 1) && (v > hi);
-      if (!(below || above)) break;
+      const bool below = (fl == 1) & (v < lo);
+      const bool above = (fh == 1) & (v > hi);
+      if (!(below | above)) break;
       v = (v < lo) ? 2.0 * lo - v : 2.0 * hi - v;
     }
   }
-  for (int g = 0; (fl == 2) && (v < lo) && g < kGuard; ++g) v = hi + (v - lo);
-  for (int g = 0; (fh == 2) && (v > hi) && g < kGuard; ++g) v = lo + (v - hi);
+  for (int g = 0; (fl == 2) & (v < lo) & (g < kGuard); ++g) v = hi + (v - lo);
+  for (int g = 0; (fh == 2) & (v > hi) & (g < kGuard); ++g) v = lo + (v - hi);
   return v;
 }
 
