@@ -114,3 +114,38 @@ def test_tie_binades_within_reach():
     v = np.where(rng.integers(0, 2, n) == 1, hi + dist, lo - dist)
     out = check(v, lo, hi, np.ones(n), np.ones(n))
     assert np.all((out >= lo) & (out <= hi))
+
+
+@pytest.mark.gpu
+def test_device_walls_equal_plain_loop():
+    """The device compile of hb_walls.hpp (hbx_wall_probe: ds_propose's
+    apply_wall, one value per lane) against the host's plain loop, bit for bit,
+    on the set_limits ranges with hot-chain excursions up to 10^5 ranges and
+    on grid-tie ranges."""
+    import sys
+    sys.path.insert(0, ROOT)
+    from hb_mcmc_amd import _lib
+
+    lib = _lib.lib()
+    f = lib.hbx_wall_probe
+    f.argtypes = [pd, pd, pd, C.c_long, pd, C.POINTER(C.c_longlong)]
+    f.restype = C.c_int
+    rng = np.random.default_rng(7)
+    n = 64 * 400
+    k = rng.integers(0, len(LIMITS), n)
+    lo = np.array([LIMITS[i][0] for i in k])
+    hi = np.array([LIMITS[i][1] for i in k])
+    # a quarter on grid-tie ranges (dyadic walls)
+    t = rng.random(n) < 0.25
+    lo[t] = np.ldexp(rng.integers(-8, 8, t.sum()), rng.integers(-3, 3, t.sum())).astype(float)
+    hi[t] = lo[t] + np.ldexp(1.0, rng.integers(-4, 3, t.sum()))
+    dist = (hi - lo) * 10 ** rng.uniform(-3, 5, n)
+    v = np.where(rng.integers(0, 2, n) == 1, hi + dist, lo - dist)
+    out = np.empty(n)
+    cyc = np.empty((n + 63) // 64, dtype=np.int64)
+    assert f(v.ctypes.data_as(pd), lo.ctypes.data_as(pd), hi.ctypes.data_as(pd), n, out.ctypes.data_as(pd),
+             cyc.ctypes.data_as(C.POINTER(C.c_longlong))) == 0, _lib.last_error()
+    ref = run(1, v, lo, hi, np.ones(n), np.ones(n))
+    bad = out.view(np.int64) != ref.view(np.int64)
+    assert not bad.any(), f"{bad.sum()} differ, first v={v[bad][0]!r} lo={lo[bad][0]!r} hi={hi[bad][0]!r}"
+    assert np.all((out >= lo) & (out <= hi))
