@@ -272,9 +272,19 @@ def sampler_e2e(L, w, iters, warm=20):
                 D.step(it)
             D.sync()
             runs.append(time.perf_counter() - t0)
+        try:  # since creation: warm-up and the three runs (diagnostic only)
+            ht = D.host_times()
+        except Exception:  # noqa: BLE001 -- a library without the timers
+            ht = None
     dt = sorted(runs)[reps // 2]
+    nit = dwarm + reps * iters
     out["device_loop"] = {"ms_per_iter": dt / iters * 1e3, "value": w * iters / dt,
-                          "runs_ms_per_iter": [x / iters * 1e3 for x in runs]}
+                          "runs_ms_per_iter": [x / iters * 1e3 for x in runs],
+                          # host side per iteration: the producer threads' schedule building (summed over
+                          # threads), the issuing thread's waits for a schedule, and its kernel issue
+                          "host_us_per_iter": None if ht is None else {
+                              "sched_build": ht["sched_build"] / nit * 1e6, "sched_wait": ht["sched_wait"] / nit * 1e6,
+                              "issue": ht["issue"] / nit * 1e6, "producer_threads": ht["threads"]}}
     S.close()
     S = SlotSampler(warm + iters, w, logp, 0, w, run=0, npast=500, ladder=1, nthreads=16)
     x, _, _ = S.get()
