@@ -1603,7 +1603,12 @@ static hb_dsampler* ds_create(hb_sampler* s, hb_ctx* ctx, const int* chain_of_sl
   // schedule producers: the swap stream as it stands now is iteration 0's start
   if (hbx_swap_rng_window(s, d->base_w)) return fail("swap stream", hipErrorInvalidValue);
   const char* nt = getenv("HB_DS_SCHED_THREADS");
-  d->nthreads = nt ? std::max(1, atoi(nt)) : (W <= 8192 ? 2 : 4);
+  // 4 producers: with 2 (the default until round 6) one schedule took about
+  // as long as one GPU iteration (154 us of building per iteration over both
+  // threads at W = 4096, bench.py device_loop.host_us_per_iter), so a slower
+  // host stalled the loop; 8 brought one 0.118-ms run on the box's 16-core
+  // share (profiles/r06/r06zn_ds_threads_ab.txt, r06zo_ds_threads_ab.txt)
+  d->nthreads = nt ? std::max(1, atoi(nt)) : 4;
   for (int i = 0; i < d->nthreads; ++i) d->workers.emplace_back(sched_worker, d);
   return d;
 }
